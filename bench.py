@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Headline benchmark: routed message->peer pairs per second, one tick = one route launch.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1] = SURVEY.md §8(d) C2): 1 world, 100k peers each subscribed
+to a 3x3x3 cube neighbourhood (2.7M subscriptions), 1M LocalMessages per tick, positions
+U[-512,512)^3, cube_size 16, ExceptSelf, synthetic (splitmix64). The table is built once
+(AreaSubscribe ops through the GPU build path; its time is reported separately); every step is
+one full tick of the hot path on HBM-resident inputs: quantise -> probe -> filter -> compact into
+CSR offsets + (msg, peer) pairs, the launch that also resolves the tick's global output offsets.
+
+Multi-GPU: world-sharded weak scaling — every rank owns its own world (its own 100k peers and
+1M messages per tick); the path has no data exchange, so there is no collective in the timed
+region. value = pairs of all ranks / max-over-ranks time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HBM3E peak BW)
+METRIC = "routed msg→peer pairs/sec per tick at 1/2/4/8 GPUs; % HBM roofline"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--scale", type=float, default=1.0, help="shrink C2 (tests only; 1.0 = the headline)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline's routing work")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "r01_pmc_route.json"))
+    return ap.parse_args()
+
+
+def algorithmic_bytes(M: int, F: int, P: int) -> int:
+    """B = M*(24 pos + 4 world + 4 sender + 1 repl) + M*32 bucket record
+    + F*4 candidate ids + P*8 (u32 msg, u32 peer) + (M+1)*4 CSR offsets."""
+    return 69 * M + 4 * F + 8 * P + 4
+
+
+def cpu_baseline(w, seconds: float) -> dict:
+    """The C restatement (oracle/wq_oracle.c: hash map world -> cube -> peer set, one message at
+    a time), single thread, on a bounded sample of the same tick."""
+    from oracle import oracle as orc
+    o = orc.COracle(w.cube_size)
+    t0 = time.perf_counter()
+    o.apply_ops(w.ops)
+    build_s = time.perf_counter() - t0
+    M = len(w.world)
+    chunk = min(M, 100_000)
+    pairs, msgs, t_route, start = 0, 0, 0.0, 0
+    while t_route < seconds and msgs < M:
+        sl = slice(start, start + chunk)
+        t0 = time.perf_counter()
+        offs, peers, _ = o.route(w.pos[sl], w.world[sl], w.sender[sl], w.repl[sl])
+        t_route += time.perf_counter() - t0
+        pairs += len(peers)
+        msgs += len(w.world[sl])
+        start += chunk
+    return {"value": pairs / t_route, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"{msgs} of the tick's {M} messages ({pairs} pairs) routed in {t_route:.2f} s by "
+                      f"oracle/wq_oracle.c on 1 host thread; table of {len(w.ops)} subscriptions built "
+                      f"in {build_s:.2f} s (not timed)"}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    from worldql_server_amd import abi, synth
+    from worldql_server_amd.router import Router
+
+    w = synth.config_c2(scale=a.scale, world_offset=rank)
+    M = len(w.world)
+    r = Router(w.cube_size, local_rank)
+    stream = torch.cuda.Stream(device=dev)  # a real stream object: its handle is never the NULL stream
+    r.set_stream(stream.cuda_stream)
+    t0 = time.perf_counter()
+    r.apply_ops(w.ops)
+    build_s = time.perf_counter() - t0
+    st = r.stats()
+
+    pos = torch.from_numpy(w.pos).to(dev)
+    world = torch.from_numpy(w.world.view(np.int32)).to(dev)
+    sender = torch.from_numpy(w.sender.view(np.int32)).to(dev)
+    repl = torch.from_numpy(w.repl).to(dev)
+    offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)  # uploads ran on the default stream
+
+    def counters():
+        torch.cuda.synchronize(dev)
+        return cnt.cpu().numpy().view(abi.COUNTERS_DTYPE)[0]
+
+    # sizing tick (capacity 0: counts only), then exact-size outputs
+    r.route_device(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
+                   0, 0, 0, cnt.data_ptr())
+    P = int(counters()["n_pairs"])
+    cap = P + 1024
+    peers = torch.empty(cap, dtype=torch.int32, device=dev)
+    msgs = torch.empty(cap, dtype=torch.int32, device=dev)
+    args = (pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
+            peers.data_ptr(), msgs.data_ptr(), cap)
+
+    def tick(c=0):
+        r.route_device(*args, c)
+
+    for _ in range(a.warmup):
+        tick()
+    tick(cnt.data_ptr())
+    c = counters()
+    P, F = int(c["n_pairs"]), int(c["n_candidates"])
+    assert c["overflow"] == 0 and c["error"] == 0, c
+
+    if world_size > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_wall = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(a.steps):
+        tick()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    t_wall = time.perf_counter() - t_wall
+    if world_size > 1:
+        dist.barrier()
+    t_ms = ev0.elapsed_time(ev1)
+    t_max = torch.tensor([t_ms], dtype=torch.float64, device=dev)
+    p_all = torch.tensor([float(P)], dtype=torch.float64, device=dev)
+    if world_size > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        dist.all_reduce(p_all, op=dist.ReduceOp.SUM)
+    t_max_ms = float(t_max.item())
+    pairs_all = float(p_all.item())
+
+    # kernel-only time of the route launch: HIP events recorded on the launch stream around
+    # every route kernel (wq_profile_enable), separate pass so the headline loop is untouched
+    r.profile_enable(True)
+    for _ in range(a.steps):
+        tick()
+    k_ms, launches = r.profile_read()
+    r.profile_enable(False)
+    k_avg_s = k_ms / launches / 1e3
+    B = algorithmic_bytes(M, F, P)
+    achieved = B / k_avg_s / 1e9
+    traffic = None
+    if os.path.exists(a.pmc_file):
+        with open(a.pmc_file) as f:
+            pmc = json.load(f)
+        if pmc.get("messages_per_tick") == M and pmc.get("pairs_per_tick") == P:
+            traffic = pmc.get("hbm_bytes_per_launch")
+
+    out = {
+        "metric": METRIC,
+        "value": pairs_all * a.steps / (t_max_ms / 1e3),
+        "unit": "pairs/s",
+        "n_gpus": world_size,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": t_max_ms / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (splitmix64, SURVEY.md §8(d) C2 generator)",
+        "config": {
+            "workload": "C2: 1 world/GPU, 100k peers x 3x3x3 cubes, 1M LocalMessages/tick, U[-512,512)^3, "
+                        "cube_size 16, ExceptSelf" + ("" if a.scale == 1.0 else f" (scaled {a.scale})"),
+            "messages_per_tick": M, "peers": w.n_peers, "subscriptions": int(st["n_entries"]),
+            "cubes": int(st["n_cubes"]), "pairs_per_tick": P, "candidates_per_tick": F,
+            "parallelism": f"world-sharded x{world_size}", "table_build_s": round(build_s, 3),
+        },
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "route_kernel", "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
+    }
+    if rank == 0 and world_size == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(w, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    r.close()
+    if world_size > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

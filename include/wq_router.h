@@ -1,0 +1,156 @@
+/*
+ * wq_router.h — C ABI of the MI355X-native WorldQL spatial message-routing path.
+ *
+ * This is the drop-in boundary for the reference server's subscription table
+ * (worldql_server/src/subscriptions/{world_map,area_map,cube_area}.rs) and the
+ * LocalMessage / AreaSubscribe / AreaUnsubscribe handlers that drive it
+ * (worldql_server/src/processing/{local_message,area_subscribe,area_unsubscribe}.rs).
+ * The reference has no FFI for this path (it is plain Rust methods);
+ * each entry point below names the Rust method(s) it replaces, and INTEGRATION.md shows
+ * the `extern "C"` block a `worldql_gpu` crate would declare to bind them.
+ *
+ * Conventions
+ *   - plain pointers and sizes only; every function returns an int status (WQ_OK = 0,
+ *     negative WQ_E_* on failure). No exception or panic crosses the ABI.
+ *   - peers are dense uint32 ids (the Rust side keeps the Uuid <-> u32 map);
+ *     worlds are dense uint32 ids interned on the host from the *sanitized* world name
+ *     (worldql_server/src/utils/world_names.rs:54-87). WQ_WORLD_INVALID is reserved.
+ *   - a handle is owned by one thread (Send, not Sync), mirroring the single owner task of
+ *     WorldMap in worldql_server/src/processing/thread.rs:113-148.
+ *   - functions without the `_device` suffix take HOST pointers and are synchronous;
+ *     `_device` variants take DEVICE pointers and are asynchronous on the handle's stream.
+ */
+#ifndef WQ_ROUTER_H
+#define WQ_ROUTER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---- */
+#define WQ_OK 0
+#define WQ_E_INVALID (-1)  /* bad argument (null handle, cube_size 0, reserved world id ...) */
+#define WQ_E_OOM (-2)      /* device allocation failed */
+#define WQ_E_HIP (-3)      /* HIP runtime error (message in wq_last_error) */
+#define WQ_E_RCCL (-4)     /* reserved for the multi-GPU exchange */
+#define WQ_E_CAPACITY (-5) /* caller's output buffer too small; required size reported */
+#define WQ_E_NODEV (-6)    /* no usable gfx950 device: the path never falls back to the CPU */
+#define WQ_E_TIMEOUT (-7)  /* a bounded in-kernel spin gave up (must never happen) */
+
+/* ---- op kinds (wq_op.kind) ---- */
+#define WQ_OP_SUBSCRIBE 0   /* AreaMap::add_subscription, area_map.rs:72-85 */
+#define WQ_OP_UNSUBSCRIBE 1 /* AreaMap::remove_subscription, area_map.rs:88-119 */
+#define WQ_OP_REMOVE_PEER 2 /* world == WQ_WORLD_INVALID: WorldMap::remove_peer (world_map.rs:41-61);
+                             otherwise that world only: AreaMap::remove_peer (area_map.rs:124-135) */
+
+/* ---- replication codes, wire values of WorldQLFB_generated.rs:176-188 ---- */
+#define WQ_REPL_EXCEPT_SELF 0    /* default; also every unknown code (replication.rs:40) */
+#define WQ_REPL_INCLUDING_SELF 1
+#define WQ_REPL_ONLY_SELF 2
+
+#define WQ_WORLD_INVALID 0xFFFFFFFFu
+
+typedef struct wq_router wq_router;
+
+/* One subscription-table op (40 bytes). key_is_raw = 1 means `key` is a CubeArea used as-is
+ * (impl ToCubeArea for CubeArea, cube_area.rs:65-70); 0 means `pos` is a Vector3 quantised
+ * by CubeArea::from_vector3 (cube_area.rs:50-56). */
+typedef struct wq_op {
+    uint32_t world;
+    uint32_t peer;
+    uint8_t kind;
+    uint8_t key_is_raw;
+    uint8_t pad_[6];
+    union {
+        double pos[3];
+        int64_t key[3];
+    } u;
+} wq_op;
+
+typedef struct wq_stats {
+    uint64_t n_entries;     /* live (world, cube, peer) subscriptions */
+    uint64_t n_cubes;       /* occupied (world, cube) buckets */
+    uint64_t n_any;         /* distinct (world, peer) pairs = sum of |subscribed_peers| */
+    uint64_t table_slots;   /* open-addressed slot count (power of two) */
+    uint64_t hash_fallbacks;/* builds that hit a 64-bit hash collision and took the exact path */
+    uint32_t cube_size;
+    int32_t device;
+} wq_stats;
+
+/* Per-call route counters written by the route kernel (device memory, see wq_route_tick_device). */
+typedef struct wq_route_counters {
+    uint64_t n_pairs;      /* P: (message, peer) pairs after the replication filter */
+    uint64_t n_candidates; /* F: peers read from the probed buckets before the filter */
+    uint32_t overflow;     /* 1 if P exceeded the caller's capacity (outputs truncated) */
+    uint32_t error;        /* non-zero if a bounded spin gave up (WQ_E_TIMEOUT) */
+} wq_route_counters;
+
+/* ---- lifetime: replaces WorldMap::new (world_map.rs:17-22) ---- */
+int wq_router_create(uint16_t cube_size, int device, wq_router** out);
+int wq_router_destroy(wq_router* h);
+const char* wq_last_error(const wq_router* h);
+/* Use the caller's HIP stream (hipStream_t as void*); NULL restores the handle's own stream. */
+int wq_set_stream(wq_router* h, void* hip_stream);
+int wq_get_stats(wq_router* h, wq_stats* out);
+
+/* ---- table mutation: AreaSubscribe / AreaUnsubscribe / disconnect ----
+ * Ops are applied in ARRAY ORDER with the reference's sequential semantics
+ * (processing/thread.rs:122-146): for each (world, cube, peer) the last op wins, and a
+ * REMOVE_PEER op removes every subscription its peer holds at that point.
+ * Replaces area_subscribe.rs:137-138 / area_unsubscribe.rs:189-190 -> AreaMap::{add,remove}_subscription
+ * and thread.rs:124-125 -> WorldMap::remove_peer. */
+int wq_apply_ops(wq_router* h, const wq_op* ops, size_t n);
+/* WorldMap::remove_peer for n peers (every world), world_map.rs:41-61. */
+int wq_remove_peers(wq_router* h, const uint32_t* peers, size_t n);
+
+/* ---- the hot path: one tick of LocalMessages ----
+ * Replaces the per-message body of handle_local_message (local_message.rs:52-86):
+ * world lookup -> Vector3::to_cube_area -> AreaMap::get_subscribed_peers -> replication filter.
+ * Validation (@global, missing position, bad world name: local_message.rs:17-50) stays on the
+ * host, before the call. Output: message-major CSR, offsets[M+1] and peers[P]; msgs[P]
+ * (nullable) repeats the message index of each pair. Pair order inside one message is
+ * ascending peer id (the reference's AHashSet order is random per process: compare sets).
+ * keys (nullable, M x 3 int64) replaces pos with raw CubeArea keys (ToCubeArea for CubeArea). */
+int wq_route_tick(wq_router* h, const double* pos, const int64_t* keys, const uint32_t* world,
+                  const uint32_t* sender, const uint8_t* repl, size_t n_msgs, uint32_t* offsets,
+                  uint32_t* peers, uint32_t* msgs, size_t capacity, size_t* n_pairs);
+/* Asynchronous form on device pointers; nothing is read back. counters (device pointer to a
+ * wq_route_counters) receives P, F and the overflow / error flags. Pairs beyond `capacity`
+ * are not written. */
+int wq_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_keys,
+                         const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
+                         size_t n_msgs, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs,
+                         size_t capacity, wq_route_counters* d_counters);
+
+/* ---- queries (the reference uses these in its unit tests, area_map.rs:33-67) ---- */
+/* AreaMap::is_peer_subscribed(uuid, cube), batched; key_or_pos is n x 3 (int64 if key_is_raw). */
+int wq_is_subscribed(wq_router* h, size_t n, const uint32_t* world, const uint32_t* peer,
+                     int key_is_raw, const void* key_or_pos, uint8_t* out);
+/* AreaMap::is_peer_subscribed_any(uuid), batched. */
+int wq_is_subscribed_any(wq_router* h, size_t n, const uint32_t* world, const uint32_t* peer,
+                         uint8_t* out);
+/* AreaMap::get_subscribed_any_peers() for one world (ascending ids). */
+int wq_world_peers(wq_router* h, uint32_t world, uint32_t* out, size_t capacity, size_t* n_out);
+
+/* ---- kernel (1) alone: CubeArea::coord_clamp over n coordinates (cube_area.rs:23-44) ---- */
+int wq_quantize(const double* coords, size_t n, uint16_t cube_size, int64_t* out);
+int wq_quantize_device(wq_router* h, const double* d_coords, size_t n, int64_t* d_out);
+
+/* ---- instrumentation ----
+ * When enabled, every route launch is bracketed by HIP events on the launch stream;
+ * wq_profile_read returns the summed kernel-only milliseconds and launch count (and resets). */
+int wq_profile_enable(wq_router* h, int enable);
+int wq_profile_read(wq_router* h, double* kernel_ms, uint64_t* launches);
+
+/* ---- test hook: keep only the low `bits` bits of the 64-bit cube hash (64 = normal).
+ * Forces bucket collisions so the exact-compare fallback paths are exercised. */
+int wq_debug_set_hash_bits(wq_router* h, int bits);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WQ_ROUTER_H */

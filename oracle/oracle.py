@@ -1,0 +1,228 @@
+"""Python restatement of the reference routing path — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may import this
+module (or the C restatement it loads), and only as the checker / timed CPU baseline. The
+product path in ``worldql_server_amd`` never imports it.
+
+Two independent restatements live here:
+
+* a numpy restatement of the quantiser (``coord_clamp_np``), following
+  worldql_server/src/subscriptions/cube_area.rs:23-44 and worldql_server/src/utils/round.rs:1-13
+  op for op (fabs, fmod == 0, divide, ceil, multiply, signed compare, Rust's saturating
+  ``as i64``, wrapping ``+`` / ``*``);
+* ``COracle``: ctypes binding of the C restatement (oracle/wq_oracle.c, built by
+  oracle/Makefile into oracle/liboracle.so) of WorldMap / AreaMap / handle_local_message.
+
+Parity pin: the reference is Rust and cannot be built here; both
+restatements are checked against the reference's own unit-test vectors in
+tests/golden/reference_kats.json, and against each other on random f64 bit patterns.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+I64_MAX = np.iinfo(np.int64).max
+I64_MIN = np.iinfo(np.int64).min
+
+
+def sat_i64_np(x: np.ndarray) -> np.ndarray:
+    """Rust ``f64 as i64``: truncate toward zero, saturate, NaN -> 0."""
+    x = np.asarray(x, dtype=np.float64)
+    out = np.zeros(x.shape, dtype=np.int64)
+    nan = np.isnan(x)
+    hi = x >= 9223372036854775808.0
+    lo = x <= -9223372036854775808.0
+    mid = ~(nan | hi | lo)
+    out[mid] = np.trunc(x[mid]).astype(np.int64)
+    out[hi] = I64_MAX
+    out[lo] = I64_MIN
+    return out
+
+
+def round_by_multiple_np(n: np.ndarray, multiple: float) -> np.ndarray:
+    """worldql_server/src/utils/round.rs:1-13 (vectorised)."""
+    n = np.asarray(n, dtype=np.float64)
+    if multiple == 0.0:
+        return n.copy()
+    with np.errstate(all="ignore"):
+        r = np.ceil(n / multiple) * multiple
+    return np.where(n == 0.0, np.float64(multiple), r)
+
+
+def coord_clamp_np(coord, size: int) -> np.ndarray:
+    """worldql_server/src/subscriptions/cube_area.rs:23-44 (vectorised, release semantics)."""
+    c = np.asarray(coord, dtype=np.float64)
+    a = np.abs(c)
+    sf = np.float64(size)
+    with np.errstate(all="ignore"):
+        is_mult = (np.fmod(a, sf) == 0.0) & (c != 0.0)
+        rounded = round_by_multiple_np(a, float(size))
+        r_i = sat_i64_np(rounded)
+        res = np.where(rounded > c, r_i, (r_i.view(np.uint64) + np.uint64(size)).view(np.int64))
+        neg = c < 0.0
+        res = np.where(neg, (np.uint64(0) - res.view(np.uint64)).view(np.int64), res)
+    return np.where(is_mult, sat_i64_np(c), res).astype(np.int64)
+
+
+def quantize_np(pos, size: int) -> np.ndarray:
+    """CubeArea::from_vector3 (cube_area.rs:50-56) over an (n, 3) array."""
+    return coord_clamp_np(np.asarray(pos, dtype=np.float64), size)
+
+
+# ------------------------------------------------------------------------------------------
+# C restatement (WorldMap / AreaMap / handle_local_message)
+# ------------------------------------------------------------------------------------------
+
+_lib = None
+
+
+def build_c_oracle() -> str:
+    """Compile oracle/wq_oracle.c (gcc) if the .so is missing or stale."""
+    src = os.path.join(HERE, "wq_oracle.c")
+    if (not os.path.exists(LIB_PATH)) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", HERE, "liboracle.so"])
+    return LIB_PATH
+
+
+def load_c_oracle():
+    global _lib
+    if _lib is not None:
+        return _lib
+    build_c_oracle()
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, u32, u16, i32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_int, ctypes.c_size_t
+    lib.wqo_round_by_multiple.argtypes = [ctypes.c_double, ctypes.c_double]
+    lib.wqo_round_by_multiple.restype = ctypes.c_double
+    lib.wqo_coord_clamp.argtypes = [ctypes.c_double, u16]
+    lib.wqo_coord_clamp.restype = ctypes.c_int64
+    lib.wqo_quantize.argtypes = [vp, sz, u16, vp]
+    lib.wqo_quantize.restype = None
+    lib.wqo_create.argtypes = [u16]
+    lib.wqo_create.restype = vp
+    lib.wqo_destroy.argtypes = [vp]
+    lib.wqo_destroy.restype = None
+    for name in ("wqo_add_subscription", "wqo_remove_subscription", "wqo_is_subscribed"):
+        f = getattr(lib, name)
+        f.argtypes = [vp, u32, u32, i32, vp]
+        f.restype = i32
+    lib.wqo_remove_peer.argtypes = [vp, u32]
+    lib.wqo_remove_peer.restype = i32
+    lib.wqo_is_subscribed_any.argtypes = [vp, u32, u32]
+    lib.wqo_is_subscribed_any.restype = i32
+    lib.wqo_world_peers.argtypes = [vp, u32, vp, sz]
+    lib.wqo_world_peers.restype = sz
+    lib.wqo_apply_ops.argtypes = [vp, vp, sz]
+    lib.wqo_apply_ops.restype = None
+    lib.wqo_route.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, sz, vp]
+    lib.wqo_route.restype = sz
+    lib.wqo_counts.argtypes = [vp, vp, vp]
+    lib.wqo_counts.restype = None
+    _lib = lib
+    return lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def c_coord_clamp(coords, size: int) -> np.ndarray:
+    lib = load_c_oracle()
+    c = np.ascontiguousarray(coords, dtype=np.float64)
+    out = np.empty(c.shape, dtype=np.int64)
+    lib.wqo_quantize(_ptr(c), c.size, size, _ptr(out))
+    return out
+
+
+class COracle:
+    """WorldMap restated in C; same op / message encodings as the C ABI (include/wq_router.h)."""
+
+    def __init__(self, cube_size: int):
+        self.lib = load_c_oracle()
+        self.cube_size = cube_size
+        self.h = self.lib.wqo_create(cube_size)
+
+    def close(self):
+        if self.h:
+            self.lib.wqo_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _key(key_is_raw, v):
+        a = np.ascontiguousarray(v, dtype=np.int64 if key_is_raw else np.float64)
+        return a, _ptr(a)
+
+    def add_subscription(self, world, peer, key_is_raw, v) -> bool:
+        a, p = self._key(key_is_raw, v)
+        return bool(self.lib.wqo_add_subscription(self.h, world, peer, int(key_is_raw), p))
+
+    def remove_subscription(self, world, peer, key_is_raw, v) -> bool:
+        a, p = self._key(key_is_raw, v)
+        return bool(self.lib.wqo_remove_subscription(self.h, world, peer, int(key_is_raw), p))
+
+    def remove_peer(self, peer) -> bool:
+        return bool(self.lib.wqo_remove_peer(self.h, peer))
+
+    def is_subscribed(self, world, peer, key_is_raw, v) -> bool:
+        a, p = self._key(key_is_raw, v)
+        return bool(self.lib.wqo_is_subscribed(self.h, world, peer, int(key_is_raw), p))
+
+    def is_subscribed_any(self, world, peer) -> bool:
+        return bool(self.lib.wqo_is_subscribed_any(self.h, world, peer))
+
+    def world_peers(self, world) -> np.ndarray:
+        n = self.lib.wqo_world_peers(self.h, world, None, 0)
+        out = np.empty(n, dtype=np.uint32)
+        self.lib.wqo_world_peers(self.h, world, _ptr(out), n)
+        return np.sort(out)
+
+    def apply_ops(self, ops: np.ndarray):
+        """ops: structured array with dtype worldql_server_amd.router.OP_DTYPE (40 bytes)."""
+        ops = np.ascontiguousarray(ops)
+        assert ops.dtype.itemsize == 40
+        self.lib.wqo_apply_ops(self.h, _ptr(ops), len(ops))
+
+    def counts(self):
+        e, c = ctypes.c_uint64(), ctypes.c_uint64()
+        self.lib.wqo_counts(self.h, ctypes.byref(e), ctypes.byref(c))
+        return e.value, c.value
+
+    def route(self, pos, world, sender, repl, keys=None):
+        """Returns (offsets[M+1] u32, peers[P] u32 sorted within each message, F)."""
+        world = np.ascontiguousarray(world, dtype=np.uint32)
+        M = len(world)
+        sender = np.ascontiguousarray(sender, dtype=np.uint32)
+        repl = np.ascontiguousarray(repl, dtype=np.uint8)
+        pos_a = None if pos is None else np.ascontiguousarray(pos, dtype=np.float64).reshape(-1, 3)
+        keys_a = None if keys is None else np.ascontiguousarray(keys, dtype=np.int64).reshape(-1, 3)
+        offsets = np.zeros(M + 1, dtype=np.uint32)
+        F = ctypes.c_uint64()
+        P = self.lib.wqo_route(self.h, _ptr(pos_a), _ptr(keys_a), _ptr(world), _ptr(sender), _ptr(repl), M,
+                               _ptr(offsets), None, 0, ctypes.byref(F))
+        peers = np.zeros(max(P, 1), dtype=np.uint32)
+        self.lib.wqo_route(self.h, _ptr(pos_a), _ptr(keys_a), _ptr(world), _ptr(sender), _ptr(repl), M,
+                           _ptr(offsets), _ptr(peers), P, None)
+        peers = peers[:P]
+        sort_within_segments(offsets, peers)
+        return offsets, peers, F.value
+
+
+def sort_within_segments(offsets: np.ndarray, values: np.ndarray) -> None:
+    """Sort each CSR segment in place (recipient order is a set in the reference)."""
+    if len(values) == 0:
+        return
+    seg = np.repeat(np.arange(len(offsets) - 1, dtype=np.int64), np.diff(offsets.astype(np.int64)))
+    order = np.lexsort((values, seg))
+    values[:] = values[order]

@@ -1,0 +1,308 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the golden fixtures.
+
+Bar: bit-exact. Cube keys are compared as integers; recipient sets are compared per message as
+sorted peer lists (the reference's AHashSet order is random per process).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from worldql_server_amd import abi, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from worldql_server_amd.router import load_library
+    return load_library()
+
+
+def mk_router(cube_size=16, hash_bits=64):
+    from worldql_server_amd.router import Router
+    return Router(cube_size, 0, hash_bits=hash_bits)
+
+
+# ---- kernel (1) -------------------------------------------------------------------------
+
+def test_quantize_reference_kats(lib, kats):
+    from worldql_server_amd.router import quantize
+    for c, s, e in kats["coord_clamp"]:
+        assert int(quantize(np.array([c]), s)[0]) == e
+    for p, s, e in kats["from_vector3"]:
+        assert quantize(np.array(p), s).tolist() == e
+
+
+def test_quantize_edge_vectors(lib, golden_dir):
+    from worldql_server_amd.router import quantize
+    with open(os.path.join(golden_dir, "quantize_edges.json")) as f:
+        vecs = json.load(f)["vectors"]
+    x = np.array([float(v[0]) for v in vecs])
+    s = np.array([v[1] for v in vecs])
+    want = np.array([v[2] for v in vecs], dtype=np.int64)
+    for size in np.unique(s):
+        m = s == size
+        got = quantize(x[m], int(size))
+        assert (got == want[m]).all(), (size, x[m][got != want[m]])
+
+
+def test_quantize_random_bit_patterns(lib, golden_dir):
+    from worldql_server_amd.router import quantize
+    z = np.load(os.path.join(golden_dir, "quantize_random.npz"))
+    for key in z.files:
+        if key.startswith("x_"):
+            assert (quantize(z[key], int(key[2:])) == z["k_" + key[2:]]).all(), key
+    rng = synth.SplitMix64(4242)
+    x = rng.next_u64(2_000_000).view(np.float64)
+    k = (rng.next_u64(500_000) >> np.uint64(11)).astype(np.float64)
+    for s in (1, 7, 16, 65535):
+        mult = k * s
+        xs = np.concatenate([x, mult, -mult, np.nextafter(mult, np.inf), np.nextafter(-mult, -np.inf)])
+        assert (quantize(xs, s) == orc.c_coord_clamp(xs, s)).all(), s
+
+
+# ---- reference unit tests through the WorldMap / AreaMap façade on the GPU ----------------
+
+@pytest.mark.parametrize("name", ["area_subscriptions", "world_subscriptions"])
+def test_area_map_kats_gpu(kats, name):
+    from tests.test_oracle import run_membership_sequence
+    from worldql_server_amd.subscriptions import CubeArea, Vector3, WorldMap
+    seq = kats[name]
+    wm = WorldMap(seq["cube_size"])
+    am = wm.get_mut("world")
+    cube = lambda raw, k: CubeArea(*map(int, k)) if raw else Vector3(*map(float, k))  # noqa: E731
+    run_membership_sequence(
+        seq,
+        add=lambda u, raw, k: am.add_subscription(u, cube(raw, k)),
+        remove=lambda u, raw, k: am.remove_subscription(u, cube(raw, k)),
+        remove_peer=lambda u: am.remove_peer(u),
+        is_sub=lambda u, raw, k: am.is_peer_subscribed(u, cube(raw, k)),
+        is_any=lambda u: am.is_peer_subscribed_any(u),
+    )
+
+
+def test_add_remove_return_values_gpu():
+    """area_map.rs:69-119: add -> newly added; remove -> was present; absent cube -> false."""
+    from worldql_server_amd.subscriptions import CubeArea, Vector3, WorldMap
+    wm = WorldMap(16)
+    am = wm.get_mut("world")
+    assert am.add_subscription("u", Vector3(6.3, 1.0, 10.5)) is True
+    assert am.add_subscription("u", CubeArea(16, 16, 16)) is False
+    assert am.remove_subscription("u", CubeArea(0, 0, 0)) is False
+    assert am.remove_subscription("u", CubeArea(16, 16, 16)) is True
+    assert am.remove_subscription("u", CubeArea(16, 16, 16)) is False
+    assert wm.get("other") is None
+    assert sorted(wm.get_mut("w2").get_subscribed_any_peers()) == []
+    am.add_subscription("v", CubeArea(16, 16, 16))
+    assert list(am.get_subscribed_peers(Vector3(1.0, 1.0, 1.0))) == ["v"]
+    assert wm.remove_peer("v") is True and wm.remove_peer("v") is False
+
+
+# ---- routing parity ---------------------------------------------------------------------
+
+def _compare(r, o, pos, world, sender, repl, keys=None):
+    offs, peers, msgs = r.route(pos, world, sender, repl, keys=keys, with_msgs=True)
+    o_offs, o_peers, _ = o.route(pos, world, sender, repl, keys=keys)
+    assert (offs == o_offs).all()
+    assert (peers == o_peers).all()  # GPU order is ascending per message; oracle sorted per message
+    M = len(world)
+    assert (msgs == np.repeat(np.arange(M, dtype=np.uint32), np.diff(offs.astype(np.int64)))).all()
+    return len(peers)
+
+
+def test_routing_golden_fixtures(golden_dir):
+    z = np.load(os.path.join(golden_dir, "routing_cases.npz"))
+    for c in range(int(z["n_cases"][0])):
+        p = f"c{c}_"
+        r = mk_router(int(z[p + "cube_size"][0]))
+        r.apply_ops(z[p + "ops"].view(abi.OP_DTYPE))
+        offs, peers, _ = r.route(z[p + "pos"], z[p + "world"], z[p + "sender"], z[p + "repl"])
+        assert (offs == z[p + "offsets"]).all(), c
+        assert (peers == z[p + "peers"]).all(), c
+
+
+@pytest.mark.parametrize("hash_bits", [64, 6, 1])
+def test_routing_vs_oracle_c1(hash_bits):
+    """C1 (the reference's CPU config) with all replication modes; hash_bits < 64 forces bucket
+    collisions so the exact build path and long probe walks are exercised."""
+    w = synth.config_c1(repl_mode="mixed")
+    r = mk_router(16, hash_bits)
+    r.apply_ops(w.ops)
+    o = orc.COracle(16)
+    o.apply_ops(w.ops)
+    assert r.stats()["n_entries"] == o.counts()[0]
+    assert r.stats()["n_cubes"] == o.counts()[1]
+    if hash_bits < 64:
+        assert r.stats()["hash_fallbacks"] >= 1
+    P = _compare(r, o, w.pos, w.world, w.sender, w.repl)
+    assert P > 0
+
+
+def test_routing_vs_oracle_c2_scaled():
+    w = synth.config_c2(repl_mode="mixed", scale=0.02)
+    r = mk_router(16)
+    r.apply_ops(w.ops)
+    o = orc.COracle(16)
+    o.apply_ops(w.ops)
+    _compare(r, o, w.pos, w.world, w.sender, w.repl)
+
+
+def test_churn_sequences_vs_oracle():
+    """Subscribe / unsubscribe / remove_peer batches applied incrementally (last op wins)."""
+    rng = synth.SplitMix64(777)
+    r = mk_router(10)
+    o = orc.COracle(10)
+    n_peers, n_worlds = 300, 4
+    for tick in range(6):
+        n = 3000
+        kind = (rng.next_u64(n) % np.uint64(10)).astype(np.int64)
+        kinds = np.where(kind < 6, abi.OP_SUBSCRIBE, np.where(kind < 9, abi.OP_UNSUBSCRIBE, abi.OP_REMOVE_PEER))
+        world = rng.below(n_worlds, n)
+        world = np.where((kinds == abi.OP_REMOVE_PEER) & (rng.below(2, n) == 0), abi.WORLD_INVALID, world)
+        peer = rng.below(n_peers, n)
+        pos = np.floor(rng.uniform(-60, 60, 3 * n).reshape(n, 3) / 5.0) * 5.0  # many repeats + multiples
+        ops = abi.ops_array(world, peer, kinds, pos=pos)
+        r.apply_ops(ops)
+        o.apply_ops(ops)
+        assert r.stats()["n_entries"] == o.counts()[0]
+        M = 4000
+        mpos = rng.uniform(-70, 70, 3 * M).reshape(M, 3)
+        mw = rng.below(n_worlds + 1, M)
+        ms = rng.below(n_peers, M)
+        mr = rng.below(3, M).astype(np.uint8)
+        _compare(r, o, mpos, mw, ms, mr)
+        for wid in range(n_worlds):
+            assert (r.world_peers(wid) == o.world_peers(wid)).all()
+        q_w, q_p = rng.below(n_worlds + 1, 500), rng.below(n_peers, 500)
+        assert (r.is_subscribed_any(q_w, q_p) == [o.is_subscribed_any(int(a), int(b)) for a, b in zip(q_w, q_p)]).all()
+
+
+def test_raw_keys_and_off_grid():
+    r = mk_router(16)
+    o = orc.COracle(16)
+    keys = np.array([[0, 0, 0], [16, 16, 16], [1, 2, 3], [-9223372036854775808, 5, 9223372036854775807]])
+    ops = abi.ops_array(np.zeros(4, np.uint32), np.arange(4), np.zeros(4, np.uint8), key=keys)
+    r.apply_ops(ops)
+    o.apply_ops(ops)
+    mk = np.concatenate([keys, [[0, 0, 1]]])
+    M = len(mk)
+    _compare(r, o, None, np.zeros(M, np.uint32), np.full(M, 99, np.uint32), np.ones(M, np.uint8), keys=mk)
+
+
+def test_edge_positions_route():
+    """NaN / inf / denormal / 2^63 positions land in the same buckets as in the reference."""
+    r = mk_router(16)
+    o = orc.COracle(16)
+    vals = np.array([0.0, -0.0, 5e-324, -5e-324, np.nan, np.inf, -np.inf, 1e300, -1e300, 2.0**63, 16.0, -16.0])
+    g = np.stack(np.meshgrid(vals, vals[:4], vals[4:8], indexing="ij"), -1).reshape(-1, 3)
+    n = len(g)
+    ops = abi.ops_array(np.zeros(n, np.uint32), np.arange(n) % 7, np.zeros(n, np.uint8), pos=g)
+    r.apply_ops(ops)
+    o.apply_ops(ops)
+    _compare(r, o, g, np.zeros(n, np.uint32), np.arange(n, dtype=np.uint32) % 9, (np.arange(n) % 3).astype(np.uint8))
+
+
+def test_empty_inputs():
+    r = mk_router(16)
+    offs, peers, _ = r.route(np.zeros((0, 3)), np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.uint8))
+    assert offs.tolist() == [0] and len(peers) == 0
+    offs, peers, _ = r.route(np.zeros((5, 3)), np.zeros(5, np.uint32), np.zeros(5, np.uint32), np.zeros(5, np.uint8))
+    assert offs.tolist() == [0] * 6
+    r.apply_ops(np.zeros(0, abi.OP_DTYPE))
+    r.remove_peers([1, 2, 3])
+    assert r.stats()["n_entries"] == 0
+
+
+def test_hot_cube_skew_and_ragged_tiles():
+    """One cube with thousands of subscribers plus light cubes; M not a multiple of the tile."""
+    r = mk_router(16)
+    o = orc.COracle(16)
+    n_hot = 5000
+    ops = [abi.ops_array(np.zeros(n_hot, np.uint32), np.arange(n_hot), np.zeros(n_hot, np.uint8),
+                         pos=np.full((n_hot, 3), 1.0))]
+    rng = synth.SplitMix64(5)
+    ops.append(abi.ops_array(np.zeros(2000, np.uint32), rng.below(9000, 2000), np.zeros(2000, np.uint8),
+                             pos=rng.uniform(-200, 200, 6000).reshape(2000, 3)))
+    ops = np.concatenate(ops)
+    r.apply_ops(ops)
+    o.apply_ops(ops)
+    M = 3 * 1024 + 77
+    pos = rng.uniform(-200, 200, 3 * M).reshape(M, 3)
+    pos[::5] = 3.0  # every fifth message hits the hot cube
+    P = _compare(r, o, pos, np.zeros(M, np.uint32), rng.below(n_hot, M), rng.below(3, M).astype(np.uint8))
+    assert P > 500 * n_hot
+
+
+def test_capacity_overflow_reports_required_size():
+    from worldql_server_amd.router import WQError
+    r = mk_router(16)
+    ops = abi.ops_array(np.zeros(100, np.uint32), np.arange(100), np.zeros(100, np.uint8), pos=np.ones((100, 3)))
+    r.apply_ops(ops)
+    with pytest.raises(WQError) as e:
+        r.route(np.ones((10, 3)), np.zeros(10, np.uint32), np.full(10, 500, np.uint32), np.zeros(10, np.uint8),
+                capacity=50)
+    assert e.value.code == abi.WQ_E_CAPACITY
+    offs, peers, _ = r.route(np.ones((10, 3)), np.zeros(10, np.uint32), np.full(10, 500, np.uint32),
+                             np.zeros(10, np.uint8))
+    assert len(peers) == 1000
+
+
+def test_device_api_counters_and_stream():
+    import torch
+    from worldql_server_amd.router import Router
+    w = synth.config_c2(scale=0.01)
+    r = Router(16, 0)
+    r.apply_ops(w.ops)
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.Stream(device=dev)
+    r.set_stream(stream.cuda_stream)
+    M = len(w.world)
+    pos = torch.from_numpy(w.pos).to(dev)
+    world = torch.from_numpy(w.world.view(np.int32)).to(dev)
+    sender = torch.from_numpy(w.sender.view(np.int32)).to(dev)
+    repl = torch.from_numpy(w.repl).to(dev)
+    cap = 40 * M
+    offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    peers = torch.empty(cap, dtype=torch.int32, device=dev)
+    msgs = torch.empty(cap, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    r.route_device(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
+                   peers.data_ptr(), msgs.data_ptr(), cap, cnt.data_ptr())
+    torch.cuda.synchronize()
+    c = cnt.cpu().numpy().view(abi.COUNTERS_DTYPE)[0]
+    o = orc.COracle(16)
+    o.apply_ops(w.ops)
+    o_offs, o_peers, F = o.route(w.pos, w.world, w.sender, w.repl)
+    assert int(c["n_pairs"]) == len(o_peers) and int(c["n_candidates"]) == F
+    assert c["overflow"] == 0 and c["error"] == 0
+    assert (offs.cpu().numpy().view(np.uint32) == o_offs).all()
+    assert (peers[: len(o_peers)].cpu().numpy().view(np.uint32) == o_peers).all()
+    r.set_stream(None)
+
+
+def test_full_c2_size_properties():
+    """BASELINE config C2 at full size: size-independent properties + a sampled exact check."""
+    w = synth.config_c2()
+    r = mk_router(16)
+    r.apply_ops(w.ops)
+    st = r.stats()
+    assert st["n_entries"] == len(w.ops)  # positions are distinct: every subscription is live
+    offs, peers, msgs = r.route(w.pos, w.world, w.sender, w.repl, with_msgs=True)
+    d = np.diff(offs.astype(np.int64))
+    assert (d >= 0).all() and offs[-1] == len(peers)
+    # ascending (hence duplicate-free) peers inside every message, never the sender (ExceptSelf)
+    same = msgs[1:] == msgs[:-1]
+    assert (peers[1:][same] > peers[:-1][same]).all()
+    assert not (peers == w.sender[msgs]).any()
+    # exact on a sample of 20k messages against the oracle
+    o = orc.COracle(16)
+    o.apply_ops(w.ops)
+    idx = np.arange(0, len(w.world), 50)
+    o_offs, o_peers, _ = o.route(w.pos[idx], w.world[idx], w.sender[idx], w.repl[idx])
+    got = np.concatenate([peers[offs[i]:offs[i + 1]] for i in idx])
+    assert (got == o_peers).all()
+    assert 0.8e7 < len(peers) < 1.3e7  # P ≈ 1.0e7

@@ -1,0 +1,69 @@
+"""Host-side constants and record layouts of the C ABI (include/wq_router.h).
+
+Pure data: importing this module loads no native code.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+WQ_OK = 0
+WQ_E_INVALID = -1
+WQ_E_OOM = -2
+WQ_E_HIP = -3
+WQ_E_RCCL = -4
+WQ_E_CAPACITY = -5
+WQ_E_NODEV = -6
+WQ_E_TIMEOUT = -7
+
+OP_SUBSCRIBE = 0    # AreaMap::add_subscription (area_map.rs:72-85)
+OP_UNSUBSCRIBE = 1  # AreaMap::remove_subscription (area_map.rs:88-119)
+OP_REMOVE_PEER = 2  # WorldMap::remove_peer (world_map.rs:41-61)
+
+REPL_EXCEPT_SELF = 0     # Replication wire codes, WorldQLFB_generated.rs:176-188
+REPL_INCLUDING_SELF = 1
+REPL_ONLY_SELF = 2
+
+WORLD_INVALID = 0xFFFFFFFF
+
+# struct wq_op: 40 bytes; `key` aliases `pos` (union).
+OP_DTYPE = np.dtype({
+    "names": ["world", "peer", "kind", "key_is_raw", "pos", "key"],
+    "formats": [np.uint32, np.uint32, np.uint8, np.uint8, (np.float64, 3), (np.int64, 3)],
+    "offsets": [0, 4, 8, 9, 16, 16],
+    "itemsize": 40,
+})
+
+# struct wq_route_counters: 24 bytes
+COUNTERS_DTYPE = np.dtype([("n_pairs", np.uint64), ("n_candidates", np.uint64),
+                           ("overflow", np.uint32), ("error", np.uint32)])
+
+
+def make_op(world: int, peer: int, kind: int, pos=None, key=None) -> np.void:
+    """One wq_op record; give `pos` (Vector3, quantised) or `key` (raw CubeArea)."""
+    o = np.zeros((), dtype=OP_DTYPE)
+    o["world"] = world
+    o["peer"] = peer
+    o["kind"] = kind
+    if key is not None:
+        o["key_is_raw"] = 1
+        o["key"] = np.asarray(key, dtype=np.int64)
+    else:
+        o["key_is_raw"] = 0
+        o["pos"] = np.asarray(pos if pos is not None else (0.0, 0.0, 0.0), dtype=np.float64)
+    return o[()]
+
+
+def ops_array(world, peer, kind, pos=None, key=None) -> np.ndarray:
+    """Vectorised op construction (all arguments broadcast over n ops)."""
+    world = np.asarray(world, dtype=np.uint32)
+    n = world.shape[0]
+    ops = np.zeros(n, dtype=OP_DTYPE)
+    ops["world"] = world
+    ops["peer"] = np.asarray(peer, dtype=np.uint32)
+    ops["kind"] = np.asarray(kind, dtype=np.uint8)
+    if key is not None:
+        ops["key_is_raw"] = 1
+        ops["key"] = np.asarray(key, dtype=np.int64).reshape(n, 3)
+    else:
+        ops["pos"] = np.asarray(pos, dtype=np.float64).reshape(n, 3)
+    return ops

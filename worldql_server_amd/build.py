@@ -1,0 +1,60 @@
+"""Builds libwq_router.so in-tree with hipcc for gfx950 (no JIT cache, no CPU variant).
+
+    python -m worldql_server_amd.build        # incremental
+    python -m worldql_server_amd.build --force
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+BUILD = os.path.join(PKG, "_build")
+LIB = os.path.join(PKG, "libwq_router.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+SOURCES = ["wq_route.hip", "wq_table.hip", "wq_router.hip"]
+HEADERS = ["wq_device.hpp", "wq_internal.hpp"]
+# No fast-math and no FMA contraction: coord_clamp must reproduce Rust's f64 op sequence.
+FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
+         "-fno-fast-math", "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
+
+
+def _mtime(p):
+    return os.path.getmtime(p) if os.path.exists(p) else 0.0
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    hdr_t = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
+    hdr_t = max(hdr_t, _mtime(os.path.join(ROOT, "include", "wq_router.h")))
+    objs = []
+    relink = force or not os.path.exists(LIB)
+    for src in SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILD, src.replace(".hip", ".o"))
+        objs.append(o)
+        if force or _mtime(o) < max(_mtime(s), hdr_t):
+            cmd = [HIPCC, *FLAGS, "-I", os.path.join(ROOT, "include"), "-c", s, "-o", o]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.check_call(cmd)
+            relink = True
+    if relink or any(_mtime(o) > _mtime(LIB) for o in objs):
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB, *objs]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args()
+    print(build(force=a.force, verbose=True))
+    sys.exit(0)

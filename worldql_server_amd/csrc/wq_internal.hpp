@@ -1,0 +1,109 @@
+// wq_internal.hpp — host-side state of one router handle (one GPU, one owner thread).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/wq_router.h"
+#include "wq_device.hpp"
+
+namespace wq {
+
+// Grow-only device buffer.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t need) {
+        if (need <= bytes) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            if (e != hipSuccess) return e;
+            p = nullptr;
+            bytes = 0;
+        }
+        size_t cap = need < 4096 ? 4096 : need + need / 4;
+        hipError_t e = hipMalloc(&p, cap);
+        if (e == hipSuccess) bytes = cap;
+        return e;
+    }
+    template <typename T>
+    T* as() const { return static_cast<T*>(p); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+// The live subscription set, sorted by (hash, world, key, peer): one entry per
+// (world, cube, peer) triple. Everything the route kernel reads is derived from it.
+struct State {
+    DevBuf h, w, kx, ky, kz, p;  // u64, u32, i64 x3, u32
+    uint64_t n = 0;
+};
+
+struct Table {
+    DevBuf slots;     // Slot[cap]
+    DevBuf claim;     // u32[cap] (build scratch)
+    DevBuf list;      // u32[n_entries + n_cubes]: per cube [count, peers...]
+    DevBuf any;       // u64[n_any] sorted (world << 32 | peer)
+    uint64_t cap = 0;
+    int shift = 64;
+    uint64_t n_cubes = 0, n_any = 0;
+};
+
+struct ProfileEvents {
+    std::vector<hipEvent_t> start, stop;
+    size_t used = 0;
+    bool enabled = false;
+};
+
+}  // namespace wq
+
+struct wq_router {
+    int device = 0;
+    uint16_t cube_size = 16;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    uint64_t hash_mask = ~0ull;
+    uint64_t hash_fallbacks = 0;
+    std::string err;
+
+    wq::State st, st_next;
+    wq::Table tab;
+
+    // build scratch
+    wq::DevBuf ev_h, ev_w, ev_kx, ev_ky, ev_kz, ev_p, ev_kind, d_ops;
+    wq::DevBuf idx_a, idx_b, key32_a, key32_b, key64_a, key64_b, flags, scan, sort_tmp, small;
+    wq::DevBuf cube_id, cube_start;
+
+    // route workspace: [counters 32 B][tile counter 16 B][status u64 x n_tiles]
+    wq::DevBuf route_ws;
+    // host-pointer convenience buffers
+    wq::DevBuf h_in, h_out;
+    wq::ProfileEvents prof;
+};
+
+namespace wq {
+// wq_table.hip
+int table_apply_segment(wq_router* h, const wq_op* ops, size_t n);
+// keys: sorted unique (world << 32 | peer); world == WQ_WORLD_INVALID removes the peer everywhere.
+int table_remove_peers(wq_router* h, const uint64_t* keys_sorted_unique, size_t n);
+int table_rebuild_derived(wq_router* h);
+int set_error(wq_router* h, int code, const char* what, hipError_t e = hipSuccess);
+}  // namespace wq
+
+#define WQ_HIP(h, call)                                                    \
+    do {                                                                   \
+        hipError_t e_ = (call);                                            \
+        if (e_ != hipSuccess) return wq::set_error((h), WQ_E_HIP, #call, e_); \
+    } while (0)
+
+#define WQ_ALLOC(h, buf, bytes)                                                     \
+    do {                                                                            \
+        hipError_t e_ = (buf).ensure(bytes);                                        \
+        if (e_ != hipSuccess) return wq::set_error((h), WQ_E_OOM, "hipMalloc " #buf, e_); \
+    } while (0)

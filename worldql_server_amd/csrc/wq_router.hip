@@ -1,0 +1,355 @@
+// wq_router.hip — the C ABI (include/wq_router.h): handle lifetime, host<->device staging,
+// op-stream segmentation and dispatch to the kernels in wq_route.hip / wq_table.hip.
+// Every compute call runs on the GPU; without a gfx950 device the calls fail with WQ_E_NODEV
+// (there is no CPU fallback anywhere in this library).
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "wq_internal.hpp"
+
+namespace wq {
+int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                 const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t* d_offsets,
+                 uint32_t* d_peers, uint32_t* d_msgs, size_t capacity);
+int launch_quantize(hipStream_t s, const double* d_in, size_t n, uint16_t cube_size, int64_t* d_out);
+int launch_is_subscribed(wq_router* h, const uint32_t* d_w, const uint32_t* d_p, int raw, const void* d_kp,
+                         uint32_t n, uint8_t* d_out);
+int launch_is_subscribed_any(wq_router* h, const uint32_t* d_w, const uint32_t* d_p, uint32_t n, uint8_t* d_out);
+int launch_world_range(wq_router* h, uint32_t w, uint64_t* d_out);
+int launch_low32(wq_router* h, const uint64_t* d_in, uint64_t n, uint32_t* d_out);
+}  // namespace wq
+
+using namespace wq;
+
+namespace {
+
+thread_local std::string g_err;  // errors before a handle exists
+
+int check_device(int device, std::string* why) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) {
+        *why = "no HIP device visible (this library has no CPU fallback)";
+        return WQ_E_NODEV;
+    }
+    if (device < 0 || device >= n) {
+        *why = "device index out of range";
+        return WQ_E_INVALID;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        *why = "hipGetDeviceProperties failed";
+        return WQ_E_NODEV;
+    }
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        *why = std::string("device is ") + prop.gcnArchName + ", this build targets gfx950 only";
+        return WQ_E_NODEV;
+    }
+    return WQ_OK;
+}
+
+// Host-staging helper: copies `bytes` from host into h->h_in at `offset` (aligned 256).
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+}  // namespace
+
+extern "C" {
+
+int wq_router_create(uint16_t cube_size, int device, wq_router** out) {
+    if (!out || cube_size == 0) return WQ_E_INVALID;  // args.rs: cube_size is NonZeroU16
+    *out = nullptr;
+    int rc = check_device(device, &g_err);
+    if (rc) return rc;
+    if (hipSetDevice(device) != hipSuccess) return WQ_E_HIP;
+    wq_router* h = new (std::nothrow) wq_router();
+    if (!h) return WQ_E_OOM;
+    h->device = device;
+    h->cube_size = cube_size;
+    if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return WQ_E_HIP;
+    }
+    h->stream = h->own_stream;
+    rc = table_rebuild_derived(h);  // empty table: all slots empty
+    if (rc) {
+        g_err = h->err;
+        wq_router_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return WQ_OK;
+}
+
+int wq_router_destroy(wq_router* h) {
+    if (!h) return WQ_E_INVALID;
+    (void)hipSetDevice(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    for (auto e : h->prof.start) (void)hipEventDestroy(e);
+    for (auto e : h->prof.stop) (void)hipEventDestroy(e);
+    DevBuf* bufs[] = {&h->st.h, &h->st.w, &h->st.kx, &h->st.ky, &h->st.kz, &h->st.p,
+                      &h->st_next.h, &h->st_next.w, &h->st_next.kx, &h->st_next.ky, &h->st_next.kz,
+                      &h->st_next.p, &h->tab.slots, &h->tab.claim, &h->tab.list, &h->tab.any,
+                      &h->ev_h, &h->ev_w, &h->ev_kx, &h->ev_ky, &h->ev_kz, &h->ev_p, &h->ev_kind,
+                      &h->d_ops, &h->idx_a, &h->idx_b, &h->key32_a, &h->key32_b, &h->key64_a,
+                      &h->key64_b, &h->flags, &h->scan, &h->sort_tmp, &h->small, &h->cube_id,
+                      &h->cube_start, &h->route_ws, &h->h_in, &h->h_out};
+    for (DevBuf* b : bufs) b->release();
+    if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+    delete h;
+    return WQ_OK;
+}
+
+const char* wq_last_error(const wq_router* h) { return h ? h->err.c_str() : g_err.c_str(); }
+
+int wq_set_stream(wq_router* h, void* stream) {
+    if (!h) return WQ_E_INVALID;
+    h->stream = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
+    return WQ_OK;
+}
+
+int wq_get_stats(wq_router* h, wq_stats* out) {
+    if (!h || !out) return WQ_E_INVALID;
+    out->n_entries = h->st.n;
+    out->n_cubes = h->tab.n_cubes;
+    out->n_any = h->tab.n_any;
+    out->table_slots = h->tab.cap;
+    out->hash_fallbacks = h->hash_fallbacks;
+    out->cube_size = h->cube_size;
+    out->device = h->device;
+    return WQ_OK;
+}
+
+int wq_debug_set_hash_bits(wq_router* h, int bits) {
+    if (!h || bits < 1 || bits > 64) return WQ_E_INVALID;
+    if (h->st.n) return set_error(h, WQ_E_INVALID, "hash bits can only change on an empty table");
+    h->hash_mask = bits == 64 ? ~0ull : ((1ull << bits) - 1);
+    return WQ_OK;
+}
+
+int wq_apply_ops(wq_router* h, const wq_op* ops, size_t n) {
+    if (!h || (n && !ops)) return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    for (size_t i = 0; i < n; ++i)
+        if (ops[i].kind > WQ_OP_REMOVE_PEER ||
+            (ops[i].kind != WQ_OP_REMOVE_PEER && ops[i].world == WQ_WORLD_INVALID))
+            return set_error(h, WQ_E_INVALID, "bad op (kind or reserved world id)");
+    // Split at REMOVE_PEER runs so the reference's sequential order is kept (thread.rs:122-146).
+    size_t i = 0;
+    std::vector<uint64_t> rm;
+    while (i < n) {
+        size_t j = i;
+        if (ops[i].kind != WQ_OP_REMOVE_PEER) {
+            while (j < n && ops[j].kind != WQ_OP_REMOVE_PEER) ++j;
+            int rc = table_apply_segment(h, ops + i, j - i);
+            if (rc) return rc;
+        } else {
+            rm.clear();
+            for (; j < n && ops[j].kind == WQ_OP_REMOVE_PEER; ++j)
+                rm.push_back(((uint64_t)ops[j].world << 32) | ops[j].peer);
+            std::sort(rm.begin(), rm.end());
+            rm.erase(std::unique(rm.begin(), rm.end()), rm.end());
+            int rc = table_remove_peers(h, rm.data(), rm.size());
+            if (rc) return rc;
+        }
+        i = j;
+    }
+    return WQ_OK;
+}
+
+int wq_remove_peers(wq_router* h, const uint32_t* peers, size_t n) {
+    if (!h || (n && !peers)) return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    std::vector<uint64_t> rm(n);
+    for (size_t i = 0; i < n; ++i) rm[i] = ((uint64_t)WQ_WORLD_INVALID << 32) | peers[i];
+    std::sort(rm.begin(), rm.end());
+    rm.erase(std::unique(rm.begin(), rm.end()), rm.end());
+    return table_remove_peers(h, rm.data(), rm.size());
+}
+
+int wq_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                         const uint32_t* d_sender, const uint8_t* d_repl, size_t n_msgs, uint32_t* d_offsets,
+                         uint32_t* d_peers, uint32_t* d_msgs, size_t capacity, wq_route_counters* d_counters) {
+    if (!h || !d_offsets || (n_msgs && (!d_world || !d_sender || !d_repl || (!d_pos && !d_keys))) ||
+        (capacity && !d_peers))
+        return WQ_E_INVALID;
+    if (n_msgs >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
+    if (capacity > 0xFFFFFFFFull) capacity = 0xFFFFFFFFull;  // u32 CSR offsets
+    WQ_HIP(h, hipSetDevice(h->device));
+    int rc = launch_route(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs, capacity);
+    if (rc) return rc;
+    if (d_counters)
+        WQ_HIP(h, hipMemcpyAsync(d_counters, h->route_ws.p, sizeof(wq_route_counters), hipMemcpyDeviceToDevice,
+                                 h->stream));
+    return WQ_OK;
+}
+
+int wq_route_tick(wq_router* h, const double* pos, const int64_t* keys, const uint32_t* world,
+                  const uint32_t* sender, const uint8_t* repl, size_t M, uint32_t* offsets, uint32_t* peers,
+                  uint32_t* msgs, size_t capacity, size_t* n_pairs) {
+    if (!h || !offsets || !n_pairs || (M && (!world || !sender || !repl || (!pos && !keys))) ||
+        (capacity && !peers))
+        return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    const size_t b_pos = keys ? M * 24 : (pos ? M * 24 : 0);
+    const size_t o_pos = 0, o_w = align256(o_pos + b_pos), o_s = align256(o_w + M * 4),
+                 o_r = align256(o_s + M * 4), n_in = align256(o_r + M + 1);
+    WQ_ALLOC(h, h->h_in, n_in);
+    char* din = h->h_in.as<char>();
+    hipStream_t s = h->stream;
+    if (M) {
+        WQ_HIP(h, hipMemcpyAsync(din + o_pos, keys ? (const void*)keys : (const void*)pos, b_pos,
+                                 hipMemcpyHostToDevice, s));
+        WQ_HIP(h, hipMemcpyAsync(din + o_w, world, M * 4, hipMemcpyHostToDevice, s));
+        WQ_HIP(h, hipMemcpyAsync(din + o_s, sender, M * 4, hipMemcpyHostToDevice, s));
+        WQ_HIP(h, hipMemcpyAsync(din + o_r, repl, M, hipMemcpyHostToDevice, s));
+    }
+    const size_t cap = std::min<size_t>(capacity, 0xFFFFFFFFull);
+    const size_t oo = 0, op = align256((M + 1) * 4), om = align256(op + cap * 4), n_out = align256(om + (msgs ? cap * 4 : 0));
+    WQ_ALLOC(h, h->h_out, n_out + 256);
+    char* dout = h->h_out.as<char>();
+    int rc = launch_route(h, keys ? nullptr : reinterpret_cast<const double*>(din + o_pos),
+                          keys ? reinterpret_cast<const int64_t*>(din + o_pos) : nullptr,
+                          reinterpret_cast<const uint32_t*>(din + o_w), reinterpret_cast<const uint32_t*>(din + o_s),
+                          reinterpret_cast<const uint8_t*>(din + o_r), M, reinterpret_cast<uint32_t*>(dout + oo),
+                          cap ? reinterpret_cast<uint32_t*>(dout + op) : nullptr,
+                          (msgs && cap) ? reinterpret_cast<uint32_t*>(dout + om) : nullptr, cap);
+    if (rc) return rc;
+    wq_route_counters cnt;
+    WQ_HIP(h, hipMemcpyAsync(&cnt, h->route_ws.p, sizeof(cnt), hipMemcpyDeviceToHost, s));
+    WQ_HIP(h, hipStreamSynchronize(s));
+    if (M == 0) cnt.n_pairs = 0;
+    *n_pairs = cnt.n_pairs;
+    if (cnt.error) return set_error(h, WQ_E_TIMEOUT, "route look-back spin gave up");
+    if (cnt.n_pairs > 0xFFFFFFFFull) return set_error(h, WQ_E_CAPACITY, "more than 2^32-1 pairs in one tick");
+    const size_t P = cnt.n_pairs;
+    WQ_HIP(h, hipMemcpyAsync(offsets, dout + oo, (M + 1) * 4, hipMemcpyDeviceToHost, s));
+    const size_t ncopy = std::min(P, cap);
+    if (ncopy) {
+        WQ_HIP(h, hipMemcpyAsync(peers, dout + op, ncopy * 4, hipMemcpyDeviceToHost, s));
+        if (msgs) WQ_HIP(h, hipMemcpyAsync(msgs, dout + om, ncopy * 4, hipMemcpyDeviceToHost, s));
+    }
+    WQ_HIP(h, hipStreamSynchronize(s));
+    if (P > capacity) return set_error(h, WQ_E_CAPACITY, "output capacity too small (required size in *n_pairs)");
+    return WQ_OK;
+}
+
+int wq_is_subscribed(wq_router* h, size_t n, const uint32_t* world, const uint32_t* peer, int key_is_raw,
+                     const void* key_or_pos, uint8_t* out) {
+    if (!h || (n && (!world || !peer || !key_or_pos || !out))) return WQ_E_INVALID;
+    if (n == 0) return WQ_OK;
+    if (n >= 0xFFFFFFFFull) return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    const size_t o_w = 0, o_p = align256(n * 4), o_k = align256(o_p + n * 4), o_o = align256(o_k + n * 24);
+    WQ_ALLOC(h, h->h_in, o_o + n);
+    char* d = h->h_in.as<char>();
+    hipStream_t s = h->stream;
+    WQ_HIP(h, hipMemcpyAsync(d + o_w, world, n * 4, hipMemcpyHostToDevice, s));
+    WQ_HIP(h, hipMemcpyAsync(d + o_p, peer, n * 4, hipMemcpyHostToDevice, s));
+    WQ_HIP(h, hipMemcpyAsync(d + o_k, key_or_pos, n * 24, hipMemcpyHostToDevice, s));
+    int rc = launch_is_subscribed(h, reinterpret_cast<uint32_t*>(d + o_w), reinterpret_cast<uint32_t*>(d + o_p),
+                                  key_is_raw ? 1 : 0, d + o_k, (uint32_t)n, reinterpret_cast<uint8_t*>(d + o_o));
+    if (rc) return rc;
+    WQ_HIP(h, hipMemcpyAsync(out, d + o_o, n, hipMemcpyDeviceToHost, s));
+    WQ_HIP(h, hipStreamSynchronize(s));
+    return WQ_OK;
+}
+
+int wq_is_subscribed_any(wq_router* h, size_t n, const uint32_t* world, const uint32_t* peer, uint8_t* out) {
+    if (!h || (n && (!world || !peer || !out))) return WQ_E_INVALID;
+    if (n == 0) return WQ_OK;
+    if (n >= 0xFFFFFFFFull) return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    const size_t o_w = 0, o_p = align256(n * 4), o_o = align256(o_p + n * 4);
+    WQ_ALLOC(h, h->h_in, o_o + n);
+    char* d = h->h_in.as<char>();
+    hipStream_t s = h->stream;
+    WQ_HIP(h, hipMemcpyAsync(d + o_w, world, n * 4, hipMemcpyHostToDevice, s));
+    WQ_HIP(h, hipMemcpyAsync(d + o_p, peer, n * 4, hipMemcpyHostToDevice, s));
+    int rc = launch_is_subscribed_any(h, reinterpret_cast<uint32_t*>(d + o_w), reinterpret_cast<uint32_t*>(d + o_p),
+                                      (uint32_t)n, reinterpret_cast<uint8_t*>(d + o_o));
+    if (rc) return rc;
+    WQ_HIP(h, hipMemcpyAsync(out, d + o_o, n, hipMemcpyDeviceToHost, s));
+    WQ_HIP(h, hipStreamSynchronize(s));
+    return WQ_OK;
+}
+
+int wq_world_peers(wq_router* h, uint32_t world, uint32_t* out, size_t capacity, size_t* n_out) {
+    if (!h || !n_out || (capacity && !out)) return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    WQ_ALLOC(h, h->small, 64);
+    hipStream_t s = h->stream;
+    int rc = launch_world_range(h, world, h->small.as<uint64_t>());
+    if (rc) return rc;
+    uint64_t range[2];
+    WQ_HIP(h, hipMemcpyAsync(range, h->small.p, 16, hipMemcpyDeviceToHost, s));
+    WQ_HIP(h, hipStreamSynchronize(s));
+    const uint64_t n = range[1] - range[0];
+    *n_out = n;
+    const uint64_t nc = std::min<uint64_t>(n, capacity);
+    if (nc) {
+        WQ_ALLOC(h, h->h_out, nc * 4);
+        rc = launch_low32(h, h->tab.any.as<uint64_t>() + range[0], nc, h->h_out.as<uint32_t>());
+        if (rc) return rc;
+        WQ_HIP(h, hipMemcpyAsync(out, h->h_out.p, nc * 4, hipMemcpyDeviceToHost, s));
+        WQ_HIP(h, hipStreamSynchronize(s));
+    }
+    if (n > capacity) return set_error(h, WQ_E_CAPACITY, "world_peers capacity too small");
+    return WQ_OK;
+}
+
+int wq_quantize(const double* coords, size_t n, uint16_t cube_size, int64_t* out) {
+    if (cube_size == 0 || (n && (!coords || !out))) return WQ_E_INVALID;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int rc = check_device(dev, &g_err);
+    if (rc) return rc;
+    if (n == 0) return WQ_OK;
+    void *din = nullptr, *dout = nullptr;
+    if (hipMalloc(&din, n * 8) != hipSuccess) return WQ_E_OOM;
+    if (hipMalloc(&dout, n * 8) != hipSuccess) {
+        (void)hipFree(din);
+        return WQ_E_OOM;
+    }
+    int status = WQ_OK;
+    if (hipMemcpy(din, coords, n * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        launch_quantize(nullptr, static_cast<const double*>(din), n, cube_size, static_cast<int64_t*>(dout)) != 0 ||
+        hipMemcpy(out, dout, n * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        status = WQ_E_HIP;
+    (void)hipFree(din);
+    (void)hipFree(dout);
+    return status;
+}
+
+int wq_quantize_device(wq_router* h, const double* d_coords, size_t n, int64_t* d_out) {
+    if (!h || (n && (!d_coords || !d_out))) return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    if (launch_quantize(h->stream, d_coords, n, h->cube_size, d_out) != 0)
+        return set_error(h, WQ_E_HIP, "quantize launch failed");
+    return WQ_OK;
+}
+
+int wq_profile_enable(wq_router* h, int enable) {
+    if (!h) return WQ_E_INVALID;
+    h->prof.enabled = enable != 0;
+    h->prof.used = 0;
+    return WQ_OK;
+}
+
+int wq_profile_read(wq_router* h, double* kernel_ms, uint64_t* launches) {
+    if (!h || !kernel_ms || !launches) return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    double total = 0.0;
+    for (size_t i = 0; i < h->prof.used; ++i) {
+        WQ_HIP(h, hipEventSynchronize(h->prof.stop[i]));
+        float ms = 0.0f;
+        WQ_HIP(h, hipEventElapsedTime(&ms, h->prof.start[i], h->prof.stop[i]));
+        total += ms;
+    }
+    *kernel_ms = total;
+    *launches = h->prof.used;
+    h->prof.used = 0;
+    return WQ_OK;
+}
+
+}  // extern "C"

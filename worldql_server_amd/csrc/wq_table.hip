@@ -1,0 +1,500 @@
+// wq_table.hip — building the cube -> peer-list hash table on the GPU.
+//
+// Replaces the mutation side of the reference subscription table:
+//   AreaMap::add_subscription     worldql_server/src/subscriptions/area_map.rs:72-85
+//   AreaMap::remove_subscription  area_map.rs:88-119
+//   AreaMap::remove_peer / WorldMap::remove_peer  area_map.rs:124-135, world_map.rs:41-61
+// The reference applies ops one by one on a single task (processing/thread.rs:113-148). Here a
+// batch of ops is applied at once with identical results: the state is the SET of live
+// (world, cube, peer) triples, and for each triple the last op of the batch decides its
+// presence (sub and unsub are single-element set ops).
+//
+// Pipeline (all on the handle's stream):
+//   events  = live entries (as "present" events) ++ ops (quantised by kernel (1), hashed)
+//   order   = stable radix sort by (hash, peer)  [exact multi-key sort if two cubes share a hash]
+//   state'  = last event of every (cube, peer) run that is a subscribe
+//   derived = per-cube peer lists (list[off] = count, then ascending peers), the open-addressed
+//             slot table (32-byte records, load <= 1/2), and sorted unique (world<<32 | peer)
+//             keys for is_peer_subscribed_any / get_subscribed_any_peers (area_map.rs:46-67).
+// Sorting uses rocPRIM's radix sort (AMD's native primitive library); every other step is a
+// kernel in this file.
+#include <cstring>
+
+#include <rocprim/rocprim.hpp>
+
+#include "wq_internal.hpp"
+
+namespace wq {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+inline unsigned grid_for(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+__global__ void k_ops_to_events(const wq_op* __restrict__ ops, uint32_t n, uint64_t base,
+                                double sf, int64_t si, uint64_t hmask, uint64_t* ev_h,
+                                uint32_t* ev_w, int64_t* ev_kx, int64_t* ev_ky, int64_t* ev_kz,
+                                uint32_t* ev_p, uint8_t* ev_kind) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const wq_op o = ops[i];
+    int64_t k0, k1, k2;
+    if (o.key_is_raw) {  // impl ToCubeArea for CubeArea: identity (cube_area.rs:65-70)
+        k0 = o.u.key[0];
+        k1 = o.u.key[1];
+        k2 = o.u.key[2];
+    } else {  // impl ToCubeArea for Vector3 -> CubeArea::from_vector3 (cube_area.rs:50-56)
+        k0 = coord_clamp_dev(o.u.pos[0], sf, si);
+        k1 = coord_clamp_dev(o.u.pos[1], sf, si);
+        k2 = coord_clamp_dev(o.u.pos[2], sf, si);
+    }
+    const uint64_t e = base + i;
+    ev_h[e] = cube_hash(o.world, k0, k1, k2) & hmask;
+    ev_w[e] = o.world;
+    ev_kx[e] = k0;
+    ev_ky[e] = k1;
+    ev_kz[e] = k2;
+    ev_p[e] = o.peer;
+    ev_kind[e] = (o.kind == WQ_OP_SUBSCRIBE) ? 1 : 0;
+}
+
+__global__ void k_fill_u8(uint8_t* a, uint64_t n, uint8_t v) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) a[i] = v;
+}
+
+__global__ void k_iota(uint32_t* a, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) a[i] = (uint32_t)i;
+}
+
+template <typename T>
+__global__ void k_gather(const T* __restrict__ src, const uint32_t* __restrict__ idx, T* dst,
+                         uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) dst[i] = src[idx[i]];
+}
+
+struct EvView {
+    const uint64_t* h;
+    const uint32_t* w;
+    const int64_t *kx, *ky, *kz;
+    const uint32_t* p;
+    __device__ bool same_cube(uint32_t a, uint32_t b) const {
+        return h[a] == h[b] && w[a] == w[b] && kx[a] == kx[b] && ky[a] == ky[b] && kz[a] == kz[b];
+    }
+};
+
+// After the (hash, peer) sort: two different cubes with one hash in adjacent positions.
+__global__ void k_detect_collision(EvView ev, const uint32_t* __restrict__ order, uint64_t n,
+                                   uint32_t* flag) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i == 0 || i >= n) return;
+    const uint32_t a = order[i - 1], b = order[i];
+    if (ev.h[a] == ev.h[b] && !ev.same_cube(a, b)) atomicOr(flag, 1u);
+}
+
+// keep[i] = event i (in sorted order) is the last one of its (cube, peer) run and subscribes.
+__global__ void k_mark_last(EvView ev, const uint8_t* __restrict__ kind,
+                            const uint32_t* __restrict__ order, uint64_t n, uint32_t* keep) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t a = order[i];
+    bool last = true;
+    if (i + 1 < n) {
+        const uint32_t b = order[i + 1];
+        last = !(ev.p[a] == ev.p[b] && ev.same_cube(a, b));
+    }
+    keep[i] = (last && kind[a]) ? 1u : 0u;
+}
+
+struct StOut {
+    uint64_t* h;
+    uint32_t* w;
+    int64_t *kx, *ky, *kz;
+    uint32_t* p;
+};
+
+__global__ void k_scatter_state(EvView ev, const uint32_t* __restrict__ order,
+                                const uint32_t* __restrict__ keep, const uint32_t* __restrict__ pos,
+                                uint64_t n, StOut out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n || !keep[i]) return;
+    const uint32_t a = order ? order[i] : (uint32_t)i;
+    const uint32_t j = pos[i];
+    out.h[j] = ev.h[a];
+    out.w[j] = ev.w[a];
+    out.kx[j] = ev.kx[a];
+    out.ky[j] = ev.ky[a];
+    out.kz[j] = ev.kz[a];
+    out.p[j] = ev.p[a];
+}
+
+__global__ void k_cube_heads(EvView st, uint64_t n, uint32_t* head) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    head[i] = (i == 0 || !st.same_cube((uint32_t)i - 1, (uint32_t)i)) ? 1u : 0u;
+}
+
+// cid = inclusive scan of head: cube index of entry i is cid[i] - 1.
+__global__ void k_cube_start(const uint32_t* __restrict__ head, const uint32_t* __restrict__ cid,
+                             uint64_t n, uint32_t n_cubes, uint32_t* cube_start) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n && head[i]) cube_start[cid[i] - 1] = (uint32_t)i;
+    if (i == 0) cube_start[n_cubes] = (uint32_t)n;
+}
+
+// Cube c's entries [s_c, s_{c+1}) land at list[s_c + c + 1 ...], its count at list[s_c + c].
+__global__ void k_fill_lists(const uint32_t* __restrict__ st_p, const uint32_t* __restrict__ head,
+                             const uint32_t* __restrict__ cid, const uint32_t* __restrict__ cube_start,
+                             uint64_t n, uint32_t* list) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = cid[i] - 1;
+    list[i + c + 1] = st_p[i];
+    if (head[i]) list[i + c] = cube_start[c + 1] - (uint32_t)i;
+}
+
+__global__ void k_insert_slots(EvView st, const uint32_t* __restrict__ cube_start, uint32_t n_cubes,
+                               uint32_t* claim, Slot* slots, uint64_t mask, int shift) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= n_cubes) return;
+    const uint32_t j = cube_start[c];
+    uint64_t s = slot_of(st.h[j], shift);
+    while (atomicCAS(&claim[s], 0u, c + 1) != 0u) s = (s + 1) & mask;
+    Slot r;
+    r.k[0] = st.kx[j];
+    r.k[1] = st.ky[j];
+    r.k[2] = st.kz[j];
+    r.world = st.w[j];
+    r.off = j + c;
+    slots[s] = r;
+}
+
+__global__ void k_any_keys(const uint32_t* __restrict__ w, const uint32_t* __restrict__ p, uint64_t n,
+                           uint64_t* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) out[i] = ((uint64_t)w[i] << 32) | p[i];
+}
+
+__global__ void k_unique_flags(const uint64_t* __restrict__ a, uint64_t n, uint32_t* flags) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) flags[i] = (i == 0 || a[i] != a[i - 1]) ? 1u : 0u;
+}
+
+__global__ void k_scatter_flagged_u64(const uint64_t* __restrict__ a, const uint32_t* __restrict__ flags,
+                                      const uint32_t* __restrict__ pos, uint64_t n, uint64_t* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n && flags[i]) out[pos[i]] = a[i];
+}
+
+// removed: sorted (world << 32 | peer); world 0xFFFFFFFF matches every world.
+__global__ void k_keep_not_removed(const uint32_t* __restrict__ st_w, const uint32_t* __restrict__ st_p,
+                                   uint64_t n, const uint64_t* __restrict__ removed, uint32_t n_removed,
+                                   uint32_t* keep) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k1 = ((uint64_t)st_w[i] << 32) | st_p[i];
+    const uint64_t k2 = ((uint64_t)kWorldEmpty << 32) | st_p[i];
+    const uint32_t a = lower_bound_dev(removed, n_removed, k1);
+    const uint32_t b = lower_bound_dev(removed, n_removed, k2);
+    const bool gone = (a < n_removed && removed[a] == k1) || (b < n_removed && removed[b] == k2);
+    keep[i] = gone ? 0u : 1u;
+}
+
+// ---- rocPRIM wrappers (temp storage in h->sort_tmp) ----
+
+template <typename K>
+int sort_pairs(wq_router* h, const K* kin, K* kout, const uint32_t* vin, uint32_t* vout, uint64_t n,
+               int end_bit) {
+    size_t bytes = 0;
+    WQ_HIP(h, rocprim::radix_sort_pairs(nullptr, bytes, kin, kout, vin, vout, (size_t)n, 0, end_bit,
+                                        h->stream));
+    WQ_ALLOC(h, h->sort_tmp, bytes);
+    WQ_HIP(h, rocprim::radix_sort_pairs(h->sort_tmp.p, bytes, kin, kout, vin, vout, (size_t)n, 0,
+                                        end_bit, h->stream));
+    return WQ_OK;
+}
+
+int sort_keys_u64(wq_router* h, const uint64_t* kin, uint64_t* kout, uint64_t n) {
+    size_t bytes = 0;
+    WQ_HIP(h, rocprim::radix_sort_keys(nullptr, bytes, kin, kout, (size_t)n, 0, 64, h->stream));
+    WQ_ALLOC(h, h->sort_tmp, bytes);
+    WQ_HIP(h, rocprim::radix_sort_keys(h->sort_tmp.p, bytes, kin, kout, (size_t)n, 0, 64, h->stream));
+    return WQ_OK;
+}
+
+int scan_u32(wq_router* h, const uint32_t* in, uint32_t* out, uint64_t n, bool inclusive) {
+    size_t bytes = 0;
+    if (inclusive) {
+        WQ_HIP(h, rocprim::inclusive_scan(nullptr, bytes, in, out, (size_t)n, rocprim::plus<uint32_t>(),
+                                          h->stream));
+        WQ_ALLOC(h, h->sort_tmp, bytes);
+        WQ_HIP(h, rocprim::inclusive_scan(h->sort_tmp.p, bytes, in, out, (size_t)n,
+                                          rocprim::plus<uint32_t>(), h->stream));
+    } else {
+        WQ_HIP(h, rocprim::exclusive_scan(nullptr, bytes, in, out, 0u, (size_t)n,
+                                          rocprim::plus<uint32_t>(), h->stream));
+        WQ_ALLOC(h, h->sort_tmp, bytes);
+        WQ_HIP(h, rocprim::exclusive_scan(h->sort_tmp.p, bytes, in, out, 0u, (size_t)n,
+                                          rocprim::plus<uint32_t>(), h->stream));
+    }
+    return WQ_OK;
+}
+
+// n-th element of a device u32 array (synchronous read; build path only).
+int read_u32(wq_router* h, const uint32_t* a, uint64_t i, uint32_t* out) {
+    WQ_HIP(h, hipMemcpyAsync(out, a + i, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+    WQ_HIP(h, hipStreamSynchronize(h->stream));
+    return WQ_OK;
+}
+
+EvView ev_view(wq_router* h) {
+    return EvView{h->ev_h.as<uint64_t>(), h->ev_w.as<uint32_t>(), h->ev_kx.as<int64_t>(),
+                  h->ev_ky.as<int64_t>(), h->ev_kz.as<int64_t>(), h->ev_p.as<uint32_t>()};
+}
+EvView st_view(const State& s) {
+    return EvView{s.h.as<uint64_t>(), s.w.as<uint32_t>(), s.kx.as<int64_t>(), s.ky.as<int64_t>(),
+                  s.kz.as<int64_t>(), s.p.as<uint32_t>()};
+}
+
+int ensure_state(wq_router* h, State& s, uint64_t n) {
+    const uint64_t m = n ? n : 1;
+    WQ_ALLOC(h, s.h, m * 8);
+    WQ_ALLOC(h, s.w, m * 4);
+    WQ_ALLOC(h, s.kx, m * 8);
+    WQ_ALLOC(h, s.ky, m * 8);
+    WQ_ALLOC(h, s.kz, m * 8);
+    WQ_ALLOC(h, s.p, m * 4);
+    return WQ_OK;
+}
+
+// Stable LSD sort of `order` by one key column (gathered through the current order).
+template <typename K>
+int refine_by(wq_router* h, const K* column, uint64_t n, int bits) {
+    uint32_t* cur = h->idx_b.as<uint32_t>();
+    uint32_t* nxt = h->idx_a.as<uint32_t>();
+    K* kg = reinterpret_cast<K*>(h->key64_a.p);
+    K* ks = reinterpret_cast<K*>(h->key64_b.p);
+    hipLaunchKernelGGL(k_gather<K>, dim3(grid_for(n)), dim3(kBlock), 0, h->stream, column, cur, kg, n);
+    int rc = sort_pairs<K>(h, kg, ks, cur, nxt, n, bits);
+    if (rc) return rc;
+    WQ_HIP(h, hipMemcpyAsync(cur, nxt, n * 4, hipMemcpyDeviceToDevice, h->stream));
+    return WQ_OK;
+}
+
+}  // namespace
+
+int set_error(wq_router* h, int code, const char* what, hipError_t e) {
+    if (h) {
+        h->err = what;
+        if (e != hipSuccess) {
+            h->err += ": ";
+            h->err += hipGetErrorString(e);
+        }
+    }
+    return code;
+}
+
+// Apply one batch of subscribe / unsubscribe ops (no REMOVE_PEER inside).
+int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops) {
+    if (n_ops == 0) return WQ_OK;
+    const uint64_t S = h->st.n;
+    const uint64_t N = S + n_ops;
+    if (N >= 0xFFFFFFFFull) return set_error(h, WQ_E_INVALID, "more than 2^32-1 subscription events");
+
+    WQ_ALLOC(h, h->d_ops, n_ops * sizeof(wq_op));
+    WQ_ALLOC(h, h->ev_h, N * 8);
+    WQ_ALLOC(h, h->ev_w, N * 4);
+    WQ_ALLOC(h, h->ev_kx, N * 8);
+    WQ_ALLOC(h, h->ev_ky, N * 8);
+    WQ_ALLOC(h, h->ev_kz, N * 8);
+    WQ_ALLOC(h, h->ev_p, N * 4);
+    WQ_ALLOC(h, h->ev_kind, N);
+    WQ_ALLOC(h, h->idx_a, N * 4);
+    WQ_ALLOC(h, h->idx_b, N * 4);
+    WQ_ALLOC(h, h->key32_a, N * 4);
+    WQ_ALLOC(h, h->key64_a, N * 8);
+    WQ_ALLOC(h, h->key64_b, N * 8);
+    WQ_ALLOC(h, h->flags, N * 4);
+    WQ_ALLOC(h, h->scan, N * 4);
+    WQ_ALLOC(h, h->small, 64);
+
+    hipStream_t s = h->stream;
+    WQ_HIP(h, hipMemcpyAsync(h->d_ops.p, ops, n_ops * sizeof(wq_op), hipMemcpyHostToDevice, s));
+    // live entries first: they are the earliest "present" events
+    if (S) {
+        WQ_HIP(h, hipMemcpyAsync(h->ev_h.p, h->st.h.p, S * 8, hipMemcpyDeviceToDevice, s));
+        WQ_HIP(h, hipMemcpyAsync(h->ev_w.p, h->st.w.p, S * 4, hipMemcpyDeviceToDevice, s));
+        WQ_HIP(h, hipMemcpyAsync(h->ev_kx.p, h->st.kx.p, S * 8, hipMemcpyDeviceToDevice, s));
+        WQ_HIP(h, hipMemcpyAsync(h->ev_ky.p, h->st.ky.p, S * 8, hipMemcpyDeviceToDevice, s));
+        WQ_HIP(h, hipMemcpyAsync(h->ev_kz.p, h->st.kz.p, S * 8, hipMemcpyDeviceToDevice, s));
+        WQ_HIP(h, hipMemcpyAsync(h->ev_p.p, h->st.p.p, S * 4, hipMemcpyDeviceToDevice, s));
+        hipLaunchKernelGGL(k_fill_u8, dim3(grid_for(S)), dim3(kBlock), 0, s, h->ev_kind.as<uint8_t>(), S,
+                           (uint8_t)1);
+    }
+    hipLaunchKernelGGL(k_ops_to_events, dim3(grid_for(n_ops)), dim3(kBlock), 0, s, h->d_ops.as<wq_op>(),
+                       (uint32_t)n_ops, S, (double)h->cube_size, (int64_t)h->cube_size, h->hash_mask,
+                       h->ev_h.as<uint64_t>(), h->ev_w.as<uint32_t>(), h->ev_kx.as<int64_t>(),
+                       h->ev_ky.as<int64_t>(), h->ev_kz.as<int64_t>(), h->ev_p.as<uint32_t>(),
+                       h->ev_kind.as<uint8_t>());
+    WQ_HIP(h, hipGetLastError());
+
+    // order = stable sort by (hash, peer): sort by peer, then stably by hash
+    uint32_t* idx_a = h->idx_a.as<uint32_t>();
+    uint32_t* idx_b = h->idx_b.as<uint32_t>();
+    hipLaunchKernelGGL(k_iota, dim3(grid_for(N)), dim3(kBlock), 0, s, idx_a, N);
+    int rc = sort_pairs<uint32_t>(h, h->ev_p.as<uint32_t>(), h->key32_a.as<uint32_t>(), idx_a, idx_b, N, 32);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_gather<uint64_t>, dim3(grid_for(N)), dim3(kBlock), 0, s, h->ev_h.as<uint64_t>(),
+                       idx_b, h->key64_a.as<uint64_t>(), N);
+    rc = sort_pairs<uint64_t>(h, h->key64_a.as<uint64_t>(), h->key64_b.as<uint64_t>(), idx_b, idx_a, N, 64);
+    if (rc) return rc;
+    uint32_t* order = idx_a;
+
+    EvView ev = ev_view(h);
+    uint32_t* dflag = h->small.as<uint32_t>();
+    WQ_HIP(h, hipMemsetAsync(dflag, 0, 4, s));
+    hipLaunchKernelGGL(k_detect_collision, dim3(grid_for(N)), dim3(kBlock), 0, s, ev, order, N, dflag);
+    uint32_t collided = 0;
+    rc = read_u32(h, dflag, 0, &collided);
+    if (rc) return rc;
+    if (collided) {
+        // exact path: LSD passes peer, kz, ky, kx, world, hash over the original event order
+        h->hash_fallbacks++;
+        hipLaunchKernelGGL(k_iota, dim3(grid_for(N)), dim3(kBlock), 0, s, idx_b, N);
+        if ((rc = refine_by<uint32_t>(h, h->ev_p.as<uint32_t>(), N, 32))) return rc;
+        if ((rc = refine_by<uint64_t>(h, reinterpret_cast<const uint64_t*>(h->ev_kz.p), N, 64))) return rc;
+        if ((rc = refine_by<uint64_t>(h, reinterpret_cast<const uint64_t*>(h->ev_ky.p), N, 64))) return rc;
+        if ((rc = refine_by<uint64_t>(h, reinterpret_cast<const uint64_t*>(h->ev_kx.p), N, 64))) return rc;
+        if ((rc = refine_by<uint32_t>(h, h->ev_w.as<uint32_t>(), N, 32))) return rc;
+        if ((rc = refine_by<uint64_t>(h, h->ev_h.as<uint64_t>(), N, 64))) return rc;
+        order = idx_b;
+    }
+
+    // last op wins per (cube, peer)
+    uint32_t* keep = h->flags.as<uint32_t>();
+    uint32_t* pos = h->scan.as<uint32_t>();
+    hipLaunchKernelGGL(k_mark_last, dim3(grid_for(N)), dim3(kBlock), 0, s, ev, h->ev_kind.as<uint8_t>(),
+                       order, N, keep);
+    if ((rc = scan_u32(h, keep, pos, N, false))) return rc;
+    uint32_t last_pos = 0, last_keep = 0;
+    if ((rc = read_u32(h, pos, N - 1, &last_pos))) return rc;
+    if ((rc = read_u32(h, keep, N - 1, &last_keep))) return rc;
+    const uint64_t S_new = (uint64_t)last_pos + last_keep;
+    if ((rc = ensure_state(h, h->st_next, S_new))) return rc;
+    StOut out{h->st_next.h.as<uint64_t>(), h->st_next.w.as<uint32_t>(), h->st_next.kx.as<int64_t>(),
+              h->st_next.ky.as<int64_t>(), h->st_next.kz.as<int64_t>(), h->st_next.p.as<uint32_t>()};
+    hipLaunchKernelGGL(k_scatter_state, dim3(grid_for(N)), dim3(kBlock), 0, s, ev, order, keep, pos, N, out);
+    WQ_HIP(h, hipGetLastError());
+    std::swap(h->st, h->st_next);
+    h->st.n = S_new;
+    return table_rebuild_derived(h);
+}
+
+// WorldMap::remove_peer / AreaMap::remove_peer for sorted unique (world << 32 | peer) keys
+// (world_map.rs:41-61, area_map.rs:124-135).
+int table_remove_peers(wq_router* h, const uint64_t* keys, size_t n_rm) {
+    const uint64_t S = h->st.n;
+    if (S == 0 || n_rm == 0) return WQ_OK;
+    hipStream_t s = h->stream;
+    WQ_ALLOC(h, h->key32_b, n_rm * 8);
+    WQ_ALLOC(h, h->flags, S * 4);
+    WQ_ALLOC(h, h->scan, S * 4);
+    WQ_HIP(h, hipMemcpyAsync(h->key32_b.p, keys, n_rm * 8, hipMemcpyHostToDevice, s));
+    uint32_t* keep = h->flags.as<uint32_t>();
+    uint32_t* pos = h->scan.as<uint32_t>();
+    hipLaunchKernelGGL(k_keep_not_removed, dim3(grid_for(S)), dim3(kBlock), 0, s, h->st.w.as<uint32_t>(),
+                       h->st.p.as<uint32_t>(), S, h->key32_b.as<uint64_t>(), (uint32_t)n_rm, keep);
+    int rc = scan_u32(h, keep, pos, S, false);
+    if (rc) return rc;
+    uint32_t last_pos = 0, last_keep = 0;
+    if ((rc = read_u32(h, pos, S - 1, &last_pos))) return rc;
+    if ((rc = read_u32(h, keep, S - 1, &last_keep))) return rc;
+    const uint64_t S_new = (uint64_t)last_pos + last_keep;
+    if (S_new == S) return WQ_OK;
+    if ((rc = ensure_state(h, h->st_next, S_new))) return rc;
+    StOut out{h->st_next.h.as<uint64_t>(), h->st_next.w.as<uint32_t>(), h->st_next.kx.as<int64_t>(),
+              h->st_next.ky.as<int64_t>(), h->st_next.kz.as<int64_t>(), h->st_next.p.as<uint32_t>()};
+    hipLaunchKernelGGL(k_scatter_state, dim3(grid_for(S)), dim3(kBlock), 0, s, st_view(h->st), nullptr, keep,
+                       pos, S, out);
+    WQ_HIP(h, hipGetLastError());
+    std::swap(h->st, h->st_next);
+    h->st.n = S_new;
+    return table_rebuild_derived(h);
+}
+
+// Per-cube lists, slot table and the (world, peer) "any" keys from the sorted state.
+int table_rebuild_derived(wq_router* h) {
+    hipStream_t s = h->stream;
+    const uint64_t S = h->st.n;
+    Table& t = h->tab;
+    int rc;
+    uint32_t n_cubes = 0;
+    EvView st = st_view(h->st);
+    if (S) {
+        WQ_ALLOC(h, h->flags, S * 4);
+        WQ_ALLOC(h, h->scan, S * 4);
+        uint32_t* head = h->flags.as<uint32_t>();
+        uint32_t* cid = h->scan.as<uint32_t>();
+        hipLaunchKernelGGL(k_cube_heads, dim3(grid_for(S)), dim3(kBlock), 0, s, st, S, head);
+        if ((rc = scan_u32(h, head, cid, S, true))) return rc;
+        if ((rc = read_u32(h, cid, S - 1, &n_cubes))) return rc;
+        WQ_ALLOC(h, h->cube_start, ((uint64_t)n_cubes + 1) * 4);
+        hipLaunchKernelGGL(k_cube_start, dim3(grid_for(S)), dim3(kBlock), 0, s, head, cid, S, n_cubes,
+                           h->cube_start.as<uint32_t>());
+        WQ_ALLOC(h, t.list, (S + n_cubes) * 4);
+        hipLaunchKernelGGL(k_fill_lists, dim3(grid_for(S)), dim3(kBlock), 0, s, h->st.p.as<uint32_t>(), head,
+                           cid, h->cube_start.as<uint32_t>(), S, t.list.as<uint32_t>());
+    } else {
+        WQ_ALLOC(h, t.list, 4);
+    }
+    // slot table: capacity = pow2 >= max(1024, 2 * cubes), so every probe walk meets an empty slot
+    uint64_t cap = 1024;
+    int log2cap = 10;
+    while (cap < 2ull * n_cubes) {
+        cap <<= 1;
+        log2cap++;
+    }
+    WQ_ALLOC(h, t.slots, cap * sizeof(Slot));
+    WQ_ALLOC(h, t.claim, cap * 4);
+    WQ_HIP(h, hipMemsetAsync(t.slots.p, 0xFF, cap * sizeof(Slot), s));
+    WQ_HIP(h, hipMemsetAsync(t.claim.p, 0, cap * 4, s));
+    t.cap = cap;
+    t.shift = 64 - log2cap;
+    if (n_cubes)
+        hipLaunchKernelGGL(k_insert_slots, dim3(grid_for(n_cubes)), dim3(kBlock), 0, s, st,
+                           h->cube_start.as<uint32_t>(), n_cubes, t.claim.as<uint32_t>(), t.slots.as<Slot>(),
+                           cap - 1, t.shift);
+    t.n_cubes = n_cubes;
+
+    // sorted unique (world << 32 | peer)
+    t.n_any = 0;
+    if (S) {
+        WQ_ALLOC(h, h->key64_a, S * 8);
+        WQ_ALLOC(h, h->key64_b, S * 8);
+        hipLaunchKernelGGL(k_any_keys, dim3(grid_for(S)), dim3(kBlock), 0, s, h->st.w.as<uint32_t>(),
+                           h->st.p.as<uint32_t>(), S, h->key64_a.as<uint64_t>());
+        if ((rc = sort_keys_u64(h, h->key64_a.as<uint64_t>(), h->key64_b.as<uint64_t>(), S))) return rc;
+        uint32_t* fl = h->flags.as<uint32_t>();
+        uint32_t* ps = h->scan.as<uint32_t>();
+        hipLaunchKernelGGL(k_unique_flags, dim3(grid_for(S)), dim3(kBlock), 0, s, h->key64_b.as<uint64_t>(), S,
+                           fl);
+        if ((rc = scan_u32(h, fl, ps, S, false))) return rc;
+        uint32_t lp = 0, lf = 0;
+        if ((rc = read_u32(h, ps, S - 1, &lp))) return rc;
+        if ((rc = read_u32(h, fl, S - 1, &lf))) return rc;
+        t.n_any = (uint64_t)lp + lf;
+        WQ_ALLOC(h, t.any, t.n_any * 8);
+        hipLaunchKernelGGL(k_scatter_flagged_u64, dim3(grid_for(S)), dim3(kBlock), 0, s,
+                           h->key64_b.as<uint64_t>(), fl, ps, S, t.any.as<uint64_t>());
+    } else {
+        WQ_ALLOC(h, t.any, 8);
+    }
+    WQ_HIP(h, hipGetLastError());
+    WQ_HIP(h, hipStreamSynchronize(s));
+    return WQ_OK;
+}
+
+}  // namespace wq

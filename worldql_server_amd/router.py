@@ -1,0 +1,201 @@
+"""Python binding of the C ABI (include/wq_router.h) — the HIP routing library, nothing else.
+
+`Router` is a thin ctypes wrapper; every compute call runs the gfx950 kernels of
+libwq_router.so. There is no CPU fallback: without the library or without a gfx950 device the
+constructor raises `WQError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import abi
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libwq_router.so")
+
+_lib = None
+
+
+class WQError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"wq error {code}: {msg}")
+        self.code = code
+
+
+def load_library(build_if_missing: bool = True):
+    """Load libwq_router.so (building it with hipcc if it is absent and hipcc exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        if not build_if_missing or not os.path.exists(os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")):
+            raise ImportError(f"{LIB_PATH} is missing: run `python -m worldql_server_amd.build`")
+        from .build import build
+        build()
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, sz, u32, u16, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_int
+    sig = {
+        "wq_router_create": ([u16, i32, ctypes.POINTER(vp)], i32),
+        "wq_router_destroy": ([vp], i32),
+        "wq_last_error": ([vp], ctypes.c_char_p),
+        "wq_set_stream": ([vp, vp], i32),
+        "wq_get_stats": ([vp, vp], i32),
+        "wq_apply_ops": ([vp, vp, sz], i32),
+        "wq_remove_peers": ([vp, vp, sz], i32),
+        "wq_route_tick": ([vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, ctypes.POINTER(sz)], i32),
+        "wq_route_tick_device": ([vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, vp], i32),
+        "wq_is_subscribed": ([vp, sz, vp, vp, i32, vp, vp], i32),
+        "wq_is_subscribed_any": ([vp, sz, vp, vp, vp], i32),
+        "wq_world_peers": ([vp, u32, vp, sz, ctypes.POINTER(sz)], i32),
+        "wq_quantize": ([vp, sz, u16, vp], i32),
+        "wq_quantize_device": ([vp, vp, sz, vp], i32),
+        "wq_profile_enable": ([vp, i32], i32),
+        "wq_profile_read": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)], i32),
+        "wq_debug_set_hash_bits": ([vp, i32], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = lib
+    return lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class WQStats(ctypes.Structure):
+    _fields_ = [("n_entries", ctypes.c_uint64), ("n_cubes", ctypes.c_uint64), ("n_any", ctypes.c_uint64),
+                ("table_slots", ctypes.c_uint64), ("hash_fallbacks", ctypes.c_uint64),
+                ("cube_size", ctypes.c_uint32), ("device", ctypes.c_int32)]
+
+
+def quantize(coords, cube_size: int) -> np.ndarray:
+    """Kernel (1) on host arrays: CubeArea::coord_clamp per coordinate (cube_area.rs:23-44)."""
+    lib = load_library()
+    c = np.ascontiguousarray(coords, dtype=np.float64)
+    out = np.empty(c.shape, dtype=np.int64)
+    rc = lib.wq_quantize(_p(c), c.size, cube_size, _p(out))
+    if rc != 0:
+        raise WQError(rc, lib.wq_last_error(None).decode())
+    return out
+
+
+class Router:
+    """One subscription table on one GPU (`WorldMap` of worldql_server/src/subscriptions/world_map.rs)."""
+
+    def __init__(self, cube_size: int = 16, device: int = 0, hash_bits: int = 64):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        rc = self.lib.wq_router_create(cube_size, device, ctypes.byref(h))
+        if rc != 0:
+            raise WQError(rc, self.lib.wq_last_error(None).decode())
+        self.h = h
+        self.cube_size = cube_size
+        self.device = device
+        if hash_bits != 64:
+            self._check(self.lib.wq_debug_set_hash_bits(self.h, hash_bits))
+
+    def _check(self, rc: int):
+        if rc != 0:
+            raise WQError(rc, self.lib.wq_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.wq_router_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- table ----
+    def apply_ops(self, ops: np.ndarray) -> None:
+        ops = np.ascontiguousarray(ops, dtype=abi.OP_DTYPE)
+        self._check(self.lib.wq_apply_ops(self.h, _p(ops), len(ops)))
+
+    def remove_peers(self, peers) -> None:
+        a = np.ascontiguousarray(peers, dtype=np.uint32)
+        self._check(self.lib.wq_remove_peers(self.h, _p(a), len(a)))
+
+    def stats(self) -> dict:
+        s = WQStats()
+        self._check(self.lib.wq_get_stats(self.h, ctypes.byref(s)))
+        return {f: getattr(s, f) for f, _ in WQStats._fields_}
+
+    # ---- hot path ----
+    def route(self, pos, world, sender, repl, keys=None, with_msgs: bool = False, capacity: int | None = None):
+        """One tick on host arrays. Returns (offsets[M+1], peers[P], msgs[P] or None)."""
+        world = np.ascontiguousarray(world, dtype=np.uint32)
+        M = len(world)
+        sender = np.ascontiguousarray(sender, dtype=np.uint32)
+        repl = np.ascontiguousarray(repl, dtype=np.uint8)
+        pos_a = None if pos is None else np.ascontiguousarray(pos, dtype=np.float64).reshape(-1, 3)
+        keys_a = None if keys is None else np.ascontiguousarray(keys, dtype=np.int64).reshape(-1, 3)
+        cap = capacity if capacity is not None else max(1024, 16 * M)
+        while True:
+            offsets = np.empty(M + 1, dtype=np.uint32)
+            peers = np.empty(max(cap, 1), dtype=np.uint32)
+            msgs = np.empty(max(cap, 1), dtype=np.uint32) if with_msgs else None
+            n = ctypes.c_size_t()
+            rc = self.lib.wq_route_tick(self.h, _p(pos_a), _p(keys_a), _p(world), _p(sender), _p(repl), M,
+                                        _p(offsets), _p(peers), _p(msgs), cap, ctypes.byref(n))
+            if rc == abi.WQ_E_CAPACITY and n.value > cap and capacity is None:
+                cap = n.value
+                continue
+            self._check(rc)
+            P = n.value
+            return offsets, peers[:P], (msgs[:P] if with_msgs else None)
+
+    def route_device(self, pos_ptr: int, world_ptr: int, sender_ptr: int, repl_ptr: int, n_msgs: int,
+                     offsets_ptr: int, peers_ptr: int, msgs_ptr: int | None, capacity: int,
+                     counters_ptr: int | None = None, keys_ptr: int | None = None) -> None:
+        """Asynchronous tick on device pointers (e.g. torch tensors' data_ptr())."""
+        self._check(self.lib.wq_route_tick_device(self.h, pos_ptr or None, keys_ptr or None, world_ptr, sender_ptr,
+                                                  repl_ptr, n_msgs, offsets_ptr, peers_ptr or None,
+                                                  msgs_ptr or None, capacity, counters_ptr or None))
+
+    def set_stream(self, stream_ptr: int | None) -> None:
+        self._check(self.lib.wq_set_stream(self.h, stream_ptr or None))
+
+    # ---- queries ----
+    def is_subscribed(self, world, peer, key_is_raw: bool, key_or_pos) -> np.ndarray:
+        world = np.ascontiguousarray(world, dtype=np.uint32)
+        peer = np.ascontiguousarray(peer, dtype=np.uint32)
+        k = np.ascontiguousarray(key_or_pos, dtype=np.int64 if key_is_raw else np.float64).reshape(-1, 3)
+        out = np.zeros(len(world), dtype=np.uint8)
+        self._check(self.lib.wq_is_subscribed(self.h, len(world), _p(world), _p(peer), int(key_is_raw), _p(k),
+                                              _p(out)))
+        return out.astype(bool)
+
+    def is_subscribed_any(self, world, peer) -> np.ndarray:
+        world = np.ascontiguousarray(world, dtype=np.uint32)
+        peer = np.ascontiguousarray(peer, dtype=np.uint32)
+        out = np.zeros(len(world), dtype=np.uint8)
+        self._check(self.lib.wq_is_subscribed_any(self.h, len(world), _p(world), _p(peer), _p(out)))
+        return out.astype(bool)
+
+    def world_peers(self, world: int) -> np.ndarray:
+        n = ctypes.c_size_t()
+        rc = self.lib.wq_world_peers(self.h, world, None, 0, ctypes.byref(n))
+        if rc not in (0, abi.WQ_E_CAPACITY):
+            self._check(rc)
+        out = np.zeros(max(n.value, 1), dtype=np.uint32)
+        self._check(self.lib.wq_world_peers(self.h, world, _p(out), n.value, ctypes.byref(n)))
+        return out[: n.value]
+
+    # ---- instrumentation ----
+    def profile_enable(self, on: bool = True) -> None:
+        self._check(self.lib.wq_profile_enable(self.h, int(on)))
+
+    def profile_read(self):
+        ms = ctypes.c_double()
+        n = ctypes.c_uint64()
+        self._check(self.lib.wq_profile_read(self.h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
