@@ -191,7 +191,7 @@ class COracle:
     def apply_ops(self, ops: np.ndarray):
         """ops: structured array with dtype worldql_server_amd.router.OP_DTYPE (40 bytes)."""
         ops = np.ascontiguousarray(ops)
-        assert ops.dtype.itemsize == 40
+        assert ops.dtype.itemsize == 40 and ops.dtype.fields["key"][1] == 16, "pass OP_DTYPE records"
         self.lib.wqo_apply_ops(self.h, _ptr(ops), len(ops))
 
     def counts(self):

@@ -226,14 +226,14 @@ def test_hot_cube_skew_and_ragged_tiles():
     rng = synth.SplitMix64(5)
     ops.append(abi.ops_array(np.zeros(2000, np.uint32), rng.below(9000, 2000), np.zeros(2000, np.uint8),
                              pos=rng.uniform(-200, 200, 6000).reshape(2000, 3)))
-    ops = np.concatenate(ops)
+    ops = abi.concat_ops(ops)
     r.apply_ops(ops)
     o.apply_ops(ops)
     M = 3 * 1024 + 77
     pos = rng.uniform(-200, 200, 3 * M).reshape(M, 3)
     pos[::5] = 3.0  # every fifth message hits the hot cube
     P = _compare(r, o, pos, np.zeros(M, np.uint32), rng.below(n_hot, M), rng.below(3, M).astype(np.uint8))
-    assert P > 500 * n_hot
+    assert P > 300 * n_hot  # ~660 hot messages, 2/3 of them not OnlySelf
 
 
 def test_capacity_overflow_reports_required_size():

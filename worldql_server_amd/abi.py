@@ -67,3 +67,8 @@ def ops_array(world, peer, kind, pos=None, key=None) -> np.ndarray:
     else:
         ops["pos"] = np.asarray(pos, dtype=np.float64).reshape(n, 3)
     return ops
+
+
+def concat_ops(parts) -> np.ndarray:
+    """np.concatenate drops the union layout of OP_DTYPE; join the raw 40-byte records instead."""
+    return np.concatenate([np.ascontiguousarray(p, dtype=OP_DTYPE).view(np.uint8) for p in parts]).view(OP_DTYPE)

@@ -35,6 +35,13 @@ def load_library(build_if_missing: bool = True):
             raise ImportError(f"{LIB_PATH} is missing: run `python -m worldql_server_amd.build`")
         from .build import build
         build()
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7. Loading torch
+    # first makes this library's libamdhip64.so.7 dependency resolve to that same copy (two
+    # runtimes in one process do not share devices). Without torch the system runtime is used.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     vp, sz, u32, u16, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_int
     sig = {
