@@ -236,6 +236,29 @@ def test_hot_cube_skew_and_ragged_tiles():
     assert P > 300 * n_hot  # ~660 hot messages, 2/3 of them not OnlySelf
 
 
+@pytest.mark.parametrize("per_cube", [27, 28, 29])
+def test_inline_boundary_and_stage_overflow(per_cube):
+    """Cubes with 27/28/29 subscribers (the 28-peer inline record boundary); every message lands in
+    them, so a tile's staged lists exceed the LDS stage and the overflow path reads HBM lists."""
+    r = mk_router(16)
+    o = orc.COracle(16)
+    n_cubes = 40
+    cx = np.repeat(np.arange(n_cubes) * 16.0 + 8.0, per_cube)
+    peer = np.arange(n_cubes * per_cube, dtype=np.uint32)
+    pos = np.stack([cx, np.full_like(cx, 8.0), np.full_like(cx, -8.0)], 1)
+    ops = abi.ops_array(np.zeros(len(cx), np.uint32), peer, np.zeros(len(cx), np.uint8), pos=pos)
+    r.apply_ops(ops)
+    o.apply_ops(ops)
+    rng = synth.SplitMix64(per_cube)
+    M = 5000
+    mpos = np.stack([rng.below(n_cubes, M) * 16.0 + rng.uniform(0.5, 15.5, M), rng.uniform(0.5, 15.5, M),
+                     -rng.uniform(0.5, 15.5, M)], 1)
+    for cfg in range(5):
+        r.set_route_config(cfg)
+        _compare(r, o, mpos, np.zeros(M, np.uint32), rng.below(n_cubes * per_cube, M),
+                 rng.below(3, M).astype(np.uint8))
+
+
 def test_capacity_overflow_reports_required_size():
     from worldql_server_amd.router import WQError
     r = mk_router(16)

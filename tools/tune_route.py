@@ -1,0 +1,67 @@
+"""Times every compiled route-kernel shape on the C2 tick (kernel-only HIP events) and checks
+that all shapes produce identical outputs. Usage: python tools/tune_route.py [--scale S]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--cfgs", default="0,1,2,3,4")
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    from worldql_server_amd import abi, synth
+    from worldql_server_amd.router import Router
+    dev = torch.device("cuda:0")
+    w = synth.config_c2(scale=a.scale)
+    M = len(w.world)
+    r = Router(16, 0)
+    s = torch.cuda.Stream(device=dev)
+    r.set_stream(s.cuda_stream)
+    r.apply_ops(w.ops)
+    pos = torch.from_numpy(w.pos).to(dev)
+    world = torch.from_numpy(w.world.view(np.int32)).to(dev)
+    sender = torch.from_numpy(w.sender.view(np.int32)).to(dev)
+    repl = torch.from_numpy(w.repl).to(dev)
+    offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    cap = 12 * M
+    peers = torch.empty(cap, dtype=torch.int32, device=dev)
+    msgs = torch.empty(cap, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    ref = None
+    res = {}
+    cfgs = [int(c) for c in a.cfgs.split(",")]
+    for rnd in range(a.rounds):
+        for cfg in cfgs:
+            r.set_route_config(cfg)
+            args = (pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
+                    peers.data_ptr(), msgs.data_ptr(), cap)
+            for _ in range(3):
+                r.route_device(*args, cnt.data_ptr())
+            torch.cuda.synchronize()
+            c = cnt.cpu().numpy().view(abi.COUNTERS_DTYPE)[0]
+            P = int(c["n_pairs"])
+            h = (offs.cpu().numpy().tobytes(), peers[:P].cpu().numpy().tobytes(), msgs[:P].cpu().numpy().tobytes())
+            if ref is None:
+                ref = h
+            assert h == ref, f"cfg {cfg} differs"
+            r.profile_enable(True)
+            for _ in range(a.steps):
+                r.route_device(*args)
+            ms, n = r.profile_read()
+            r.profile_enable(False)
+            res.setdefault(cfg, []).append(ms / n * 1e3)
+    print(json.dumps({"M": M, "P": P, "us_per_launch": {k: [round(x, 2) for x in v] for k, v in res.items()}}))
+
+
+if __name__ == "__main__":
+    main()

@@ -65,6 +65,52 @@ __host__ __device__ __forceinline__ uint64_t cube_hash(uint32_t w, int64_t x, in
     return h;
 }
 
+// ---- bucket records (the table the hot path probes) --------------------------------------
+// A "regular" cube — world < 1023 and every key coordinate an exact multiple k = a*s of the cube
+// size with a in [-2^17, 2^17) — has an exact 64-bit packed key
+//   pk = (world + 1) << 54 | (ax + 2^17) << 36 | (ay + 2^17) << 18 | (az + 2^17)   (pk != 0).
+// Every key a Vector3 can produce for coordinates within +-2^17 cubes of the origin is regular.
+// Regular cubes live in 128-byte records (one cache line: one fabric request per lookup):
+//   pk, peer count, offset of the cube's full list in `list`, and the first kInline peers.
+// Everything else (raw off-grid keys, NaN/inf/huge coordinates, world ids >= 1023) lives in the
+// 32-byte full-key Slot table. Both tables are exact; a key is in exactly one of them.
+constexpr int kInline = 28;
+constexpr uint32_t kAxisBias = 1u << 17;
+
+struct __attribute__((aligned(128))) Record {
+    uint64_t pk;       // 0 = empty
+    uint32_t count;    // peers subscribed to the cube
+    uint32_t list_off; // list[list_off] = count, list[list_off+1 ..] = ascending peers
+    uint32_t peers[kInline];  // the first min(count, kInline) peers, ascending; rest 0xFFFFFFFF
+};
+static_assert(sizeof(Record) == 128, "Record must be one 128-byte line");
+
+__host__ __device__ __forceinline__ bool pack_key(uint32_t w, int64_t x, int64_t y, int64_t z, double sf,
+                                                  uint64_t* pk) {
+    if (w >= 1023u) return false;
+    const int64_t k[3] = {x, y, z};
+    uint64_t a[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        // |k| < 2^33: exact in f64, and k/s is an integer iff the quotient is
+        if (k[d] <= -(1ll << 33) || k[d] >= (1ll << 33)) return false;
+        const double q = (double)k[d] / sf;
+        if (q != trunc(q) || q < -131072.0 || q >= 131072.0) return false;
+        a[d] = (uint64_t)((int64_t)q + (int64_t)kAxisBias);
+    }
+    *pk = ((uint64_t)(w + 1) << 54) | (a[0] << 36) | (a[1] << 18) | a[2];
+    return true;
+}
+
+__host__ __device__ __forceinline__ uint64_t rec_hash(uint64_t pk) {
+    uint64_t h = pk ^ (pk >> 31);
+    h *= 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 32;
+    return h;
+}
+
 // Slot index from the hash's high bits. shift = 64 - log2(capacity), capacity >= 1024.
 __device__ __forceinline__ uint64_t slot_of(uint64_t h, int shift) { return h >> shift; }
 
@@ -97,6 +143,43 @@ __device__ __forceinline__ uint32_t probe(const Slot* slots, uint64_t mask, int 
         if (s.world == w && s.k0 == x && s.k1 == y && s.k2 == z) return s.off;
         i = (i + 1) & mask;
     }
+}
+
+struct TableView {
+    const Record* recs;
+    uint64_t rec_mask;
+    int rec_shift;
+    const Slot* slots;
+    uint64_t slot_mask;
+    int slot_shift;
+    uint64_t hash_mask;
+    const uint32_t* list;
+    double sf;
+};
+
+// Header of the record probe sequence for pk: walks while the slot holds another key.
+__device__ __forceinline__ uint64_t find_record(const TableView& t, uint64_t pk, uint4* hdr) {
+    uint64_t i = slot_of(rec_hash(pk) & t.hash_mask, t.rec_shift);
+    for (;;) {
+        const uint4 h = *reinterpret_cast<const uint4*>(t.recs + i);
+        const uint64_t k = ((uint64_t)h.y << 32) | h.x;
+        if (k == 0 || k == pk) {
+            *hdr = h;
+            return i;
+        }
+        i = (i + 1) & t.rec_mask;
+    }
+}
+
+// Offset of the cube's list in t.list, or kNone (both tables).
+__device__ __forceinline__ uint32_t find_list(const TableView& t, uint32_t w, int64_t x, int64_t y, int64_t z) {
+    uint64_t pk;
+    if (pack_key(w, x, y, z, t.sf, &pk)) {
+        uint4 h;
+        find_record(t, pk, &h);
+        return (h.x | h.y) ? h.w : kNone;
+    }
+    return probe(t.slots, t.slot_mask, t.slot_shift, cube_hash(w, x, y, z) & t.hash_mask, w, x, y, z);
 }
 
 // First index in sorted a[0..n) with a[i] >= v.

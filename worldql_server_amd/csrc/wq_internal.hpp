@@ -46,13 +46,30 @@ struct State {
 };
 
 struct Table {
-    DevBuf slots;     // Slot[cap]
+    DevBuf recs;      // Record[rec_cap]: regular cubes (wq_device.hpp), load <= 0.3
+    DevBuf rclaim;    // u32[rec_cap] (build scratch)
+    uint64_t rec_cap = 0;
+    int rec_shift = 64;
+    DevBuf slots;     // Slot[cap]: cubes without a packed key
     DevBuf claim;     // u32[cap] (build scratch)
     DevBuf list;      // u32[n_entries + n_cubes]: per cube [count, peers...]
     DevBuf any;       // u64[n_any] sorted (world << 32 | peer)
     uint64_t cap = 0;
     int shift = 64;
     uint64_t n_cubes = 0, n_any = 0;
+};
+
+// Route workspace, persistent across calls so a tick needs no memset: a monotonic scan-tile
+// ticket, two counter slots (each call zeroes the next call's), epoch-tagged scan status words,
+// and the per-message locators the count pass hands to the emit pass.
+struct RouteWs {
+    DevBuf buf;
+    DevBuf info;  // uint2[M]
+    uint64_t status_cap = 0;
+    uint64_t ticket_base = 0;
+    uint32_t epoch = 0;
+    uint64_t calls = 0;
+    wq_route_counters* last = nullptr;  // counters of the most recent call (device)
 };
 
 struct ProfileEvents {
@@ -80,14 +97,29 @@ struct wq_router {
     wq::DevBuf idx_a, idx_b, key32_a, key32_b, key64_a, key64_b, flags, scan, sort_tmp, small;
     wq::DevBuf cube_id, cube_start;
 
-    // route workspace: [counters 32 B][tile counter 16 B][status u64 x n_tiles]
-    wq::DevBuf route_ws;
+    wq::RouteWs rws;
+    int route_cfg = 0;  // route kernel shapes (wq_route.hip kCfgs)
     // host-pointer convenience buffers
     wq::DevBuf h_in, h_out;
     wq::ProfileEvents prof;
 };
 
 namespace wq {
+inline TableView table_view(const wq_router* h) {
+    TableView v;
+    v.recs = h->tab.recs.as<Record>();
+    v.rec_mask = h->tab.rec_cap - 1;
+    v.rec_shift = h->tab.rec_shift;
+    v.slots = h->tab.slots.as<Slot>();
+    v.slot_mask = h->tab.cap - 1;
+    v.slot_shift = h->tab.shift;
+    v.hash_mask = h->hash_mask;
+    v.list = h->tab.list.as<uint32_t>();
+    v.sf = (double)h->cube_size;
+    return v;
+}
+// wq_route.hip
+int route_config_count();
 // wq_table.hip
 int table_apply_segment(wq_router* h, const wq_op* ops, size_t n);
 // keys: sorted unique (world << 32 | peer); world == WQ_WORLD_INVALID removes the peer everywhere.

@@ -93,7 +93,8 @@ int wq_router_destroy(wq_router* h) {
                       &h->ev_h, &h->ev_w, &h->ev_kx, &h->ev_ky, &h->ev_kz, &h->ev_p, &h->ev_kind,
                       &h->d_ops, &h->idx_a, &h->idx_b, &h->key32_a, &h->key32_b, &h->key64_a,
                       &h->key64_b, &h->flags, &h->scan, &h->sort_tmp, &h->small, &h->cube_id,
-                      &h->cube_start, &h->route_ws, &h->h_in, &h->h_out};
+                      &h->cube_start, &h->rws.buf, &h->rws.info, &h->h_in, &h->h_out,
+                      &h->tab.recs, &h->tab.rclaim};
     for (DevBuf* b : bufs) b->release();
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -117,6 +118,12 @@ int wq_get_stats(wq_router* h, wq_stats* out) {
     out->hash_fallbacks = h->hash_fallbacks;
     out->cube_size = h->cube_size;
     out->device = h->device;
+    return WQ_OK;
+}
+
+int wq_debug_set_route_config(wq_router* h, int cfg) {
+    if (!h || cfg < 0 || cfg >= route_config_count()) return WQ_E_INVALID;
+    h->route_cfg = cfg;
     return WQ_OK;
 }
 
@@ -179,7 +186,7 @@ int wq_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_key
     int rc = launch_route(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs, capacity);
     if (rc) return rc;
     if (d_counters)
-        WQ_HIP(h, hipMemcpyAsync(d_counters, h->route_ws.p, sizeof(wq_route_counters), hipMemcpyDeviceToDevice,
+        WQ_HIP(h, hipMemcpyAsync(d_counters, h->rws.last, sizeof(wq_route_counters), hipMemcpyDeviceToDevice,
                                  h->stream));
     return WQ_OK;
 }
@@ -216,7 +223,7 @@ int wq_route_tick(wq_router* h, const double* pos, const int64_t* keys, const ui
                           (msgs && cap) ? reinterpret_cast<uint32_t*>(dout + om) : nullptr, cap);
     if (rc) return rc;
     wq_route_counters cnt;
-    WQ_HIP(h, hipMemcpyAsync(&cnt, h->route_ws.p, sizeof(cnt), hipMemcpyDeviceToHost, s));
+    WQ_HIP(h, hipMemcpyAsync(&cnt, h->rws.last, sizeof(cnt), hipMemcpyDeviceToHost, s));
     WQ_HIP(h, hipStreamSynchronize(s));
     if (M == 0) cnt.n_pairs = 0;
     *n_pairs = cnt.n_pairs;

@@ -156,11 +156,26 @@ __global__ void k_fill_lists(const uint32_t* __restrict__ st_p, const uint32_t* 
     if (head[i]) list[i + c] = cube_start[c + 1] - (uint32_t)i;
 }
 
-__global__ void k_insert_slots(EvView st, const uint32_t* __restrict__ cube_start, uint32_t n_cubes,
-                               uint32_t* claim, Slot* slots, uint64_t mask, int shift) {
+// Regular cubes -> 128-byte records (one line per lookup); the rest -> 32-byte full-key slots.
+__global__ void k_insert_cubes(EvView st, const uint32_t* __restrict__ cube_start, uint32_t n_cubes,
+                               uint32_t* rclaim, Record* recs, uint64_t rmask, int rshift, uint32_t* claim,
+                               Slot* slots, uint64_t mask, int shift, uint64_t hmask, double sf) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     if (c >= n_cubes) return;
     const uint32_t j = cube_start[c];
+    const uint32_t cnt = cube_start[c + 1] - j;
+    uint64_t pk;
+    if (pack_key(st.w[j], st.kx[j], st.ky[j], st.kz[j], sf, &pk)) {
+        uint64_t s = slot_of(rec_hash(pk) & hmask, rshift);
+        while (atomicCAS(&rclaim[s], 0u, c + 1) != 0u) s = (s + 1) & rmask;
+        Record& r = recs[s];
+        r.pk = pk;
+        r.count = cnt;
+        r.list_off = j + c;
+#pragma unroll 4
+        for (int i = 0; i < kInline; ++i) r.peers[i] = (uint32_t)i < cnt ? st.p[j + i] : 0xFFFFFFFFu;
+        return;
+    }
     uint64_t s = slot_of(st.h[j], shift);
     while (atomicCAS(&claim[s], 0u, c + 1) != 0u) s = (s + 1) & mask;
     Slot r;
@@ -463,10 +478,24 @@ int table_rebuild_derived(wq_router* h) {
     WQ_HIP(h, hipMemsetAsync(t.claim.p, 0, cap * 4, s));
     t.cap = cap;
     t.shift = 64 - log2cap;
+    // record table: load <= 0.3 so a lookup is ~1.2 line reads
+    uint64_t rcap = 1024;
+    int log2r = 10;
+    while (rcap * 3 < 10ull * n_cubes) {
+        rcap <<= 1;
+        log2r++;
+    }
+    WQ_ALLOC(h, t.recs, rcap * sizeof(Record));
+    WQ_ALLOC(h, t.rclaim, rcap * 4);
+    WQ_HIP(h, hipMemsetAsync(t.recs.p, 0, rcap * sizeof(Record), s));
+    WQ_HIP(h, hipMemsetAsync(t.rclaim.p, 0, rcap * 4, s));
+    t.rec_cap = rcap;
+    t.rec_shift = 64 - log2r;
     if (n_cubes)
-        hipLaunchKernelGGL(k_insert_slots, dim3(grid_for(n_cubes)), dim3(kBlock), 0, s, st,
-                           h->cube_start.as<uint32_t>(), n_cubes, t.claim.as<uint32_t>(), t.slots.as<Slot>(),
-                           cap - 1, t.shift);
+        hipLaunchKernelGGL(k_insert_cubes, dim3(grid_for(n_cubes)), dim3(kBlock), 0, s, st,
+                           h->cube_start.as<uint32_t>(), n_cubes, t.rclaim.as<uint32_t>(), t.recs.as<Record>(),
+                           rcap - 1, t.rec_shift, t.claim.as<uint32_t>(), t.slots.as<Slot>(), cap - 1, t.shift,
+                           h->hash_mask, (double)h->cube_size);
     t.n_cubes = n_cubes;
 
     // sorted unique (world << 32 | peer)

@@ -62,6 +62,7 @@ def load_library(build_if_missing: bool = True):
         "wq_profile_enable": ([vp, i32], i32),
         "wq_profile_read": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)], i32),
         "wq_debug_set_hash_bits": ([vp, i32], i32),
+        "wq_debug_set_route_config": ([vp, i32], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -196,6 +197,9 @@ class Router:
         out = np.zeros(max(n.value, 1), dtype=np.uint32)
         self._check(self.lib.wq_world_peers(self.h, world, _p(out), n.value, ctypes.byref(n)))
         return out[: n.value]
+
+    def set_route_config(self, cfg: int) -> None:
+        self._check(self.lib.wq_debug_set_route_config(self.h, cfg))
 
     # ---- instrumentation ----
     def profile_enable(self, on: bool = True) -> None:
