@@ -51,6 +51,25 @@ def algorithmic_bytes(M: int, F: int, P: int) -> int:
     return 69 * M + 4 * F + 8 * P + 4
 
 
+def shard_workload(rank: int, scale: float = 1.0):
+    """World-sharded weak scaling: rank r owns world r (its own peers and its own tick of
+    messages); no message crosses ranks, so there is no exchange step."""
+    from worldql_server_amd import synth
+    return synth.config_c2(scale=scale, world_offset=rank)
+
+
+def reduce_over_ranks(t_ms: float, pairs: int, dev, world_size: int):
+    """(max over ranks of the timed region, sum over ranks of pairs per tick)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([t_ms], dtype=torch.float64, device=dev)
+    p = torch.tensor([float(pairs)], dtype=torch.float64, device=dev)
+    if world_size > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(p, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(p.item())
+
+
 def cpu_baseline(w, seconds: float) -> dict:
     """The C restatement (oracle/wq_oracle.c: hash map world -> cube -> peer set, one message at
     a time), single thread, on a bounded sample of the same tick."""
@@ -92,7 +111,7 @@ def main():
     from worldql_server_amd import abi, synth
     from worldql_server_amd.router import Router
 
-    w = synth.config_c2(scale=a.scale, world_offset=rank)
+    w = shard_workload(rank, a.scale)
     M = len(w.world)
     r = Router(w.cube_size, local_rank)
     stream = torch.cuda.Stream(device=dev)  # a real stream object: its handle is never the NULL stream
@@ -148,13 +167,7 @@ def main():
     if world_size > 1:
         dist.barrier()
     t_ms = ev0.elapsed_time(ev1)
-    t_max = torch.tensor([t_ms], dtype=torch.float64, device=dev)
-    p_all = torch.tensor([float(P)], dtype=torch.float64, device=dev)
-    if world_size > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        dist.all_reduce(p_all, op=dist.ReduceOp.SUM)
-    t_max_ms = float(t_max.item())
-    pairs_all = float(p_all.item())
+    t_max_ms, pairs_all = reduce_over_ranks(t_ms, P, dev, world_size)
 
     # kernel-only time of the route launch: HIP events recorded on the launch stream around
     # every route kernel (wq_profile_enable), separate pass so the headline loop is untouched
