@@ -1,0 +1,66 @@
+// route_common.hpp — shared constants and wave/LDS helpers of the route kernels (wq_route.hip).
+#pragma once
+#include <algorithm>
+
+#include "wq_internal.hpp"
+
+namespace wq {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+// locator (info.x)
+constexpr uint32_t kLocGlobal = 0x80000000u;  // offset of the full list in `list`
+constexpr uint32_t kLocSelf = 0x40000000u;    // the one recipient is the sender
+constexpr uint32_t kLocMask = 0x3FFFFFFFu;    // otherwise: record slot (inline list)
+// info.y for an inline record: count << 24 | skipped index (kSkipNone24 = none)
+constexpr uint32_t kSkipNone24 = 0xFFFFFFu;
+// emit base[]
+constexpr uint32_t kGlobal = 0x80000000u;        // index into `list`, not the stage
+constexpr uint32_t kSelfSentinel = 0xFFFFFFFFu;  // the recipient is the sender (stage overflow)
+
+__device__ __forceinline__ uint32_t wave_incl_scan_add(uint32_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan_max(uint32_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v = v > t ? v : t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// Workgroup barrier that orders LDS only: global loads stay in flight across it (a plain
+// __syncthreads() also waits vmcnt(0)). No kernel here hands global memory between threads of
+// one workgroup.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Message q (0 .. 64*IPT-1) of wave w sits at strided tile index (q/64)*256 + w*64 + q%64.
+template <int IPT>
+__device__ __forceinline__ uint32_t wave_msg(int wave, uint32_t q) {
+    return (q >> 6) * kBlock + wave * 64 + (q & 63);
+}
+
+struct RouteIn {
+    const double* pos;
+    const int64_t* keys;
+    const uint32_t* world;
+    const uint32_t* sender;
+    const uint8_t* repl;
+    uint32_t M;
+    int64_t si;
+};
+
+}  // namespace wq

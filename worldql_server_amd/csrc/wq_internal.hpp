@@ -59,15 +59,14 @@ struct Table {
     uint64_t n_cubes = 0, n_any = 0;
 };
 
-// Route workspace, persistent across calls so a tick needs no memset: a monotonic scan-tile
-// ticket, two counter slots (each call zeroes the next call's), epoch-tagged scan status words,
-// and the per-message locators the count pass hands to the emit pass.
+// Route workspace, persistent across calls so a tick needs no memset: two counter slots (each
+// call's count pass zeroes the next call's) and the per-message state the count pass hands to
+// the scan and emit passes.
 struct RouteWs {
-    DevBuf buf;
-    DevBuf info;  // uint2[M]
-    uint64_t status_cap = 0;
-    uint64_t ticket_base = 0;
-    uint32_t epoch = 0;
+    DevBuf buf;    // [pad 64][wq_route_counters x2]
+    DevBuf info;   // uint2[M]: locators, count pass -> emit pass
+    DevBuf e;      // u32[M]: filtered counts
+    DevBuf tiles;  // u32[2 * n_count_blocks]: block totals, then their exclusive prefix
     uint64_t calls = 0;
     wq_route_counters* last = nullptr;  // counters of the most recent call (device)
 };
