@@ -139,6 +139,42 @@ int wq_world_peers(wq_router* h, uint32_t world, uint32_t* out, size_t capacity,
 int wq_quantize(const double* coords, size_t n, uint16_t cube_size, int64_t* out);
 int wq_quantize_device(wq_router* h, const double* d_coords, size_t n, int64_t* d_out);
 
+/* ---- multi-GPU: cube-hash ownership ----
+ * The reference is single-process (one WorldMap owned by one task, thread.rs:113-148); these
+ * entry points partition that one table over G GPUs without changing any result. Each (world,
+ * cube) bucket has one owner shard in [0, G) computed from the QUANTISED key, so the owner
+ * holds every subscription a message to that cube can reach. A sharded tick is
+ *   wq_shard_messages_device -> all-to-all of the records (RCCL) -> wq_route_records_device on
+ *   the owner -> all-to-all of per-message counts and peers back to the ingesting GPU.
+ * worldql_server_amd/sharded.py drives it over torch.distributed. */
+#define WQ_MAX_SHARDS 64
+#define WQ_SHARD_ALL 0xFFFFFFFFu /* owner of a REMOVE_PEER op: every shard */
+
+/* One message on the wire between GPUs (40 bytes): its quantised CubeArea, world, sender,
+ * index in the ingesting GPU's batch, and replication code. */
+typedef struct wq_msg_rec {
+    int64_t key[3];
+    uint32_t world;
+    uint32_t sender;
+    uint32_t msg;
+    uint8_t repl;
+    uint8_t pad_[3];
+} wq_msg_rec;
+
+/* Owner shard of each op (host arrays); REMOVE_PEER ops get WQ_SHARD_ALL. Each shard applies,
+ * in array order, the ops it owns plus every REMOVE_PEER (area_subscribe.rs / area_unsubscribe.rs
+ * / thread.rs:124-125 on the owner). */
+int wq_shard_ops(wq_router* h, const wq_op* ops, size_t n, uint32_t n_shards, uint32_t* owner);
+/* Quantise (or take raw keys), compute owners and write the records grouped by owner, stable in
+ * message order: d_out[M] and d_counts[n_shards] (device). Asynchronous on the handle's stream. */
+int wq_shard_messages_device(wq_router* h, const double* d_pos, const int64_t* d_keys,
+                             const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
+                             size_t n_msgs, uint32_t n_shards, wq_msg_rec* d_out, uint32_t* d_counts);
+/* wq_route_tick_device on received records (the owner side of a sharded tick). */
+int wq_route_records_device(wq_router* h, const wq_msg_rec* d_recs, size_t n_msgs, uint32_t* d_offsets,
+                            uint32_t* d_peers, uint32_t* d_msgs, size_t capacity,
+                            wq_route_counters* d_counters);
+
 /* ---- instrumentation ----
  * When enabled, every route launch is bracketed by HIP events on the launch stream;
  * wq_profile_read returns the summed kernel-only milliseconds and launch count (and resets). */

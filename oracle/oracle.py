@@ -226,3 +226,35 @@ def sort_within_segments(offsets: np.ndarray, values: np.ndarray) -> None:
     seg = np.repeat(np.arange(len(offsets) - 1, dtype=np.int64), np.diff(offsets.astype(np.int64)))
     order = np.lexsort((values, seg))
     values[:] = values[order]
+
+
+# ---- cube-hash ownership (restates csrc/wq_device.hpp cube_hash + csrc/wq_shard.hip shard_of) ----
+# Not a reference function (the reference is single-process); checked so the GPU owners and the
+# CPU sharding tests agree on where every bucket lives.
+def _as_u64(a) -> np.ndarray:
+    a = np.asarray(a)
+    return a if a.dtype == np.uint64 else a.astype(np.int64).view(np.uint64)
+
+
+def cube_hash_np(w, x, y, z) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        u = _as_u64
+        h = u(x) * np.uint64(0x9E3779B97F4A7C15)
+        h ^= u(y) * np.uint64(0xC2B2AE3D27D4EB4F)
+        h ^= u(z) * np.uint64(0x165667B19E3779F9)
+        h ^= (np.asarray(w, dtype=np.uint64) + np.uint64(0x27D4EB2F165667C5)) * np.uint64(0xD6E8FEB86659FD93)
+        h ^= h >> np.uint64(32)
+        h *= np.uint64(0xD6E8FEB86659FD93)
+        h ^= h >> np.uint64(29)
+        h *= np.uint64(0x94D049BB133111EB)
+        h ^= h >> np.uint64(32)
+    return h
+
+
+def shard_of_np(w, x, y, z, n_shards: int) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        v = cube_hash_np(w, x, y, z)
+        v ^= v >> np.uint64(31)
+        v *= np.uint64(0xBF58476D1CE4E5B9)
+        v ^= v >> np.uint64(29)
+        return (((v >> np.uint64(32)) * np.uint64(n_shards)) >> np.uint64(32)).astype(np.uint32)

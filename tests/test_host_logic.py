@@ -91,6 +91,8 @@ def host_shim(tmp_path_factory):
     lib.wq_test_coord_clamp_host.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint16, ctypes.c_void_p]
     lib.wq_test_cube_hash_host.restype = ctypes.c_uint64
     lib.wq_test_cube_hash_host.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64]
+    lib.wq_test_shard_of_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+                                          ctypes.c_void_p]
     return lib
 
 
@@ -124,6 +126,23 @@ def test_cube_hash_host_instance_is_stable(host_shim):
     b = host_shim.wq_test_cube_hash_host(1, 16, 16, 16)
     c = host_shim.wq_test_cube_hash_host(0, 16, 16, 32)
     assert len({a, b, c}) == 3
+
+
+def test_shard_owner_host_instance_matches_oracle(host_shim):
+    """shard_of (csrc/wq_device.hpp) == oracle.shard_of_np: where every bucket lives."""
+    rng = synth.SplitMix64(7)
+    n = 50_000
+    w = (rng.next_u64(n) % np.uint64(70)).astype(np.uint32)
+    k = rng.next_u64(3 * n).view(np.int64).copy()
+    k[: 3 * n // 2] = (k[: 3 * n // 2] % 4096) * 16  # on-grid keys
+    for G in (1, 2, 3, 8, 64):
+        out = np.empty(n, np.uint32)
+        host_shim.wq_test_shard_of_host(w.ctypes.data, k.ctypes.data, n, G, out.ctypes.data)
+        ref = orc.shard_of_np(w, k[0::3], k[1::3], k[2::3], G)
+        assert (out == ref).all(), G
+        assert out.max() < G
+        if G > 1:  # owners spread evenly
+            assert np.bincount(out, minlength=G).min() > 0.8 * n / G
 
 
 # ---- flush-on-reorder batching, with the C oracle standing in for the GPU table -------------

@@ -72,3 +72,16 @@ def ops_array(world, peer, kind, pos=None, key=None) -> np.ndarray:
 def concat_ops(parts) -> np.ndarray:
     """np.concatenate drops the union layout of OP_DTYPE; join the raw 40-byte records instead."""
     return np.concatenate([np.ascontiguousarray(p, dtype=OP_DTYPE).view(np.uint8) for p in parts]).view(OP_DTYPE)
+
+
+# ---- multi-GPU (include/wq_router.h, "cube-hash ownership") ----
+MAX_SHARDS = 64
+SHARD_ALL = 0xFFFFFFFF  # owner of a REMOVE_PEER op
+
+# struct wq_msg_rec: 40 bytes on the wire between GPUs
+MSG_REC_DTYPE = np.dtype({
+    "names": ["key", "world", "sender", "msg", "repl"],
+    "formats": [(np.int64, 3), np.uint32, np.uint32, np.uint32, np.uint8],
+    "offsets": [0, 24, 28, 32, 36],
+    "itemsize": 40,
+})

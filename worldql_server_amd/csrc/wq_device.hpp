@@ -65,6 +65,16 @@ __host__ __device__ __forceinline__ uint64_t cube_hash(uint32_t w, int64_t x, in
     return h;
 }
 
+// Owner of a bucket. Decorrelated from rec_hash / the slot hash (both use cube_hash directly), so
+// a shard's local table still spreads over all of its slots. Never affected by hash_bits.
+__host__ __device__ __forceinline__ uint32_t shard_of(uint32_t w, int64_t x, int64_t y, int64_t z, uint32_t G) {
+    uint64_t v = cube_hash(w, x, y, z);
+    v ^= v >> 31;
+    v *= 0xBF58476D1CE4E5B9ull;
+    v ^= v >> 29;
+    return (uint32_t)(((v >> 32) * (uint64_t)G) >> 32);
+}
+
 // ---- bucket records (the table the hot path probes) --------------------------------------
 // A "regular" cube — world < 1023 and every key coordinate an exact multiple k = a*s of the cube
 // size with a in [-2^17, 2^17) — has an exact 64-bit packed key

@@ -97,6 +97,8 @@ struct wq_router {
     wq::DevBuf cube_id, cube_start;
 
     wq::RouteWs rws;
+    // sharded ticks (wq_shard.hip): owner histograms, unpacked received records
+    wq::DevBuf shard_hist, rec_keys, rec_w, rec_s, rec_r;
     int route_cfg = 0;  // route kernel shapes (wq_route.hip kCfgs)
     // host-pointer convenience buffers
     wq::DevBuf h_in, h_out;

@@ -18,6 +18,12 @@ int launch_is_subscribed(wq_router* h, const uint32_t* d_w, const uint32_t* d_p,
 int launch_is_subscribed_any(wq_router* h, const uint32_t* d_w, const uint32_t* d_p, uint32_t n, uint8_t* d_out);
 int launch_world_range(wq_router* h, uint32_t w, uint64_t* d_out);
 int launch_low32(wq_router* h, const uint64_t* d_in, uint64_t n, uint32_t* d_out);
+int launch_shard_messages(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                          const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, wq_msg_rec* d_out,
+                          uint32_t* d_counts);
+int launch_op_owner(wq_router* h, const wq_op* d_ops, size_t n, uint32_t G, uint32_t* d_owner);
+int launch_route_records(wq_router* h, const wq_msg_rec* d_recs, size_t M, uint32_t* d_offsets, uint32_t* d_peers,
+                         uint32_t* d_msgs, size_t capacity);
 }  // namespace wq
 
 using namespace wq;
@@ -93,8 +99,9 @@ int wq_router_destroy(wq_router* h) {
                       &h->ev_h, &h->ev_w, &h->ev_kx, &h->ev_ky, &h->ev_kz, &h->ev_p, &h->ev_kind,
                       &h->d_ops, &h->idx_a, &h->idx_b, &h->key32_a, &h->key32_b, &h->key64_a,
                       &h->key64_b, &h->flags, &h->scan, &h->sort_tmp, &h->small, &h->cube_id,
-                      &h->cube_start, &h->rws.buf, &h->rws.info, &h->h_in, &h->h_out,
-                      &h->tab.recs, &h->tab.rclaim};
+                      &h->cube_start, &h->rws.buf, &h->rws.info, &h->rws.e, &h->rws.tiles,
+                      &h->h_in, &h->h_out, &h->tab.recs, &h->tab.rclaim, &h->shard_hist,
+                      &h->rec_keys, &h->rec_w, &h->rec_s, &h->rec_r};
     for (DevBuf* b : bufs) b->release();
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -238,6 +245,48 @@ int wq_route_tick(wq_router* h, const double* pos, const int64_t* keys, const ui
     }
     WQ_HIP(h, hipStreamSynchronize(s));
     if (P > capacity) return set_error(h, WQ_E_CAPACITY, "output capacity too small (required size in *n_pairs)");
+    return WQ_OK;
+}
+
+int wq_shard_ops(wq_router* h, const wq_op* ops, size_t n, uint32_t n_shards, uint32_t* owner) {
+    if (!h || (n && (!ops || !owner)) || n_shards == 0 || n_shards > WQ_MAX_SHARDS) return WQ_E_INVALID;
+    if (n == 0) return WQ_OK;
+    if (n >= 0xFFFFFFFFull) return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    const size_t o_o = align256(n * sizeof(wq_op));
+    WQ_ALLOC(h, h->h_in, o_o + n * 4);
+    char* d = h->h_in.as<char>();
+    hipStream_t s = h->stream;
+    WQ_HIP(h, hipMemcpyAsync(d, ops, n * sizeof(wq_op), hipMemcpyHostToDevice, s));
+    int rc = launch_op_owner(h, reinterpret_cast<const wq_op*>(d), n, n_shards, reinterpret_cast<uint32_t*>(d + o_o));
+    if (rc) return rc;
+    WQ_HIP(h, hipMemcpyAsync(owner, d + o_o, n * 4, hipMemcpyDeviceToHost, s));
+    WQ_HIP(h, hipStreamSynchronize(s));
+    return WQ_OK;
+}
+
+int wq_shard_messages_device(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                             const uint32_t* d_sender, const uint8_t* d_repl, size_t n_msgs, uint32_t n_shards,
+                             wq_msg_rec* d_out, uint32_t* d_counts) {
+    if (!h || !d_counts || n_shards == 0 || n_shards > WQ_MAX_SHARDS ||
+        (n_msgs && (!d_world || !d_sender || !d_repl || (!d_pos && !d_keys) || !d_out)))
+        return WQ_E_INVALID;
+    if (n_msgs >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
+    WQ_HIP(h, hipSetDevice(h->device));
+    return launch_shard_messages(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, n_shards, d_out, d_counts);
+}
+
+int wq_route_records_device(wq_router* h, const wq_msg_rec* d_recs, size_t n_msgs, uint32_t* d_offsets,
+                            uint32_t* d_peers, uint32_t* d_msgs, size_t capacity, wq_route_counters* d_counters) {
+    if (!h || !d_offsets || (n_msgs && !d_recs) || (capacity && !d_peers)) return WQ_E_INVALID;
+    if (n_msgs >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
+    if (capacity > 0xFFFFFFFFull) capacity = 0xFFFFFFFFull;
+    WQ_HIP(h, hipSetDevice(h->device));
+    int rc = launch_route_records(h, d_recs, n_msgs, d_offsets, d_peers, d_msgs, capacity);
+    if (rc) return rc;
+    if (d_counters)
+        WQ_HIP(h, hipMemcpyAsync(d_counters, h->rws.last, sizeof(wq_route_counters), hipMemcpyDeviceToDevice,
+                                 h->stream));
     return WQ_OK;
 }
 

@@ -1,0 +1,273 @@
+// wq_shard.hip — cube-hash ownership for the multi-GPU path.
+//
+// Every (world, cube) bucket is independent, so the table is partitioned by a hash of the
+// quantised key: owner(world, key) = shard_of(...) in [0, G). A tick on G GPUs is
+//   (1) shard_messages: quantise each ingested message (kernel 1), compute its owner, and group
+//       the messages by owner into 40-byte records, stable in message order (three launches:
+//       per-block owner histograms -> one flat scan -> ballot-ranked scatter);
+//   (2) an RCCL all-to-all of the records (host side: worldql_server_amd/sharded.py);
+//   (3) route_records: the single-GPU route (count / scan / emit) on the received records —
+//       keys are already quantised, so the count pass takes its raw-key branch;
+//   (4) the pairs return to the ingesting GPU with a second all-to-all.
+// Subscription ops go to the owner of their cube (op_owner_kernel); REMOVE_PEER goes to all.
+// The per-message body that runs on the owner is still local_message.rs:52-86.
+#include "route_common.hpp"
+
+namespace wq {
+
+constexpr int kShardIPT = 4;                  // messages per thread
+constexpr uint32_t kShardTile = kBlock * kShardIPT;
+constexpr int kScanThreads1 = 1024;
+
+static_assert(sizeof(wq_msg_rec) == 40, "wq_msg_rec is 40 bytes");
+
+struct ShardIn {
+    const double* pos;
+    const int64_t* keys;
+    const uint32_t* world;
+    const uint32_t* sender;
+    const uint8_t* repl;
+    uint32_t M;
+    uint32_t G;
+    uint32_t nblk;
+    double sf;
+    int64_t si;
+};
+
+template <bool RAW>
+__device__ __forceinline__ void msg_key(const ShardIn& in, uint32_t m, int64_t& x, int64_t& y, int64_t& z) {
+    if (RAW) {
+        x = in.keys[3ull * m];
+        y = in.keys[3ull * m + 1];
+        z = in.keys[3ull * m + 2];
+    } else {
+        x = coord_clamp_dev(in.pos[3ull * m], in.sf, in.si);
+        y = coord_clamp_dev(in.pos[3ull * m + 1], in.sf, in.si);
+        z = coord_clamp_dev(in.pos[3ull * m + 2], in.sf, in.si);
+    }
+}
+
+// (1a) per-block owner histogram, stored owner-major: counts[d * nblk + b]. A flat exclusive scan
+// of that array is then directly each (owner, block) pair's first output slot.
+template <bool RAW>
+__global__ void __launch_bounds__(kBlock) shard_count_kernel(ShardIn in, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t cnt[WQ_MAX_SHARDS];
+    for (uint32_t d = threadIdx.x; d < in.G; d += kBlock) cnt[d] = 0;
+    __syncthreads();
+    const uint32_t m0 = blockIdx.x * kShardTile + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint32_t m = m0 + i * kBlock;
+        if (m < in.M) {
+            int64_t x, y, z;
+            msg_key<RAW>(in, m, x, y, z);
+            atomicAdd(&cnt[shard_of(in.world[m], x, y, z, in.G)], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < in.G; d += kBlock) counts[(uint64_t)d * in.nblk + blockIdx.x] = cnt[d];
+}
+
+// (1b) one block: exclusive scan of the n = G * nblk histogram entries in place; per-owner totals.
+__global__ void __launch_bounds__(kScanThreads1)
+    shard_scan_kernel(uint32_t* __restrict__ v, uint32_t nblk, uint32_t G, uint32_t* __restrict__ dest_counts) {
+    __shared__ uint32_t wsum[kScanThreads1 / 64];
+    __shared__ uint32_t carry_s;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t n = nblk * G;
+    if (threadIdx.x == 0) carry_s = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < n; base += kScanThreads1) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t x = i < n ? v[i] : 0;
+        const uint32_t inc = wave_incl_scan_add(x, lane);
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        if (wave == 0) {
+            const uint32_t s = lane < kScanThreads1 / 64 ? wsum[lane] : 0;
+            const uint32_t si = wave_incl_scan_add(s, lane);
+            if (lane < kScanThreads1 / 64) wsum[lane] = si - s;
+        }
+        __syncthreads();
+        const uint32_t carry = carry_s;
+        if (i < n) v[i] = carry + wsum[wave] + inc - x;
+        __syncthreads();
+        if (threadIdx.x == kScanThreads1 - 1) carry_s = carry + wsum[wave] + inc;
+        __syncthreads();
+    }
+    // v is visible to this block after the last barrier (same workgroup, global memory, fenced).
+    __threadfence_block();
+    const uint32_t total = carry_s;
+    for (uint32_t d = threadIdx.x; d < G; d += kScanThreads1) {
+        const uint32_t lo = v[(uint64_t)d * nblk];
+        const uint32_t hi = d + 1 < G ? v[(uint64_t)(d + 1) * nblk] : total;
+        dest_counts[d] = hi - lo;
+    }
+}
+
+// (1c) stable scatter. Message order inside a block is (iteration, wave, lane); each wave ranks
+// its messages per owner with ballots (one round per distinct owner in the wave), the 4*IPT
+// (iteration, wave) groups are scanned per owner in LDS, and the scanned histogram gives the
+// block's first slot per owner.
+template <bool RAW>
+__global__ void __launch_bounds__(kBlock)
+    shard_scatter_kernel(ShardIn in, const uint32_t* __restrict__ base, wq_msg_rec* __restrict__ out) {
+    __shared__ uint32_t wc[kShardIPT * kWaves][WQ_MAX_SHARDS];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t k = threadIdx.x; k < kShardIPT * kWaves * WQ_MAX_SHARDS; k += kBlock) (&wc[0][0])[k] = 0;
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1;
+    const uint32_t m0 = blockIdx.x * kShardTile + threadIdx.x;
+    int64_t kx[kShardIPT], ky[kShardIPT], kz[kShardIPT];
+    uint32_t own[kShardIPT], rank[kShardIPT];
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint32_t m = m0 + i * kBlock;
+        const bool valid = m < in.M;
+        own[i] = 0xFFFFFFFFu;
+        rank[i] = 0;
+        if (valid) {
+            msg_key<RAW>(in, m, kx[i], ky[i], kz[i]);
+            own[i] = shard_of(in.world[m], kx[i], ky[i], kz[i], in.G);
+        }
+        uint64_t todo = __ballot(valid);
+        while (todo) {
+            const int leader = __ffsll((unsigned long long)todo) - 1;
+            const uint32_t d = __shfl(own[i], leader, 64);
+            const uint64_t mask = __ballot(own[i] == d);
+            if (own[i] == d) rank[i] = __popcll(mask & lt);
+            if (lane == leader) wc[i * kWaves + wave][d] = __popcll(mask);
+            todo &= ~mask;
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < in.G; d += kBlock) {
+        uint32_t run = base[(uint64_t)d * in.nblk + blockIdx.x];
+#pragma unroll
+        for (int k = 0; k < kShardIPT * kWaves; ++k) {
+            const uint32_t t = wc[k][d];
+            wc[k][d] = run;
+            run += t;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint32_t m = m0 + i * kBlock;
+        if (m < in.M) {
+            wq_msg_rec r;
+            r.key[0] = kx[i];
+            r.key[1] = ky[i];
+            r.key[2] = kz[i];
+            r.world = in.world[m];
+            r.sender = in.sender[m];
+            r.msg = m;
+            r.repl = in.repl[m];
+            r.pad_[0] = r.pad_[1] = r.pad_[2] = 0;
+            out[wc[i * kWaves + wave][own[i]] + rank[i]] = r;
+        }
+    }
+}
+
+__global__ void op_owner_kernel(const wq_op* __restrict__ ops, uint32_t n, double sf, int64_t si, uint32_t G,
+                                uint32_t* __restrict__ owner) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const wq_op op = ops[i];
+    if (op.kind == WQ_OP_REMOVE_PEER) {
+        owner[i] = WQ_SHARD_ALL;
+        return;
+    }
+    int64_t x, y, z;
+    if (op.key_is_raw) {
+        x = op.u.key[0];
+        y = op.u.key[1];
+        z = op.u.key[2];
+    } else {
+        x = coord_clamp_dev(op.u.pos[0], sf, si);
+        y = coord_clamp_dev(op.u.pos[1], sf, si);
+        z = coord_clamp_dev(op.u.pos[2], sf, si);
+    }
+    owner[i] = shard_of(op.world, x, y, z, G);
+}
+
+// Records -> the SoA inputs of the route passes (keys are already quantised).
+__global__ void unpack_records_kernel(const wq_msg_rec* __restrict__ r, uint32_t M, int64_t* __restrict__ keys,
+                                      uint32_t* __restrict__ world, uint32_t* __restrict__ sender,
+                                      uint8_t* __restrict__ repl) {
+    const uint32_t m = blockIdx.x * kBlock + threadIdx.x;
+    if (m >= M) return;
+    const wq_msg_rec x = r[m];
+    keys[3ull * m] = x.key[0];
+    keys[3ull * m + 1] = x.key[1];
+    keys[3ull * m + 2] = x.key[2];
+    world[m] = x.world;
+    sender[m] = x.sender;
+    repl[m] = x.repl;
+}
+
+int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                 const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t* d_offsets,
+                 uint32_t* d_peers, uint32_t* d_msgs, size_t capacity);
+
+int launch_shard_messages(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                          const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, wq_msg_rec* d_out,
+                          uint32_t* d_counts) {
+    hipStream_t s = h->stream;
+    if (M == 0) {
+        WQ_HIP(h, hipMemsetAsync(d_counts, 0, G * 4, s));
+        return WQ_OK;
+    }
+    ShardIn in;
+    in.pos = d_pos;
+    in.keys = d_keys;
+    in.world = d_world;
+    in.sender = d_sender;
+    in.repl = d_repl;
+    in.M = (uint32_t)M;
+    in.G = G;
+    in.nblk = (uint32_t)((M + kShardTile - 1) / kShardTile);
+    in.sf = (double)h->cube_size;
+    in.si = (int64_t)h->cube_size;
+    WQ_ALLOC(h, h->shard_hist, (uint64_t)in.nblk * G * 4);
+    uint32_t* hist = h->shard_hist.as<uint32_t>();
+    if (d_keys)
+        hipLaunchKernelGGL((shard_count_kernel<true>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist);
+    else
+        hipLaunchKernelGGL((shard_count_kernel<false>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist);
+    WQ_HIP(h, hipGetLastError());
+    hipLaunchKernelGGL(shard_scan_kernel, dim3(1), dim3(kScanThreads1), 0, s, hist, in.nblk, G, d_counts);
+    WQ_HIP(h, hipGetLastError());
+    if (d_keys)
+        hipLaunchKernelGGL((shard_scatter_kernel<true>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist, d_out);
+    else
+        hipLaunchKernelGGL((shard_scatter_kernel<false>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist, d_out);
+    WQ_HIP(h, hipGetLastError());
+    return WQ_OK;
+}
+
+int launch_op_owner(wq_router* h, const wq_op* d_ops, size_t n, uint32_t G, uint32_t* d_owner) {
+    if (n == 0) return WQ_OK;
+    hipLaunchKernelGGL(op_owner_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, h->stream,
+                       d_ops, (uint32_t)n, (double)h->cube_size, (int64_t)h->cube_size, G, d_owner);
+    WQ_HIP(h, hipGetLastError());
+    return WQ_OK;
+}
+
+int launch_route_records(wq_router* h, const wq_msg_rec* d_recs, size_t M, uint32_t* d_offsets, uint32_t* d_peers,
+                         uint32_t* d_msgs, size_t capacity) {
+    WQ_ALLOC(h, h->rec_keys, M * 24 + 256);
+    WQ_ALLOC(h, h->rec_w, M * 4 + 256);
+    WQ_ALLOC(h, h->rec_s, M * 4 + 256);
+    WQ_ALLOC(h, h->rec_r, M + 256);
+    if (M) {
+        hipLaunchKernelGGL(unpack_records_kernel, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           h->stream, d_recs, (uint32_t)M, h->rec_keys.as<int64_t>(), h->rec_w.as<uint32_t>(),
+                           h->rec_s.as<uint32_t>(), h->rec_r.as<uint8_t>());
+        WQ_HIP(h, hipGetLastError());
+    }
+    return launch_route(h, nullptr, h->rec_keys.as<int64_t>(), h->rec_w.as<uint32_t>(), h->rec_s.as<uint32_t>(),
+                        h->rec_r.as<uint8_t>(), M, d_offsets, d_peers, d_msgs, capacity);
+}
+
+}  // namespace wq

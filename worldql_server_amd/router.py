@@ -63,6 +63,9 @@ def load_library(build_if_missing: bool = True):
         "wq_profile_read": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)], i32),
         "wq_debug_set_hash_bits": ([vp, i32], i32),
         "wq_debug_set_route_config": ([vp, i32], i32),
+        "wq_shard_ops": ([vp, vp, sz, u32, vp], i32),
+        "wq_shard_messages_device": ([vp, vp, vp, vp, vp, vp, sz, u32, vp, vp], i32),
+        "wq_route_records_device": ([vp, vp, sz, vp, vp, vp, sz, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -168,6 +171,28 @@ class Router:
         self._check(self.lib.wq_route_tick_device(self.h, pos_ptr or None, keys_ptr or None, world_ptr, sender_ptr,
                                                   repl_ptr, n_msgs, offsets_ptr, peers_ptr or None,
                                                   msgs_ptr or None, capacity, counters_ptr or None))
+
+    # ---- multi-GPU (cube-hash ownership; driven by sharded.py) ----
+    def shard_ops(self, ops: np.ndarray, n_shards: int) -> np.ndarray:
+        """Owner shard of each op (abi.SHARD_ALL for REMOVE_PEER)."""
+        ops = np.ascontiguousarray(ops, dtype=abi.OP_DTYPE)
+        out = np.empty(len(ops), dtype=np.uint32)
+        self._check(self.lib.wq_shard_ops(self.h, _p(ops), len(ops), n_shards, _p(out)))
+        return out
+
+    def shard_messages_device(self, pos_ptr: int | None, keys_ptr: int | None, world_ptr: int, sender_ptr: int,
+                              repl_ptr: int, n_msgs: int, n_shards: int, recs_ptr: int, counts_ptr: int) -> None:
+        """Group a tick's messages by owner shard into 40-byte records (asynchronous)."""
+        self._check(self.lib.wq_shard_messages_device(self.h, pos_ptr or None, keys_ptr or None, world_ptr or None,
+                                                      sender_ptr or None, repl_ptr or None, n_msgs, n_shards,
+                                                      recs_ptr or None, counts_ptr))
+
+    def route_records_device(self, recs_ptr: int | None, n_msgs: int, offsets_ptr: int, peers_ptr: int | None,
+                             msgs_ptr: int | None, capacity: int, counters_ptr: int | None = None) -> None:
+        """Route received records on this shard (asynchronous)."""
+        self._check(self.lib.wq_route_records_device(self.h, recs_ptr or None, n_msgs, offsets_ptr,
+                                                     peers_ptr or None, msgs_ptr or None, capacity,
+                                                     counters_ptr or None))
 
     def set_stream(self, stream_ptr: int | None) -> None:
         self._check(self.lib.wq_set_stream(self.h, stream_ptr or None))
