@@ -12,9 +12,13 @@ U[-512,512)^3, cube_size 16, ExceptSelf, synthetic (splitmix64). The table is bu
 one full tick of the hot path on HBM-resident inputs: quantise -> probe -> filter -> compact into
 CSR offsets + (msg, peer) pairs, the launch that also resolves the tick's global output offsets.
 
-Multi-GPU: world-sharded weak scaling — every rank owns its own world (its own 100k peers and
-1M messages per tick); the path has no data exchange, so there is no collective in the timed
-region. value = pairs of all ranks / max-over-ranks time.
+Multi-GPU (weak scaling, value = pairs of all ranks / max-over-ranks time):
+  --shard world (default)  every rank owns its own world (its own 100k peers and 1M messages per
+                           tick); no message crosses ranks, so no collective in the timed region.
+  --shard cube             one world G times the C2 volume (100k*G peers); every rank ingests 1M
+                           messages anywhere in it, and the tick runs the cube-hash sharded path
+                           (worldql_server_amd/sharded.py): owner grouping, RCCL all-to-all of the
+                           records, route on the owner, all-to-all of the pairs back.
 """
 from __future__ import annotations
 
@@ -41,6 +45,8 @@ def parse():
     ap.add_argument("--scale", type=float, default=1.0, help="shrink C2 (tests only; 1.0 = the headline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline's routing work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", choices=["world", "cube"], default="world",
+                    help="multi-GPU partitioning (see module docstring)")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "r01_pmc_route.json"))
     return ap.parse_args()
 
@@ -56,6 +62,19 @@ def shard_workload(rank: int, scale: float = 1.0):
     messages); no message crosses ranks, so there is no exchange step."""
     from worldql_server_amd import synth
     return synth.config_c2(scale=scale, world_offset=rank)
+
+
+def cube_workload(rank: int, world_size: int, scale: float = 1.0):
+    """Cube-hash weak scaling: one world of G x the C2 volume and peers; every rank generates the
+    same subscription stream and ingests its own 1M-message slice of the tick."""
+    from worldql_server_amd import synth
+    G = world_size
+    n_peers = max(1, int(round(100_000 * scale * G)))
+    n_msgs = max(1, int(round(1_000_000 * scale))) * G
+    half = 512.0 * ((scale * G) ** (1.0 / 3.0))
+    w = synth.uniform_box(2, n_peers, n_msgs, half, neighbourhood=True)
+    lo, hi = rank * n_msgs // G, (rank + 1) * n_msgs // G
+    return w, lo, hi
 
 
 def reduce_over_ranks(t_ms: float, pairs: int, dev, world_size: int):
@@ -108,7 +127,10 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
-    from worldql_server_amd import abi, synth
+    if a.shard == "cube":
+        return run_cube(a, rank, world_size, local_rank, dev)
+
+    from worldql_server_amd import abi
     from worldql_server_amd.router import Router
 
     w = shard_workload(rank, a.scale)
@@ -208,10 +230,94 @@ def main():
         },
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "route_kernel", "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
+                     "kernel": "route tick (count + tile_scan + emit)", "kernel_avg_us": k_avg_s * 1e6,
+                     "algorithmic_bytes": B},
     }
     if rank == 0 and world_size == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(w, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    r.close()
+    if world_size > 1:
+        dist.destroy_process_group()
+
+
+def run_cube(a, rank, world_size, local_rank, dev):
+    """--shard cube: the cube-hash sharded tick, timed end to end (exchanges included)."""
+    import torch
+    import torch.distributed as dist
+    from worldql_server_amd.router import Router
+    from worldql_server_amd.sharded import DeviceShard, DistExchange, LocalExchange, ShardedRouter
+
+    w, lo, hi = cube_workload(rank, world_size, a.scale)
+    stream = torch.cuda.Stream(device=dev)
+    r = Router(w.cube_size, local_rank)
+    be = DeviceShard(r, stream)
+    sr = ShardedRouter(be, DistExchange() if world_size > 1 else LocalExchange())
+    t0 = time.perf_counter()
+    sr.apply_ops(w.ops)
+    build_s = time.perf_counter() - t0
+    st = r.stats()
+    M = hi - lo
+    with torch.cuda.stream(stream):
+        pos = torch.from_numpy(w.pos[lo:hi]).to(dev)
+        world = torch.from_numpy(w.world[lo:hi].view(np.int32)).to(dev)
+        sender = torch.from_numpy(w.sender[lo:hi].view(np.int32)).to(dev)
+        repl = torch.from_numpy(w.repl[lo:hi]).to(dev)
+        for _ in range(max(a.warmup, 1)):
+            res = sr.tick(world, sender, repl, pos=pos)
+        stream.synchronize()
+        P_in = int(res.peers.shape[0])  # pairs of the messages this rank ingested
+        P_own, F_own = be.read_counters()  # pairs / candidates routed on this shard
+        R = sr.last_recv
+        if world_size > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t_wall = time.perf_counter()
+        for _ in range(a.steps):
+            res = sr.tick(world, sender, repl, pos=pos)
+        torch.cuda.synchronize(dev)
+        t_ms = (time.perf_counter() - t_wall) * 1e3
+        if world_size > 1:
+            dist.barrier()
+        t_max_ms, pairs_all = reduce_over_ranks(t_ms, P_in, dev, world_size)
+        r.profile_enable(True)
+        for _ in range(a.steps):
+            sr.tick(world, sender, repl, pos=pos)
+        k_ms, launches = r.profile_read()
+        r.profile_enable(False)
+    k_avg_s = k_ms / launches / 1e3
+    B = algorithmic_bytes(R, F_own, P_own)
+    achieved = B / k_avg_s / 1e9
+    out = {
+        "metric": METRIC,
+        "value": pairs_all * a.steps / (t_max_ms / 1e3),
+        "unit": "pairs/s",
+        "n_gpus": world_size,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": t_max_ms / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (splitmix64, SURVEY.md §8(d) C2 generator, volume and peers x n_gpus)",
+        "config": {
+            "workload": f"C2 x{world_size}: 1 world, {w.n_peers} peers x 3x3x3 cubes, 1M LocalMessages/GPU/tick, "
+                        "cube_size 16, ExceptSelf" + ("" if a.scale == 1.0 else f" (scaled {a.scale})"),
+            "messages_per_tick": M * world_size, "messages_per_gpu": M, "peers": w.n_peers,
+            "subscriptions_this_shard": int(st["n_entries"]), "pairs_per_tick": int(pairs_all),
+            "parallelism": f"cube-hash x{world_size}" + (" (RCCL all-to-all)" if world_size > 1 else ""),
+            "table_build_s": round(build_s, 3),
+        },
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "route tick on the owner shard (count + tile_scan + emit)",
+                     "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
+    }
+    if rank == 0 and world_size == 1 and not a.no_cpu_baseline:
+        w1 = shard_workload(0, a.scale)
+        out["cpu_baseline"] = cpu_baseline(w1, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     r.close()

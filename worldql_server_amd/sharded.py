@@ -45,6 +45,11 @@ class DistExchange:
         self.dist.all_to_all_single(out, inp, list(out_splits), list(in_splits), group=self.group)
 
 
+class LocalExchange:
+    """G = 1: no exchange (the single-GPU path)."""
+    rank, size = 0, 1
+
+
 class ThreadHub:
     """Shared mailbox of a ThreadExchange group."""
 
@@ -91,6 +96,8 @@ class DeviceShard:
         router.set_stream(stream.cuda_stream)
         self.cap = 0
         self._peers = None
+        # wq_route_counters of the latest route call (P, F, overflow, error), device memory
+        self.counters = torch.zeros(abi.COUNTERS_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
 
     def shard_ops(self, ops: np.ndarray, n_shards: int) -> np.ndarray:
         return self.router.shard_ops(ops, n_shards)
@@ -116,7 +123,8 @@ class DeviceShard:
             self._peers = torch.empty(max(self.cap, 1), dtype=torch.int32, device=self.device)
         offsets = torch.empty(n + 1, dtype=torch.int32, device=self.device)
         self.router.route_records_device(recs.data_ptr() if n else None, n, offsets.data_ptr(),
-                                         self._peers.data_ptr() if self.cap else None, None, self.cap)
+                                         self._peers.data_ptr() if self.cap else None, None, self.cap,
+                                         self.counters.data_ptr())
         return offsets, self._peers
 
     def route_local(self, pos, keys, world, sender, repl, P_hint: int | None = None):
@@ -129,8 +137,15 @@ class DeviceShard:
         offsets = torch.empty(M + 1, dtype=torch.int32, device=self.device)
         self.router.route_device(_ptr(pos), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M,
                                  offsets.data_ptr(), self._peers.data_ptr() if self.cap else None, None,
-                                 self.cap, keys_ptr=_ptr(keys))
+                                 self.cap, self.counters.data_ptr(), keys_ptr=_ptr(keys))
         return offsets, self._peers
+
+    def read_counters(self):
+        """(P, F) of the latest route call (synchronises the stream)."""
+        self.stream.synchronize()
+        c = self.counters.cpu().numpy().view(abi.COUNTERS_DTYPE)[0]
+        assert c["error"] == 0, c
+        return int(c["n_pairs"]), int(c["n_candidates"])
 
 
 def _ptr(t):
@@ -167,6 +182,7 @@ class ShardedRouter:
         self.ex = exchange
         self.G = exchange.size
         self.rank = exchange.rank
+        self.last_recv = 0  # messages routed on this shard in the latest tick
 
     def apply_ops(self, ops: np.ndarray) -> None:
         """The full op stream of the tick (every rank sees it); keep what this shard owns."""
@@ -185,6 +201,7 @@ class ShardedRouter:
         M = int(world.shape[0])
         dev = world.device
         if G == 1:
+            self.last_recv = M
             offsets, peers = be.route_local(pos, keys, world, sender, repl)
             P = int(offsets[M].item()) if M else 0
             if P > be.cap:
@@ -199,6 +216,7 @@ class ShardedRouter:
         sc_rc = torch.cat([send_counts, recv_counts]).cpu().tolist()  # host sync 1
         sc, rc = sc_rc[:G], sc_rc[G:]
         R = sum(rc)
+        self.last_recv = R
         recv = torch.empty((R, recs.shape[1]), dtype=recs.dtype, device=dev)
         ex.all_to_all(recv, recs, rc, sc)
 
