@@ -25,6 +25,9 @@ struct CountSmem {
     uint32_t slot[kBlock * IPT];
     uint32_t me[kBlock * IPT];
     uint32_t meta[kBlock * IPT];
+    uint32_t e[kBlock * IPT];   // results, written to HBM in one coalesced pass at the end: on
+    uint2 info[kBlock * IPT];   // gfx9 stores count in vmcnt, so a store inside the probe loop
+                                // would make every later load-wait also wait for it
     uint64_t wave_F[kWaves];
     uint64_t wave_E[kWaves];
 };
@@ -65,24 +68,41 @@ __global__ __launch_bounds__(kBlock) void count_kernel(CountParams p) {
     uint32_t E_local = 0;
 
     // ---- A: one lane per message — inputs, quantise, packed key, home slot ----
+    // Every input of the IPT messages is loaded before any of them is used, so a wave waits for
+    // memory once here instead of once per coordinate.
+    uint32_t in_w[IPT], in_me[IPT];
+    uint8_t in_rp[IPT];
+    uint64_t in_c[IPT][3];  // f64 bits, or raw keys
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+        const uint32_t m = m0 + i * kBlock + tid;
+        const uint32_t mm = m < p.in.M ? m : 0;
+        in_w[i] = p.in.world[mm];
+        in_me[i] = p.in.sender[mm];
+        in_rp[i] = p.in.repl[mm];
+        const uint64_t* src = RAW_KEYS ? reinterpret_cast<const uint64_t*>(p.in.keys)
+                                       : reinterpret_cast<const uint64_t*>(p.in.pos);
+        in_c[i][0] = src[3ull * mm];
+        in_c[i][1] = src[3ull * mm + 1];
+        in_c[i][2] = src[3ull * mm + 2];
+    }
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
         const uint32_t j = i * kBlock + tid;
         const uint32_t m = m0 + j;
         const bool valid = m < p.in.M;
-        const uint32_t mm = valid ? m : 0;
-        const uint32_t w = p.in.world[mm];
-        const uint32_t me = p.in.sender[mm];
-        const uint8_t rp = p.in.repl[mm];
+        const uint32_t w = in_w[i];
+        const uint32_t me = in_me[i];
+        const uint8_t rp = in_rp[i];
         int64_t x, y, z;
         if (RAW_KEYS) {
-            x = p.in.keys[3ull * mm];
-            y = p.in.keys[3ull * mm + 1];
-            z = p.in.keys[3ull * mm + 2];
+            x = (int64_t)in_c[i][0];
+            y = (int64_t)in_c[i][1];
+            z = (int64_t)in_c[i][2];
         } else {
-            x = coord_clamp_dev(p.in.pos[3ull * mm], tv.sf, p.in.si);
-            y = coord_clamp_dev(p.in.pos[3ull * mm + 1], tv.sf, p.in.si);
-            z = coord_clamp_dev(p.in.pos[3ull * mm + 2], tv.sf, p.in.si);
+            x = coord_clamp_dev(__longlong_as_double((long long)in_c[i][0]), tv.sf, p.in.si);
+            y = coord_clamp_dev(__longlong_as_double((long long)in_c[i][1]), tv.sf, p.in.si);
+            z = coord_clamp_dev(__longlong_as_double((long long)in_c[i][2]), tv.sf, p.in.si);
         }
         uint64_t pk = 0;
         const bool reg = pack_key(w, x, y, z, tv.sf, &pk);
@@ -101,8 +121,8 @@ __global__ __launch_bounds__(kBlock) void count_kernel(CountParams p) {
             uint32_t e;
             uint2 inf;
             finish_message(cnt, rp, false, 0, loff, at, has, &e, &inf);
-            p.e[m] = e;
-            p.info[m] = inf;
+            sm.e[j] = e;
+            sm.info[j] = inf;
             F_local += cnt;
             E_local += e;
             meta |= kMetaDone;
@@ -117,36 +137,51 @@ __global__ __launch_bounds__(kBlock) void count_kernel(CountParams p) {
     // ---- B: eight lanes per message — one coalesced record-line load, parallel compare ----
     const int grp = lane >> 3, part = lane & 7;
     const uint4* recs4 = reinterpret_cast<const uint4*>(tv.recs);
+    const int lead = lane & ~7;
     for (int r0 = 0; r0 < 8 * IPT; r0 += U) {
         uint4 v[U];
         uint32_t jj[U], sl[U], meta[U];
+        uint64_t pkv[U];
+        bool pend[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             jj[u] = wave_msg<IPT>(wave, 8 * (r0 + u) + grp);
             meta[u] = sm.meta[jj[u]];
             sl[u] = sm.slot[jj[u]];
-            const bool act = (meta[u] & (kMetaValid | kMetaDone)) == kMetaValid;
-            v[u] = act ? recs4[(uint64_t)sl[u] * 8 + part] : make_uint4(0, 0, 0, 0);
+            pkv[u] = sm.pk[jj[u]];
+            pend[u] = (meta[u] & (kMetaValid | kMetaDone)) == kMetaValid;  // uniform per group
+            v[u] = pend[u] ? recs4[(uint64_t)sl[u] * 8 + part] : make_uint4(0, 0, 0, 0);
+        }
+        // Linear-probe collisions: check every line's key, then re-issue the loads of all groups
+        // that hit another cube together, so a round costs one extra round trip per probe
+        // DEPTH rather than one per collided message.
+        for (;;) {
+            bool again = false;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!pend[u]) continue;
+                const uint32_t hx = __shfl(v[u].x, lead, 64), hy = __shfl(v[u].y, lead, 64);
+                const uint64_t key = ((uint64_t)hy << 32) | hx;
+                if (key != 0 && key != pkv[u]) {
+                    sl[u] = (sl[u] + 1) & (uint32_t)tv.rec_mask;
+                    again = true;
+                } else {
+                    pend[u] = false;
+                }
+            }
+            if (!__any(again)) break;
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (pend[u]) v[u] = recs4[(uint64_t)sl[u] * 8 + part];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if ((meta[u] & (kMetaValid | kMetaDone)) != kMetaValid) continue;  // uniform per group
-            const uint64_t pk = sm.pk[jj[u]];
             const uint32_t me = sm.me[jj[u]];
             const uint8_t rp = (uint8_t)(meta[u] >> 8);
-            const int lead = lane & ~7;
-            uint32_t hx = __shfl(v[u].x, lead, 64), hy = __shfl(v[u].y, lead, 64);
-            uint32_t hz = __shfl(v[u].z, lead, 64), hw = __shfl(v[u].w, lead, 64);
-            uint64_t key = ((uint64_t)hy << 32) | hx;
-            while (key != 0 && key != pk) {  // collision walk, whole group in step
-                sl[u] = (sl[u] + 1) & (uint32_t)tv.rec_mask;
-                v[u] = recs4[(uint64_t)sl[u] * 8 + part];
-                hx = __shfl(v[u].x, lead, 64);
-                hy = __shfl(v[u].y, lead, 64);
-                hz = __shfl(v[u].z, lead, 64);
-                hw = __shfl(v[u].w, lead, 64);
-                key = ((uint64_t)hy << 32) | hx;
-            }
+            const uint32_t hx = __shfl(v[u].x, lead, 64), hy = __shfl(v[u].y, lead, 64);
+            const uint32_t hz = __shfl(v[u].z, lead, 64), hw = __shfl(v[u].w, lead, 64);
+            const uint64_t key = ((uint64_t)hy << 32) | hx;
             const uint32_t cnt = key != 0 ? hz : 0u;
             const bool inl = cnt <= (uint32_t)kInline;
             uint32_t lt = 0, eq = 0;
@@ -177,9 +212,8 @@ __global__ __launch_bounds__(kBlock) void count_kernel(CountParams p) {
                 uint32_t e;
                 uint2 inf;
                 finish_message(cnt, rp, inl, sl[u], hw, at, has, &e, &inf);
-                const uint32_t m = m0 + jj[u];
-                p.e[m] = e;
-                p.info[m] = inf;
+                sm.e[jj[u]] = e;
+                sm.info[jj[u]] = inf;
                 F_local += cnt;
                 E_local += e;
             }
@@ -193,6 +227,14 @@ __global__ __launch_bounds__(kBlock) void count_kernel(CountParams p) {
         sm.wave_E[wave] = Ew;
     }
     lds_barrier();
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+        const uint32_t j = i * kBlock + tid;
+        if (m0 + j < p.in.M) {
+            p.e[m0 + j] = sm.e[j];
+            p.info[m0 + j] = sm.info[j];
+        }
+    }
     if (tid == 0) {
         uint64_t Fb = 0, Eb = 0;
 #pragma unroll

@@ -52,13 +52,20 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(EmitParams p) {
 
     // ---- A0: CSR offsets of the tile — count-block prefix + block-local scan in message order ----
     uint32_t e[IPT], st[IPT], sc[IPT];
+    uint2 inf[IPT];
     uint32_t g0 = 0, T = 0;  // global offset of the tile's first output; outputs in the tile
     {
         uint32_t incl[IPT];
+        // the locators are loaded with the counts, ahead of the offset stores (gfx9: a later
+        // load-wait would otherwise also wait for those stores)
 #pragma unroll
         for (int i = 0; i < IPT; ++i) {
             const uint32_t m = m0 + i * kBlock + tid;
             e[i] = m < p.M ? p.e[m] : 0u;
+            inf[i] = (p.peers && m < p.M) ? p.info[m] : make_uint2(0, kNone);
+        }
+#pragma unroll
+        for (int i = 0; i < IPT; ++i) {
             incl[i] = wave_incl_scan_add(e[i], lane);
             if (lane == 63) sm.rowt[i][wave] = incl[i];
         }
@@ -91,13 +98,8 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(EmitParams p) {
     if (!p.peers) return;  // counts-only call: offsets are all that is asked for
 
     // ---- A: one lane per message — locators, stage positions ----
-    uint2 inf[IPT];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
-        const uint32_t m = m0 + i * kBlock + tid;
-        const bool valid = m < p.M;
-        const uint32_t mm = valid ? m : p.M - 1;
-        inf[i] = p.info[mm];
         const bool rec = !(inf[i].x & (kLocGlobal | kLocSelf));
         sc[i] = !e[i] ? 0u : rec ? (inf[i].y >> 24) : (inf[i].x & kLocSelf) ? 1u : 0u;
     }

@@ -28,11 +28,16 @@ struct __attribute__((aligned(32))) Slot {
 static_assert(sizeof(Slot) == 32, "Slot must be 32 bytes");
 
 // Rust `f64 as i64`: truncation toward zero, saturating, NaN -> 0 (C's cast is UB out of range).
+// Branch-free (selects only), so the compiler can keep a wave's loads in flight across it.
 __host__ __device__ __forceinline__ int64_t sat_i64(double x) {
-    if (x != x) return 0;
-    if (x >= 9223372036854775808.0) return INT64_MAX;
-    if (x <= -9223372036854775808.0) return INT64_MIN;
-    return (int64_t)x;
+    const bool nan = x != x;
+    const bool hi = x >= 9223372036854775808.0;
+    const bool lo = x <= -9223372036854775808.0;
+    const double t = (nan | hi | lo) ? 0.0 : x;  // in range: the cast below is defined
+    int64_t v = (int64_t)t;
+    v = hi ? INT64_MAX : v;
+    v = lo ? INT64_MIN : v;
+    return v;
 }
 
 // cube_area.rs:23-44, release-build semantics (wrapping i64 + and *). The reference's
@@ -44,12 +49,14 @@ __host__ __device__ __forceinline__ int64_t sat_i64(double x) {
 __host__ __device__ __forceinline__ int64_t coord_clamp_dev(double c, double sf, int64_t si) {
     const double a = fabs(c);
     const double q = a / sf;
-    const bool is_mult = (q == trunc(q)) && (fma(q, sf, -a) == 0.0) && (c != 0.0);
-    if (is_mult) return sat_i64(c);
+    // exact multiple (and not +-0): the reference returns `c as i64` (cube_area.rs:30-32)
+    const bool is_mult = (q == trunc(q)) & (fma(q, sf, -a) == 0.0) & (c != 0.0);
     const double r = (a == 0.0) ? sf : ceil(q) * sf;  // round_by_multiple(a, s)
-    int64_t res = sat_i64(r);
-    if (!(r > c)) res = (int64_t)((uint64_t)res + (uint64_t)si);
-    return (c < 0.0) ? (int64_t)(0ull - (uint64_t)res) : res;
+    int64_t res = sat_i64(is_mult ? c : r);
+    const bool add = !is_mult & !(r > c);             // `if r > c {r} else {r + size}`, wrapping
+    res = add ? (int64_t)((uint64_t)res + (uint64_t)si) : res;
+    const bool neg = !is_mult & (c < 0.0);            // `* mult`, wrapping
+    return neg ? (int64_t)(0ull - (uint64_t)res) : res;
 }
 
 __host__ __device__ __forceinline__ uint64_t cube_hash(uint32_t w, int64_t x, int64_t y, int64_t z) {

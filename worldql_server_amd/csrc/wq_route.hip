@@ -57,12 +57,12 @@ void launch_emit(const EmitParams& p, hipStream_t s, unsigned grid) {
 #define WQ_CFG(cipt, cu, eipt, chunk, stage, eu) \
     {cipt, eipt, &launch_count<cipt, cu>, &launch_emit<eipt, chunk, stage, eu>}
 const Cfg kCfgs[] = {
-    WQ_CFG(2, 8, 1, 1024, 3072, 8),   // 0: default
-    WQ_CFG(2, 8, 2, 1024, 6144, 8),   // 1
-    WQ_CFG(1, 8, 1, 1024, 3072, 8),   // 2
-    WQ_CFG(4, 8, 1, 1024, 3072, 8),   // 3
-    WQ_CFG(2, 4, 1, 512, 3072, 4),    // 4
-    WQ_CFG(2, 16, 2, 2048, 6144, 16), // 5
+    WQ_CFG(2, 4, 1, 1024, 3072, 8),   // 0: default
+    WQ_CFG(2, 8, 1, 512, 3072, 4),    // 1
+    WQ_CFG(1, 4, 2, 1024, 6144, 8),   // 2
+    WQ_CFG(4, 4, 1, 1024, 3072, 4),   // 3
+    WQ_CFG(2, 2, 1, 512, 3072, 8),    // 4
+    WQ_CFG(4, 8, 2, 2048, 6144, 16),  // 5
 };
 #undef WQ_CFG
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
