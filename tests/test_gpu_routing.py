@@ -253,7 +253,7 @@ def test_inline_boundary_and_stage_overflow(per_cube):
     M = 5000
     mpos = np.stack([rng.below(n_cubes, M) * 16.0 + rng.uniform(0.5, 15.5, M), rng.uniform(0.5, 15.5, M),
                      -rng.uniform(0.5, 15.5, M)], 1)
-    for cfg in range(5):
+    for cfg in range(6):
         r.set_route_config(cfg)
         _compare(r, o, mpos, np.zeros(M, np.uint32), rng.below(n_cubes * per_cube, M),
                  rng.below(3, M).astype(np.uint8))

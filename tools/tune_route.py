@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--cfgs", default="0,1,2,3,4")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--raw-keys", action="store_true", help="route pre-quantised keys (skips kernel 1)")
     a = ap.parse_args()
     import torch
     from worldql_server_amd import abi, synth
@@ -36,6 +37,10 @@ def main():
     peers = torch.empty(cap, dtype=torch.int32, device=dev)
     msgs = torch.empty(cap, dtype=torch.int32, device=dev)
     cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+    keys = None
+    if a.raw_keys:
+        keys = torch.empty((M, 3), dtype=torch.int64, device=dev)
+        r.lib.wq_quantize_device(r.h, pos.data_ptr(), 3 * M, keys.data_ptr())
     torch.cuda.synchronize()
     ref = None
     res = {}
@@ -43,10 +48,11 @@ def main():
     for rnd in range(a.rounds):
         for cfg in cfgs:
             r.set_route_config(cfg)
-            args = (pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
-                    peers.data_ptr(), msgs.data_ptr(), cap)
+            args = (0 if a.raw_keys else pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M,
+                    offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap)
+            kw = {"keys_ptr": keys.data_ptr()} if a.raw_keys else {}
             for _ in range(3):
-                r.route_device(*args, cnt.data_ptr())
+                r.route_device(*args, cnt.data_ptr(), **kw)
             torch.cuda.synchronize()
             c = cnt.cpu().numpy().view(abi.COUNTERS_DTYPE)[0]
             P = int(c["n_pairs"])
@@ -56,7 +62,7 @@ def main():
             assert h == ref, f"cfg {cfg} differs"
             r.profile_enable(True)
             for _ in range(a.steps):
-                r.route_device(*args)
+                r.route_device(*args, **kw)
             ms, n = r.profile_read()
             r.profile_enable(False)
             res.setdefault(cfg, []).append(ms / n * 1e3)

@@ -150,7 +150,8 @@ __global__ __launch_bounds__(kBlock) void count_kernel(CountParams p) {
             sl[u] = sm.slot[jj[u]];
             pkv[u] = sm.pk[jj[u]];
             pend[u] = (meta[u] & (kMetaValid | kMetaDone)) == kMetaValid;  // uniform per group
-            v[u] = pend[u] ? recs4[(uint64_t)sl[u] * 8 + part] : make_uint4(0, 0, 0, 0);
+            if (!pend[u]) sl[u] = (m0 + jj[u]) & (uint32_t)tv.rec_mask;  // spread dummy line
+            v[u] = recs4[(uint64_t)sl[u] * 8 + part];  // unconditional: see route_count_lpm.hpp
         }
         // Linear-probe collisions: check every line's key, then re-issue the loads of all groups
         // that hit another cube together, so a round costs one extra round trip per probe

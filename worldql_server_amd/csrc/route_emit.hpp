@@ -165,7 +165,10 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(EmitParams p) {
                 const uint32_t sl = sm.slot[j];
                 sp[u] = sm.spos[j];
                 act[u] = sl != kNone && part > 0;
-                v[u] = act[u] ? recs4[(uint64_t)sl * 8 + part] : make_uint4(0, 0, 0, 0);
+                // unconditional load, no drain between rounds; groups with no record read a dummy
+                // line spread by message index (a shared line would serialise on one L2 channel)
+                const uint64_t line = sl != kNone ? sl : ((m0 + j) & (uint32_t)tv.rec_mask);
+                v[u] = recs4[line * 8 + part];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {

@@ -25,6 +25,7 @@
 #include <algorithm>
 
 #include "route_count.hpp"
+#include "route_count_lpm.hpp"
 #include "route_emit.hpp"
 #include "route_scan.hpp"
 
@@ -49,6 +50,14 @@ void launch_count(const CountParams& p, hipStream_t s, unsigned grid) {
         hipLaunchKernelGGL((count_kernel<false, IPT, U>), dim3(grid), dim3(kBlock), 0, s, p);
 }
 
+template <int IPT, int MINW>
+void launch_count_lpm(const CountParams& p, hipStream_t s, unsigned grid) {
+    if (p.in.keys)
+        hipLaunchKernelGGL((count_lpm_kernel<true, IPT, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
+    else
+        hipLaunchKernelGGL((count_lpm_kernel<false, IPT, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
+}
+
 template <int IPT, int CHUNK, int STAGE, int U>
 void launch_emit(const EmitParams& p, hipStream_t s, unsigned grid) {
     hipLaunchKernelGGL((emit_kernel<IPT, CHUNK, STAGE, U>), dim3(grid), dim3(kBlock), 0, s, p);
@@ -56,15 +65,20 @@ void launch_emit(const EmitParams& p, hipStream_t s, unsigned grid) {
 
 #define WQ_CFG(cipt, cu, eipt, chunk, stage, eu) \
     {cipt, eipt, &launch_count<cipt, cu>, &launch_emit<eipt, chunk, stage, eu>}
+#define WQ_CFG_LPM(cipt, minw, eipt, chunk, stage, eu) \
+    {cipt, eipt, &launch_count_lpm<cipt, minw>, &launch_emit<eipt, chunk, stage, eu>}
+// count: (messages per thread, record lines per 8-lane round) or lane-per-message (LPM);
+// emit: (messages per thread, expansion chunk, stage words, lines per round)
 const Cfg kCfgs[] = {
-    WQ_CFG(2, 4, 1, 1024, 3072, 8),   // 0: default
-    WQ_CFG(2, 8, 1, 512, 3072, 4),    // 1
-    WQ_CFG(1, 4, 2, 1024, 6144, 8),   // 2
-    WQ_CFG(4, 4, 1, 1024, 3072, 4),   // 3
-    WQ_CFG(2, 2, 1, 512, 3072, 8),    // 4
-    WQ_CFG(4, 8, 2, 2048, 6144, 16),  // 5
+    WQ_CFG_LPM(2, 4, 1, 1024, 3072, 8),  // 0: default (count 52 us on C2, profiles/r01_kernel_stats_v7.csv)
+    WQ_CFG_LPM(1, 1, 1, 1024, 3072, 8),  // 1
+    WQ_CFG(2, 2, 1, 512, 3072, 8),       // 2: 8 lanes per record line
+    WQ_CFG(2, 4, 1, 1024, 3072, 8),      // 3
+    WQ_CFG(4, 4, 2, 1024, 6144, 8),      // 4
+    WQ_CFG_LPM(2, 4, 1, 512, 3072, 8),   // 5
 };
 #undef WQ_CFG
+#undef WQ_CFG_LPM
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 }  // namespace
 
