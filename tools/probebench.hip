@@ -143,5 +143,46 @@ int main() {
         }
         printf("%-34s warm %7.1f us   after 128 MB stream %7.1f us\n", vv.name, ms * 1e3 / 20, cold * 1e3 / 20);
     }
+    // HBM-bound sector test: 8M messages over 8M distinct lines of a 2 GB table (past the 256 MB
+    // Infinity Cache): does reading 16 / 64 B of a line cost less than the whole 128 B?
+    {
+        const uint32_t M2 = 8u << 20, T2 = 16u << 20, occ2 = 8u << 20;
+        uint4* tab2;
+        uint32_t *o2, *e2;
+        uint2* i2;
+        double* p2;
+        uint32_t* w2;
+        hipMalloc(&tab2, (size_t)T2 * 128);
+        hipMalloc(&o2, (size_t)occ2 * 4);
+        hipMalloc(&e2, (size_t)M2 * 4);
+        hipMalloc(&i2, (size_t)M2 * 8);
+        hipMalloc(&p2, (size_t)M2 * 24);
+        hipMalloc(&w2, (size_t)M2 * 4);
+        hipMemset(tab2, 1, (size_t)T2 * 128);
+        uint32_t* hh = new uint32_t[occ2];
+        for (uint32_t i = 0; i < occ2; ++i) {
+            x = x * 6364136223846793005ull + 1442695040888963407ull;
+            hh[i] = (uint32_t)(x >> 33) & (T2 - 1);
+        }
+        hipMemcpy(o2, hh, (size_t)occ2 * 4, hipMemcpyHostToDevice);
+        for (int words : {1, 2, 4, 8}) {
+            auto go = [&]() {
+                const unsigned grid = (M2 + 511) / 512;
+#define L2(W) if (words == W) hipLaunchKernelGGL((probe<2, W>), dim3(grid), dim3(256), 0, 0, tab2, o2, occ2, T2 - 1, p2, w2, M2, 0u, 0, e2, i2);
+                L2(1) L2(2) L2(4) L2(8)
+#undef L2
+            };
+            go();
+            hipEventRecord(a);
+            for (int r = 0; r < 5; ++r) go();
+            hipEventRecord(b);
+            hipEventSynchronize(b);
+            float ms;
+            hipEventElapsedTime(&ms, a, b);
+            const double t = ms / 5 * 1e-3;
+            printf("HBM-bound: %3d B of each random line: %8.1f us  %.2f G lines/s  %.2f TB/s if whole lines\n",
+                   words * 16, t * 1e6, M2 / t / 1e9, M2 * 128.0 / t / 1e12);
+        }
+    }
     return 0;
 }

@@ -5,7 +5,7 @@
 // 16-byte loads issued back to back (one line request; the other seven hit it in flight), and
 // compares the sender with the <= 28 inline peers in registers. No LDS, no shuffles: the 8-lane
 // form spends ~8x the VALU instructions per message on broadcasts and reductions (PMC:
-// VALU ~60% busy, profiles/r01_pmc_v6.md).
+// VALU ~60% busy, profiles/r01_pmc_v6_cfg4.txt).
 #pragma once
 #include "route_count.hpp"
 
