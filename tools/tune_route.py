@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--cfgs", default="0,1,2,3,4")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--no-check", action="store_true", help="timing-only configs (wrong outputs)")
     ap.add_argument("--raw-keys", action="store_true", help="route pre-quantised keys (skips kernel 1)")
     a = ap.parse_args()
     import torch
@@ -59,7 +60,7 @@ def main():
             h = (offs.cpu().numpy().tobytes(), peers[:P].cpu().numpy().tobytes(), msgs[:P].cpu().numpy().tobytes())
             if ref is None:
                 ref = h
-            assert h == ref, f"cfg {cfg} differs"
+            assert a.no_check or h == ref, f"cfg {cfg} differs"
             r.profile_enable(True)
             for _ in range(a.steps):
                 r.route_device(*args, **kw)

@@ -1,12 +1,22 @@
 // route_count.hpp — pass 1 of the tick: count_kernel (see wq_route.hip).
+//
+// One lane per message, IPT messages per lane. Per message the pass needs the cube's peer count
+// and whether the sender is one of its peers (local_message.rs:60-86). Both come from the first
+// 32 bytes of the cube's 128-byte record line (wq_device.hpp): chunk 0 = {pk, count, list_off},
+// chunk 1 = {sig, p0, p1}, where sig is a 64-bit Bloom signature of the cube's peers. A sender
+// whose signature bits are not all set is certainly not subscribed; only the rest (C2: ~7% false
+// positives plus the true positives) read further chunks of the inline list. So a lookup is two
+// 16-byte loads and 8 VGPRs per message, not eight loads and 32 VGPRs for the whole line.
+//
+// Work that needs another memory round trip — a linear-probe step past a foreign key, or the
+// next two chunks of a list being verified — runs as a per-lane state machine: every round each
+// pending message issues its two loads, all IPT messages of the lane together, so a wave pays one
+// round trip per round whatever mix of probes and verifications it holds.
 #pragma once
 #include "route_common.hpp"
 
 namespace wq {
 
-// ------------------------------------------------------------------------------------------
-// 1. count
-// ------------------------------------------------------------------------------------------
 struct CountParams {
     RouteIn in;
     TableView t;
@@ -15,21 +25,6 @@ struct CountParams {
     uint32_t* tile_total;  // out: sum of e over each block's messages
     wq_route_counters* cnt;
     wq_route_counters* cnt_next;
-};
-
-constexpr uint32_t kMetaValid = 1u, kMetaDone = 2u;  // meta: flags | repl << 8
-
-template <int IPT>
-struct CountSmem {
-    uint64_t pk[kBlock * IPT];
-    uint32_t slot[kBlock * IPT];
-    uint32_t me[kBlock * IPT];
-    uint32_t meta[kBlock * IPT];
-    uint32_t e[kBlock * IPT];   // results, written to HBM in one coalesced pass at the end: on
-    uint2 info[kBlock * IPT];   // gfx9 stores count in vmcnt, so a store inside the probe loop
-                                // would make every later load-wait also wait for it
-    uint64_t wave_F[kWaves];
-    uint64_t wave_E[kWaves];
 };
 
 // e / locator once count, membership and list position are known (local_message.rs:60-86)
@@ -51,10 +46,13 @@ __device__ __forceinline__ void finish_message(uint32_t cnt, uint8_t rp, bool in
     }
 }
 
-template <bool RAW_KEYS, int IPT, int U>
-__global__ __launch_bounds__(kBlock) void count_kernel(CountParams p) {
-    constexpr int TILE = kBlock * IPT;
-    __shared__ CountSmem<IPT> sm;
+// per-message probe state
+constexpr uint32_t kStDone = 0, kStProbe = 1, kStVerify = 2;
+
+template <bool RAW_KEYS, int IPT, int MINW>
+__global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
+    __shared__ uint64_t wave_F[kWaves];
+    __shared__ uint64_t wave_E[kWaves];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const TableView& tv = p.t;
     if (blockIdx.x == 0 && tid == 0) {
@@ -63,16 +61,14 @@ __global__ __launch_bounds__(kBlock) void count_kernel(CountParams p) {
         p.cnt_next->overflow = 0;
         p.cnt_next->error = 0;
     }
-    const uint32_t m0 = blockIdx.x * TILE;
+    const uint32_t m0 = blockIdx.x * (kBlock * IPT);
     uint64_t F_local = 0;
     uint32_t E_local = 0;
 
-    // ---- A: one lane per message — inputs, quantise, packed key, home slot ----
-    // Every input of the IPT messages is loaded before any of them is used, so a wave waits for
-    // memory once here instead of once per coordinate.
+    // ---- A: inputs (all loads first), quantise (kernel 1), packed key, home slot ----
     uint32_t in_w[IPT], in_me[IPT];
     uint8_t in_rp[IPT];
-    uint64_t in_c[IPT][3];  // f64 bits, or raw keys
+    uint64_t in_c[IPT][3];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
         const uint32_t m = m0 + i * kBlock + tid;
@@ -86,14 +82,15 @@ __global__ __launch_bounds__(kBlock) void count_kernel(CountParams p) {
         in_c[i][1] = src[3ull * mm + 1];
         in_c[i][2] = src[3ull * mm + 2];
     }
+    uint64_t pk[IPT];
+    uint32_t sl[IPT], st[IPT], e_out[IPT];
+    bool via_rec[IPT];
+    uint2 inf_out[IPT];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
-        const uint32_t j = i * kBlock + tid;
-        const uint32_t m = m0 + j;
+        const uint32_t m = m0 + i * kBlock + tid;
         const bool valid = m < p.in.M;
         const uint32_t w = in_w[i];
-        const uint32_t me = in_me[i];
-        const uint8_t rp = in_rp[i];
         int64_t x, y, z;
         if (RAW_KEYS) {
             x = (int64_t)in_c[i][0];
@@ -104,10 +101,19 @@ __global__ __launch_bounds__(kBlock) void count_kernel(CountParams p) {
             y = coord_clamp_dev(__longlong_as_double((long long)in_c[i][1]), tv.sf, p.in.si);
             z = coord_clamp_dev(__longlong_as_double((long long)in_c[i][2]), tv.sf, p.in.si);
         }
-        uint64_t pk = 0;
-        const bool reg = pack_key(w, x, y, z, tv.sf, &pk);
-        uint32_t meta = (valid ? kMetaValid : 0u) | ((uint32_t)rp << 8);
-        if (valid && !reg) {  // full-key slot table: rare, finished here one lane per message
+        pk[i] = 0;
+        const bool reg = pack_key(w, x, y, z, tv.sf, &pk[i]);
+        // lanes with nothing to probe read a dummy line spread by message index (never one shared
+        // line: a chip-wide hot line serialises on its L2 channel)
+        sl[i] = reg ? (uint32_t)slot_of(rec_hash(pk[i]) & tv.hash_mask, tv.rec_shift)
+                    : (m & (uint32_t)tv.rec_mask);
+        via_rec[i] = valid && reg;
+        st[i] = via_rec[i] ? kStProbe : kStDone;
+        e_out[i] = 0;
+        inf_out[i] = make_uint2(0, kNone);
+        if (valid && !reg) {  // full-key slot table: rare, finished here
+            const uint32_t me = in_me[i];
+            const uint8_t rp = in_rp[i];
             const uint32_t loff = probe(tv.slots, tv.slot_mask, tv.slot_shift, cube_hash(w, x, y, z) & tv.hash_mask,
                                         w, x, y, z);
             const uint32_t cnt = loff != kNone ? tv.list[loff] : 0u;
@@ -118,130 +124,120 @@ __global__ __launch_bounds__(kBlock) void count_kernel(CountParams p) {
                 at = lower_bound_dev(lp, cnt, me);
                 has = at < cnt && lp[at] == me;
             }
-            uint32_t e;
-            uint2 inf;
-            finish_message(cnt, rp, false, 0, loff, at, has, &e, &inf);
-            sm.e[j] = e;
-            sm.info[j] = inf;
+            finish_message(cnt, rp, false, 0, loff, at, has, &e_out[i], &inf_out[i]);
             F_local += cnt;
-            E_local += e;
-            meta |= kMetaDone;
+            E_local += e_out[i];
         }
-        sm.pk[j] = pk;
-        sm.slot[j] = reg ? (uint32_t)slot_of(rec_hash(pk) & tv.hash_mask, tv.rec_shift) : 0u;
-        sm.me[j] = me;
-        sm.meta[j] = meta;
     }
-    lds_barrier();
 
-    // ---- B: eight lanes per message — one coalesced record-line load, parallel compare ----
-    const int grp = lane >> 3, part = lane & 7;
+    // ---- B: rounds of two 16-byte loads per pending message ----
     const uint4* recs4 = reinterpret_cast<const uint4*>(tv.recs);
-    const int lead = lane & ~7;
-    for (int r0 = 0; r0 < 8 * IPT; r0 += U) {
-        uint4 v[U];
-        uint32_t jj[U], sl[U], meta[U];
-        uint64_t pkv[U];
-        bool pend[U];
+    uint4 c0[IPT], c1[IPT];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            jj[u] = wave_msg<IPT>(wave, 8 * (r0 + u) + grp);
-            meta[u] = sm.meta[jj[u]];
-            sl[u] = sm.slot[jj[u]];
-            pkv[u] = sm.pk[jj[u]];
-            pend[u] = (meta[u] & (kMetaValid | kMetaDone)) == kMetaValid;  // uniform per group
-            if (!pend[u]) sl[u] = (m0 + jj[u]) & (uint32_t)tv.rec_mask;  // spread dummy line
-            v[u] = recs4[(uint64_t)sl[u] * 8 + part];  // unconditional: see route_count_lpm.hpp
-        }
-        // Linear-probe collisions: check every line's key, then re-issue the loads of all groups
-        // that hit another cube together, so a round costs one extra round trip per probe
-        // DEPTH rather than one per collided message.
-        for (;;) {
-            bool again = false;
+    for (int i = 0; i < IPT; ++i) {
+        c0[i] = recs4[(uint64_t)sl[i] * 8];
+        c1[i] = recs4[(uint64_t)sl[i] * 8 + 1];
+    }
+    uint32_t cnt[IPT], loff[IPT], lt[IPT], vc[IPT];
+    bool has[IPT];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (!pend[u]) continue;
-                const uint32_t hx = __shfl(v[u].x, lead, 64), hy = __shfl(v[u].y, lead, 64);
-                const uint64_t key = ((uint64_t)hy << 32) | hx;
-                if (key != 0 && key != pkv[u]) {
-                    sl[u] = (sl[u] + 1) & (uint32_t)tv.rec_mask;
-                    again = true;
-                } else {
-                    pend[u] = false;
-                }
-            }
-            if (!__any(again)) break;
+    for (int i = 0; i < IPT; ++i) {
+        cnt[i] = 0;
+        loff[i] = 0;
+        lt[i] = 0;
+        vc[i] = 0;
+        has[i] = false;
+    }
+    for (;;) {
+        bool pending = false;
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (pend[u]) v[u] = recs4[(uint64_t)sl[u] * 8 + part];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if ((meta[u] & (kMetaValid | kMetaDone)) != kMetaValid) continue;  // uniform per group
-            const uint32_t me = sm.me[jj[u]];
-            const uint8_t rp = (uint8_t)(meta[u] >> 8);
-            const uint32_t hx = __shfl(v[u].x, lead, 64), hy = __shfl(v[u].y, lead, 64);
-            const uint32_t hz = __shfl(v[u].z, lead, 64), hw = __shfl(v[u].w, lead, 64);
-            const uint64_t key = ((uint64_t)hy << 32) | hx;
-            const uint32_t cnt = key != 0 ? hz : 0u;
-            const bool inl = cnt <= (uint32_t)kInline;
-            uint32_t lt = 0, eq = 0;
-            if (cnt && inl && rp != WQ_REPL_INCLUDING_SELF && part > 0) {
-                const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                for (int e4 = 0; e4 < 4; ++e4) {
-                    const uint32_t idx = 4 * (part - 1) + e4;
-                    if (idx < cnt) {
-                        lt += vv[e4] < me ? 1u : 0u;
-                        eq |= vv[e4] == me ? 1u : 0u;
+        for (int i = 0; i < IPT; ++i) {
+            const uint32_t me = in_me[i];
+            if (st[i] == kStProbe) {
+                const uint64_t key = ((uint64_t)c0[i].y << 32) | c0[i].x;
+                if (key == pk[i] || key == 0) {  // found, or an empty slot: the cube has no peers
+                    cnt[i] = key ? c0[i].z : 0u;
+                    loff[i] = c0[i].w;
+                    st[i] = kStDone;
+                    if (cnt[i] && in_rp[i] != WQ_REPL_INCLUDING_SELF) {
+                        const uint64_t sig = ((uint64_t)c1[i].y << 32) | c1[i].x;
+                        const uint64_t bits = peer_sig(me);
+                        if ((sig & bits) == bits) {  // maybe subscribed: verify
+                            if (cnt[i] <= (uint32_t)kInline) {
+                                // p0, p1 are in chunk 1; the rest from chunk 2 on
+                                const bool in0 = c1[i].z == me, in1 = cnt[i] > 1 && c1[i].w == me;
+                                lt[i] = (c1[i].z < me ? 1u : 0u) + ((cnt[i] > 1 && c1[i].w < me) ? 1u : 0u);
+                                has[i] = in0 | in1;
+                                const bool stop = has[i] || c1[i].z > me || (cnt[i] > 1 && c1[i].w > me);
+                                if (!stop && cnt[i] > 2) {
+                                    st[i] = kStVerify;
+                                    vc[i] = 2;
+                                }
+                            } else {  // > kInline peers: binary search of the full list (rare in C2)
+                                const uint32_t* lp = tv.list + loff[i] + 1;
+                                lt[i] = lower_bound_dev(lp, cnt[i], me);
+                                has[i] = lt[i] < cnt[i] && lp[lt[i]] == me;
+                            }
+                        }
                     }
+                } else {
+                    sl[i] = (sl[i] + 1) & (uint32_t)tv.rec_mask;
                 }
-            }
+            } else if (st[i] == kStVerify) {
+                // chunks vc, vc+1 hold peers 4*vc-6 .. 4*vc+1; the list is ascending, so the first
+                // peer >= me ends the search
+                const uint32_t v[8] = {c0[i].x, c0[i].y, c0[i].z, c0[i].w, c1[i].x, c1[i].y, c1[i].z, c1[i].w};
+                const uint32_t b = 4 * vc[i] - 6;
+                bool stop = false;
 #pragma unroll
-            for (int d = 1; d < 8; d <<= 1) {
-                lt += __shfl_xor(lt, d, 64);
-                eq |= __shfl_xor(eq, d, 64);
-            }
-            if (part == 0) {
-                uint32_t at = lt;
-                bool has = eq != 0;
-                if (cnt && !inl && rp != WQ_REPL_INCLUDING_SELF) {  // > 28 peers: search the full list
-                    const uint32_t* lp = tv.list + hw + 1;
-                    at = lower_bound_dev(lp, cnt, me);
-                    has = at < cnt && lp[at] == me;
+                for (int q = 0; q < 8; ++q) {
+                    const bool in = b + q < cnt[i];
+                    lt[i] += (in & (v[q] < me)) ? 1u : 0u;
+                    has[i] |= in & (v[q] == me);
+                    stop |= in & (v[q] >= me);
                 }
-                uint32_t e;
-                uint2 inf;
-                finish_message(cnt, rp, inl, sl[u], hw, at, has, &e, &inf);
-                sm.e[jj[u]] = e;
-                sm.info[jj[u]] = inf;
-                F_local += cnt;
-                E_local += e;
+                vc[i] += 2;
+                if (stop || 4 * vc[i] - 6 >= cnt[i]) st[i] = kStDone;
             }
+            pending |= st[i] != kStDone;
         }
+        if (!__any(pending)) break;
+#pragma unroll
+        for (int i = 0; i < IPT; ++i) {
+            if (st[i] == kStDone) continue;
+            const uint32_t q = st[i] == kStProbe ? 0u : vc[i];  // vc <= 6: chunks q, q+1 <= 7
+            c0[i] = recs4[(uint64_t)sl[i] * 8 + q];
+            c1[i] = recs4[(uint64_t)sl[i] * 8 + q + 1];
+        }
+    }
+
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+        const uint32_t m = m0 + i * kBlock + tid;
+        if (m >= p.in.M) continue;
+        if (via_rec[i]) {
+            finish_message(cnt[i], in_rp[i], cnt[i] <= (uint32_t)kInline, sl[i], loff[i], lt[i], has[i], &e_out[i],
+                           &inf_out[i]);
+            F_local += cnt[i];
+            E_local += e_out[i];
+        }
+        p.e[m] = e_out[i];
+        p.info[m] = inf_out[i];
     }
 
     const uint64_t Fw = wave_sum_u64(F_local);
     const uint64_t Ew = wave_sum_u64(E_local);
     if (lane == 0) {
-        sm.wave_F[wave] = Fw;
-        sm.wave_E[wave] = Ew;
+        wave_F[wave] = Fw;
+        wave_E[wave] = Ew;
     }
     lds_barrier();
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-        const uint32_t j = i * kBlock + tid;
-        if (m0 + j < p.in.M) {
-            p.e[m0 + j] = sm.e[j];
-            p.info[m0 + j] = sm.info[j];
-        }
-    }
     if (tid == 0) {
         uint64_t Fb = 0, Eb = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) {
-            Fb += sm.wave_F[w];
-            Eb += sm.wave_E[w];
+            Fb += wave_F[w];
+            Eb += wave_E[w];
         }
         if (Fb) atomicAdd(reinterpret_cast<unsigned long long*>(&p.cnt->n_candidates), (unsigned long long)Fb);
         p.tile_total[blockIdx.x] = Eb > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Eb;

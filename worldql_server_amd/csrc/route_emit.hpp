@@ -1,5 +1,7 @@
 // route_emit.hpp — pass 3 of the tick: emit_kernel (see wq_route.hip).
 #pragma once
+#include <type_traits>
+
 #include "route_common.hpp"
 
 namespace wq {
@@ -21,39 +23,45 @@ struct EmitParams {
     uint64_t capacity;
 };
 
-// owner marks: [generation:20][1 + message index:12] — one generation per expansion chunk, so
-// stale marks of earlier chunks lose every max and the array never needs clearing.
-constexpr int kOwnerIdxBits = 12;
-constexpr uint32_t kOwnerIdxMask = (1u << kOwnerIdxBits) - 1;
-constexpr uint32_t kMaxGen = (1u << (32 - kOwnerIdxBits)) - 1;
-
-template <int IPT, int CHUNK, int STAGE>
+template <int IPT, int STAGE>
 struct EmitSmem {
-    uint32_t stage[STAGE];          // staged inline peer lists (tile-local, compacted)
-    uint32_t base[kBlock * IPT];    // stage index (or kGlobal | list index) of the message's output 0
-    uint32_t skip[kBlock * IPT];    // output index at which the sender is skipped, or kNone
+    using Om = typename std::conditional<IPT == 1, uint8_t, uint16_t>::type;
+    uint32_t op[STAGE];             // window of the tile's output: peers, in output order
+    Om om[STAGE];                   // ... and the tile-local index of each output's message
     uint32_t start[kBlock * IPT];   // tile-local first output of the message
-    uint32_t slot[kBlock * IPT];    // record slot to stage from, or kNone
-    uint32_t spos[kBlock * IPT];    // stage position / count for the staging pass
-    uint32_t owner[2][CHUNK];       // double-buffered tagged owner of each chunk output
+    uint32_t slot[kBlock * IPT];    // inline record slot, or kNone
+    uint32_t meta[kBlock * IPT];    // inline: count | skipped index << 8 (0xFF: none)
+    uint32_t gq_j[kBlock * IPT];    // messages whose list is read from `list` (> kInline peers)
+    uint32_t gq_off[kBlock * IPT];  // ... its list offset (first peer)
+    uint32_t gq_skip[kBlock * IPT]; // ... skipped list index or kNone
+    uint32_t gq_e[kBlock * IPT];    // ... outputs
+    uint32_t n_gq;
     uint32_t wave_tot[kWaves];
     uint32_t rowt[IPT + 1][kWaves]; // per-row wave totals of e (+ earlier messages of the count block)
 };
 
-template <int IPT, int CHUNK, int STAGE, int U>
+// Pass 3. The tile's outputs [0, T) are produced in windows of STAGE positions: every message's
+// peers are written straight into an LDS image of the window IN OUTPUT ORDER (the sender's own
+// entry skipped while staging), together with the message's tile-local index, and the window is
+// then copied out with coalesced stores. C2 tiles (256 messages, ~2,560 outputs) take one window.
+//   inline records (<= kInline peers): eight lanes per record line, lane `part` reading chunk
+//     `part` (peers 4*part-6 .. 4*part-3) only if it holds one of the message's peers;
+//   longer lists: the block copies the list slice that falls in the window from `list`;
+//   OnlySelf: the sender itself, written by the message's own lane.
+template <int IPT, int STAGE, int U, int DBG = 0>
 __global__ __launch_bounds__(kBlock) void emit_kernel(EmitParams p) {
     constexpr int TILE = kBlock * IPT;
-    constexpr int PER = CHUNK / kBlock;
-    static_assert(CHUNK % kBlock == 0 && TILE < (1 << kOwnerIdxBits), "bad emit shape");
-    __shared__ EmitSmem<IPT, CHUNK, STAGE> sm;
+    static_assert(IPT == 1 || IPT == 2, "tile-local message index must fit EmitSmem::Om");
+    __shared__ EmitSmem<IPT, STAGE> sm;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const TableView& tv = p.t;
     const uint32_t m0 = blockIdx.x * TILE;
 
     // ---- A0: CSR offsets of the tile — count-block prefix + block-local scan in message order ----
-    uint32_t e[IPT], st[IPT], sc[IPT];
+    uint32_t e[IPT], st[IPT];
     uint2 inf[IPT];
     uint32_t g0 = 0, T = 0;  // global offset of the tile's first output; outputs in the tile
+    if (tid == 0) sm.n_gq = 0;
     {
         uint32_t incl[IPT];
         // the locators are loaded with the counts, ahead of the offset stores (gfx9: a later
@@ -90,162 +98,109 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(EmitParams p) {
             st[i] = rows + before + incl[i] - e[i];
             rows += tot;
             const uint32_t m = m0 + i * kBlock + tid;
-            if (m < p.M) p.offsets[m] = g + st[i];
+            if (m < p.M && !(DBG & 4)) p.offsets[m] = g + st[i];
         }
         g0 = g;
         T = rows;
     }
     if (!p.peers) return;  // counts-only call: offsets are all that is asked for
 
-    // ---- A: one lane per message — locators, stage positions ----
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-        const bool rec = !(inf[i].x & (kLocGlobal | kLocSelf));
-        sc[i] = !e[i] ? 0u : rec ? (inf[i].y >> 24) : (inf[i].x & kLocSelf) ? 1u : 0u;
-    }
-    uint32_t run;
-    {
-        uint32_t tsum = 0;
-#pragma unroll
-        for (int i = 0; i < IPT; ++i) tsum += sc[i];
-        const uint32_t incl = wave_incl_scan_add(tsum, lane);
-        if (lane == 63) sm.wave_tot[wave] = incl;
-        lds_barrier();
-        run = incl - tsum;
-#pragma unroll
-        for (int u = 0; u < kWaves; ++u)
-            if (u < wave) run += sm.wave_tot[u];
-    }
+    // ---- A: per message — what to stage, and from where ----
+    bool self[IPT];
+    uint32_t self_peer[IPT];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
         const uint32_t j = i * kBlock + tid;
-        const uint32_t pos = run;
-        run += sc[i];
-        const bool fits = pos + sc[i] <= (uint32_t)STAGE;
-        const bool rec = !(inf[i].x & (kLocGlobal | kLocSelf));
-        uint32_t base = 0, skip = kNone, slot = kNone;
-        if (e[i]) {
+        uint32_t slot = kNone, meta = 0;
+        self[i] = e[i] && (inf[i].x & kLocSelf);
+        self_peer[i] = self[i] ? p.sender[m0 + j] : 0u;
+        if (e[i] && !(inf[i].x & kLocSelf)) {
             if (inf[i].x & kLocGlobal) {
-                base = kGlobal | ((inf[i].x & ~kLocGlobal) + 1);
-                skip = inf[i].y;
-            } else if (inf[i].x & kLocSelf) {
-                base = fits ? pos : kSelfSentinel;
-                if (fits) sm.stage[pos] = p.sender[m0 + j];
+                const uint32_t q = atomicAdd(&sm.n_gq, 1u);
+                sm.gq_j[q] = j;
+                sm.gq_off[q] = (inf[i].x & ~kLocGlobal) + 1;
+                sm.gq_skip[q] = inf[i].y;
+                sm.gq_e[q] = e[i];
             } else {
                 const uint32_t s24 = inf[i].y & kSkipNone24;
-                skip = s24 == kSkipNone24 ? kNone : s24;
-                if (fits) {
-                    base = pos;
-                    slot = inf[i].x;
-                } else {  // stage full: read the full list from HBM (offset in the record header)
-                    base = kGlobal | (tv.recs[inf[i].x].list_off + 1);
-                }
+                slot = inf[i].x;
+                meta = (inf[i].y >> 24) | ((s24 == kSkipNone24 ? 0xFFu : s24) << 8);
             }
         }
-        (void)rec;
-        sm.base[j] = base;
-        sm.skip[j] = skip;
         sm.start[j] = st[i];
         sm.slot[j] = slot;
-        sm.spos[j] = (pos << 8) | sc[i];
+        sm.meta[j] = meta;
     }
     lds_barrier();
+    const uint32_t n_gq = sm.n_gq;
 
-    // ---- B: eight lanes per record line — stage the inline peers ----
-    {
-        const int grp = lane >> 3, part = lane & 7;
-        const uint4* recs4 = reinterpret_cast<const uint4*>(tv.recs);
+    const int grp = lane >> 3, part = lane & 7;
+    const uint4* recs4 = reinterpret_cast<const uint4*>(tv.recs);
+    const uint32_t first = part <= 1 ? 0u : 4u * part - 6u;  // first peer index in chunk `part`
+    for (uint32_t w0 = 0; w0 < T; w0 += STAGE) {
+        const uint32_t w1 = T - w0 < (uint32_t)STAGE ? T : w0 + STAGE;
+        // OnlySelf: the message's own lane
+#pragma unroll
+        for (int i = 0; i < IPT; ++i)
+            if (self[i] && st[i] >= w0 && st[i] < w1) {
+                sm.op[st[i] - w0] = self_peer[i];
+                sm.om[st[i] - w0] = (typename EmitSmem<IPT, STAGE>::Om)(i * kBlock + tid);
+            }
+        // inline records: eight lanes per line, U lines per lane in flight
         for (int r0 = 0; r0 < 8 * IPT; r0 += U) {
             uint4 v[U];
-            uint32_t sp[U];
+            uint32_t jj[U], sp[U], mt[U];
             bool act[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t j = wave_msg<IPT>(wave, 8 * (r0 + u) + grp);
-                const uint32_t sl = sm.slot[j];
-                sp[u] = sm.spos[j];
-                act[u] = sl != kNone && part > 0;
-                // unconditional load, no drain between rounds; groups with no record read a dummy
-                // line spread by message index (a shared line would serialise on one L2 channel)
-                const uint64_t line = sl != kNone ? sl : ((m0 + j) & (uint32_t)tv.rec_mask);
-                v[u] = recs4[line * 8 + part];
+                jj[u] = wave_msg<IPT>(wave, 8 * (r0 + u) + grp);
+                const uint32_t sl = sm.slot[jj[u]];
+                sp[u] = sm.start[jj[u]];
+                mt[u] = sm.meta[jj[u]];
+                const uint32_t cnt = mt[u] & 0xFF, skip = mt[u] >> 8;
+                const uint32_t ej = cnt - (skip != 0xFFu ? 1u : 0u);
+                act[u] = sl != kNone && part >= 1 && first < cnt && sp[u] < w1 && sp[u] + ej > w0;
+                if (act[u]) v[u] = (DBG & 1) ? make_uint4(sl, part, 0, 0) : recs4[(uint64_t)sl * 8 + part];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 if (!act[u]) continue;
-                const uint32_t pos = sp[u] >> 8, cnt = sp[u] & 0xFF;
+                const uint32_t cnt = mt[u] & 0xFF, skip = mt[u] >> 8;
                 const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
                 for (int e4 = 0; e4 < 4; ++e4) {
-                    const uint32_t idx = 4 * (part - 1) + e4;
-                    if (idx < cnt) sm.stage[pos + idx] = vv[e4];
+                    const int idx = 4 * part + e4 - kInlineWord0;
+                    if (idx < 0 || (uint32_t)idx >= cnt || (uint32_t)idx == skip) continue;
+                    const uint32_t pos = sp[u] + (uint32_t)idx - ((uint32_t)idx > skip && skip != 0xFFu ? 1u : 0u);
+                    if (pos >= w0 && pos < w1) {
+                        sm.op[pos - w0] = vv[e4];
+                        sm.om[pos - w0] = (typename EmitSmem<IPT, STAGE>::Om)jj[u];
+                    }
                 }
             }
         }
-    }
-    lds_barrier();
-
-    // ---- C: expand + compact, CHUNK outputs at a time ----
-    uint32_t gen = 0;
-    uint32_t carry = 0;
-    for (uint32_t c0 = 0; c0 < T; c0 += CHUNK) {
-        if (gen == 0 || gen == kMaxGen) {  // first chunk of the block / tag space exhausted
-#pragma unroll
-            for (int x = 0; x < 2 * PER; ++x) (&sm.owner[0][0])[x * kBlock + tid] = 0;
-            gen = 0;
-            lds_barrier();
-        }
-        ++gen;
-        uint32_t* own = sm.owner[gen & 1];
-        const uint32_t tag = gen << kOwnerIdxBits;
-#pragma unroll
-        for (int i = 0; i < IPT; ++i)
-            if (e[i] && st[i] >= c0 && st[i] < c0 + CHUNK) own[st[i] - c0] = tag | (uint32_t)(i * kBlock + tid + 1);
-        lds_barrier();
-        uint32_t v[PER];
-        uint32_t tm = 0;
-#pragma unroll
-        for (int x = 0; x < PER; ++x) {
-            const uint32_t y = own[tid * PER + x];
-            tm = y > tm ? y : tm;
-            v[x] = tm;
-        }
-        const uint32_t wi = wave_incl_scan_max(tm, lane);
-        if (lane == 63) sm.wave_tot[wave] = wi;
-        lds_barrier();
-        uint32_t before = carry ? (tag | carry) : 0u;
-#pragma unroll
-        for (int u = 0; u < kWaves; ++u)
-            if (u < wave) before = before > sm.wave_tot[u] ? before : sm.wave_tot[u];
-        const uint32_t lane_before = __shfl_up(wi, 1, 64);
-        if (lane > 0) before = before > lane_before ? before : lane_before;
-#pragma unroll
-        for (int x = 0; x < PER; ++x) own[tid * PER + x] = v[x] > before ? v[x] : before;
-        lds_barrier();
-        carry = own[CHUNK - 1] & kOwnerIdxMask;
-#pragma unroll
-        for (int x = 0; x < PER; ++x) {
-            const uint32_t jl = x * kBlock + tid;
-            const uint32_t j = c0 + jl;
-            if (j < T) {
-                const uint32_t k = (own[jl] & kOwnerIdxMask) - 1;
-                const uint32_t r = j - sm.start[k];
-                const uint32_t b = sm.base[k];
-                uint32_t peer;
-                if (b == kSelfSentinel) {
-                    peer = p.sender[m0 + k];
-                } else {
-                    const uint32_t idx = (b & ~kGlobal) + r + (r >= sm.skip[k] ? 1u : 0u);
-                    peer = (b & kGlobal) ? tv.list[idx] : sm.stage[idx];
-                }
-                const uint64_t out = (uint64_t)g0 + j;
-                if (out < p.capacity) {
-                    p.peers[out] = peer;
-                    if (p.msgs) p.msgs[out] = m0 + k;
-                }
+        // long lists: the block copies each one's slice of the window from `list`
+        for (uint32_t q = 0; q < n_gq; ++q) {
+            const uint32_t j = sm.gq_j[q], s0 = sm.start[j], ej = sm.gq_e[q];
+            const uint32_t lo = s0 > w0 ? s0 : w0, hi = s0 + ej < w1 ? s0 + ej : w1;
+            const uint32_t off = sm.gq_off[q], skip = sm.gq_skip[q];
+            for (uint32_t k = lo + tid; k < hi; k += kBlock) {
+                const uint32_t o = k - s0;
+                sm.op[k - w0] = tv.list[off + o + (o >= skip ? 1u : 0u)];
+                sm.om[k - w0] = (typename EmitSmem<IPT, STAGE>::Om)j;
             }
         }
-        // no barrier: the next chunk marks the other owner buffer
+        lds_barrier();
+        // copy-out: one coalesced stream per array
+        const uint32_t n = w1 - w0;
+        for (uint32_t k = tid; k < n; k += kBlock) {
+            const uint64_t out = (uint64_t)g0 + w0 + k;
+            if (out < p.capacity && !(DBG & 2)) {
+                p.peers[out] = sm.op[k];
+                if (p.msgs) p.msgs[out] = m0 + sm.om[k];
+            }
+        }
+        if (w1 < T) lds_barrier();  // the next window reuses the image
     }
 }
 

@@ -25,7 +25,6 @@
 #include <algorithm>
 
 #include "route_count.hpp"
-#include "route_count_lpm.hpp"
 #include "route_emit.hpp"
 #include "route_scan.hpp"
 
@@ -42,43 +41,36 @@ struct Cfg {
     void (*emit)(const EmitParams&, hipStream_t, unsigned);
 };
 
-template <int IPT, int U>
+template <int IPT, int MINW>
 void launch_count(const CountParams& p, hipStream_t s, unsigned grid) {
     if (p.in.keys)
-        hipLaunchKernelGGL((count_kernel<true, IPT, U>), dim3(grid), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL((count_kernel<true, IPT, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
     else
-        hipLaunchKernelGGL((count_kernel<false, IPT, U>), dim3(grid), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL((count_kernel<false, IPT, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
 }
 
-template <int IPT, int MINW>
-void launch_count_lpm(const CountParams& p, hipStream_t s, unsigned grid) {
-    if (p.in.keys)
-        hipLaunchKernelGGL((count_lpm_kernel<true, IPT, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
-    else
-        hipLaunchKernelGGL((count_lpm_kernel<false, IPT, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
-}
-
-template <int IPT, int CHUNK, int STAGE, int U>
+template <int IPT, int STAGE, int U, int DBG = 0>
 void launch_emit(const EmitParams& p, hipStream_t s, unsigned grid) {
-    hipLaunchKernelGGL((emit_kernel<IPT, CHUNK, STAGE, U>), dim3(grid), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL((emit_kernel<IPT, STAGE, U, DBG>), dim3(grid), dim3(kBlock), 0, s, p);
 }
 
-#define WQ_CFG(cipt, cu, eipt, chunk, stage, eu) \
-    {cipt, eipt, &launch_count<cipt, cu>, &launch_emit<eipt, chunk, stage, eu>}
-#define WQ_CFG_LPM(cipt, minw, eipt, chunk, stage, eu) \
-    {cipt, eipt, &launch_count_lpm<cipt, minw>, &launch_emit<eipt, chunk, stage, eu>}
-// count: (messages per thread, record lines per 8-lane round) or lane-per-message (LPM);
-// emit: (messages per thread, expansion chunk, stage words, lines per round)
+#define WQ_CFG(cipt, minw, eipt, stage, eu) \
+    {cipt, eipt, &launch_count<cipt, minw>, &launch_emit<eipt, stage, eu>}
+// count: (messages per lane, min waves per SIMD); emit: (messages per thread, window positions,
+// record lines per lane in flight)
 const Cfg kCfgs[] = {
-    WQ_CFG_LPM(2, 4, 1, 1024, 3072, 8),  // 0: default (count 52 us on C2, profiles/r01_kernel_stats_v7.csv)
-    WQ_CFG_LPM(1, 1, 1, 1024, 3072, 8),  // 1
-    WQ_CFG(2, 2, 1, 512, 3072, 8),       // 2: 8 lanes per record line
-    WQ_CFG(2, 4, 1, 1024, 3072, 8),      // 3
-    WQ_CFG(4, 4, 2, 1024, 6144, 8),      // 4
-    WQ_CFG_LPM(2, 4, 1, 512, 3072, 8),   // 5
+    WQ_CFG(4, 2, 1, 4096, 8),  // 0: default
+    WQ_CFG(4, 2, 1, 3072, 8),  // 1
+    WQ_CFG(4, 2, 2, 6144, 8),  // 2
+    WQ_CFG(2, 4, 1, 4096, 8),  // 3
+    WQ_CFG(4, 2, 1, 2048, 8),  // 4
+    WQ_CFG(4, 2, 1, 4096, 4),  // 5
+    {4, 1, &launch_count<4, 2>, &launch_emit<1, 3072, 8, 1>},  // 6 timing only: no record loads
+    {4, 1, &launch_count<4, 2>, &launch_emit<1, 3072, 8, 2>},  // 7 timing only: no output stores
+    {4, 1, &launch_count<4, 2>, &launch_emit<1, 3072, 8, 4>},  // 8 timing only: no offset stores
+    {4, 1, &launch_count<4, 2>, &launch_emit<1, 3072, 8, 7>},  // 9 timing only: none
 };
 #undef WQ_CFG
-#undef WQ_CFG_LPM
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 }  // namespace
 

@@ -172,7 +172,10 @@ __global__ void k_insert_cubes(EvView st, const uint32_t* __restrict__ cube_star
         r.pk = pk;
         r.count = cnt;
         r.list_off = j + c;
-#pragma unroll 4
+        uint64_t sig = 0;
+        for (uint32_t i = 0; i < cnt; ++i) sig |= peer_sig(st.p[j + i]);
+        r.sig = sig;
+#pragma unroll 2
         for (int i = 0; i < kInline; ++i) r.peers[i] = (uint32_t)i < cnt ? st.p[j + i] : 0xFFFFFFFFu;
         return;
     }
@@ -478,10 +481,11 @@ int table_rebuild_derived(wq_router* h) {
     WQ_HIP(h, hipMemsetAsync(t.claim.p, 0, cap * 4, s));
     t.cap = cap;
     t.shift = 64 - log2cap;
-    // record table: load <= 0.3 so a lookup is ~1.2 line reads
+    // record table: load <= 1/8, so ~97% of lookups end at the home slot (one round trip). The
+    // untouched slots cost memory, not time: a tick touches one line per cube whatever the capacity
     uint64_t rcap = 1024;
     int log2r = 10;
-    while (rcap * 3 < 10ull * n_cubes) {
+    while (rcap < 8ull * n_cubes) {
         rcap <<= 1;
         log2r++;
     }
