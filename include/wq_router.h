@@ -187,6 +187,11 @@ int wq_debug_set_hash_bits(wq_router* h, int bits);
 /* ---- tuning hook: select a compiled route-kernel shape (messages per thread, expansion chunk);
  * 0 is the default. Results are identical for every shape. */
 int wq_debug_set_route_config(wq_router* h, int cfg);
+/* Number of route kernel configurations (valid cfg values are 0 .. n-1). */
+int wq_debug_route_config_count(void);
+/* Diagnostics: when d_stamps is non-null, the single-launch tick writes four s_memrealtime stamps
+ * (100 MHz) per block — start, counted, prefix known, done — to d_stamps[4*block ..]. */
+int wq_debug_set_timeline(wq_router* h, uint64_t* d_stamps);
 
 #ifdef __cplusplus
 }

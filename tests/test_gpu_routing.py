@@ -236,10 +236,10 @@ def test_hot_cube_skew_and_ragged_tiles():
     assert P > 300 * n_hot  # ~660 hot messages, 2/3 of them not OnlySelf
 
 
-@pytest.mark.parametrize("per_cube", [27, 28, 29])
+@pytest.mark.parametrize("per_cube", [23, 24, 25, 60])
 def test_inline_boundary_and_stage_overflow(per_cube):
-    """Cubes with 27/28/29 subscribers (the 28-peer inline record boundary); every message lands in
-    them, so a tile's staged lists exceed the LDS stage and the overflow path reads HBM lists."""
+    """Cubes around the inline record boundary (kInline = 24 peers: 23/24/25) and far past it (60),
+    every message landing in them, under every route kernel configuration."""
     r = mk_router(16)
     o = orc.COracle(16)
     n_cubes = 40
@@ -253,7 +253,7 @@ def test_inline_boundary_and_stage_overflow(per_cube):
     M = 5000
     mpos = np.stack([rng.below(n_cubes, M) * 16.0 + rng.uniform(0.5, 15.5, M), rng.uniform(0.5, 15.5, M),
                      -rng.uniform(0.5, 15.5, M)], 1)
-    for cfg in range(6):
+    for cfg in range(r.route_config_count()):
         r.set_route_config(cfg)
         _compare(r, o, mpos, np.zeros(M, np.uint32), rng.below(n_cubes * per_cube, M),
                  rng.below(3, M).astype(np.uint8))

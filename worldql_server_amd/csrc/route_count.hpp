@@ -3,9 +3,9 @@
 // One lane per message, IPT messages per lane. Per message the pass needs the cube's peer count
 // and whether the sender is one of its peers (local_message.rs:60-86). Both come from the first
 // 32 bytes of the cube's 128-byte record line (wq_device.hpp): chunk 0 = {pk, count, list_off},
-// chunk 1 = {sig, p0, p1}, where sig is a 64-bit Bloom signature of the cube's peers. A sender
-// whose signature bits are not all set is certainly not subscribed; only the rest (C2: ~7% false
-// positives plus the true positives) read further chunks of the inline list. So a lookup is two
+// chunk 1 = {sig, -}, where sig is a 64-bit Bloom signature of the cube's peers. A sender whose
+// signature bits are not all set is certainly not subscribed; only the rest (C2: ~7% false
+// positives plus the true positives) read the inline peers, two chunks per round. So a lookup is two
 // 16-byte loads and 8 VGPRs per message, not eight loads and 32 VGPRs for the whole line.
 //
 // Work that needs another memory round trip — a linear-probe step past a foreign key, or the
@@ -23,6 +23,9 @@ struct CountParams {
     uint32_t* e;           // out: filtered recipient count e_m
     uint2* info;           // out: locator
     uint32_t* tile_total;  // out: sum of e over each block's messages
+    uint32_t* tile_F;      // out: candidates (unfiltered peers) over each block's messages
+                           // (per-block words, summed by tile_scan: one shared atomic counter
+                           // would serialise ~1k blocks at ~90 adds/us)
     wq_route_counters* cnt;
     wq_route_counters* cnt_next;
 };
@@ -49,21 +52,13 @@ __device__ __forceinline__ void finish_message(uint32_t cnt, uint8_t rp, bool in
 // per-message probe state
 constexpr uint32_t kStDone = 0, kStProbe = 1, kStVerify = 2;
 
-template <bool RAW_KEYS, int IPT, int MINW>
-__global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
-    __shared__ uint64_t wave_F[kWaves];
-    __shared__ uint64_t wave_E[kWaves];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const TableView& tv = p.t;
-    if (blockIdx.x == 0 && tid == 0) {
-        p.cnt_next->n_pairs = 0;
-        p.cnt_next->n_candidates = 0;
-        p.cnt_next->overflow = 0;
-        p.cnt_next->error = 0;
-    }
-    const uint32_t m0 = blockIdx.x * (kBlock * IPT);
-    uint64_t F_local = 0;
-    uint32_t E_local = 0;
+// Messages m0 + i*kBlock + threadIdx.x, i < IPT: filtered count and locator of each (zero for
+// m >= in.M), with F (candidates) and E (recipients) accumulated into the caller's sums.
+template <bool RAW_KEYS, int IPT, int DBG = 0>
+__device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& tv, uint32_t m0,
+                                           uint32_t (&e_out)[IPT], uint2 (&inf_out)[IPT], uint64_t& F_local,
+                                           uint32_t& E_local) {
+    const int tid = threadIdx.x;
 
     // ---- A: inputs (all loads first), quantise (kernel 1), packed key, home slot ----
     uint32_t in_w[IPT], in_me[IPT];
@@ -72,24 +67,23 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
         const uint32_t m = m0 + i * kBlock + tid;
-        const uint32_t mm = m < p.in.M ? m : 0;
-        in_w[i] = p.in.world[mm];
-        in_me[i] = p.in.sender[mm];
-        in_rp[i] = p.in.repl[mm];
-        const uint64_t* src = RAW_KEYS ? reinterpret_cast<const uint64_t*>(p.in.keys)
-                                       : reinterpret_cast<const uint64_t*>(p.in.pos);
+        const uint32_t mm = m < in.M ? m : 0;
+        in_w[i] = in.world[mm];
+        in_me[i] = in.sender[mm];
+        in_rp[i] = in.repl[mm];
+        const uint64_t* src = RAW_KEYS ? reinterpret_cast<const uint64_t*>(in.keys)
+                                       : reinterpret_cast<const uint64_t*>(in.pos);
         in_c[i][0] = src[3ull * mm];
         in_c[i][1] = src[3ull * mm + 1];
         in_c[i][2] = src[3ull * mm + 2];
     }
     uint64_t pk[IPT];
-    uint32_t sl[IPT], st[IPT], e_out[IPT];
+    uint32_t sl[IPT], st[IPT];
     bool via_rec[IPT];
-    uint2 inf_out[IPT];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
         const uint32_t m = m0 + i * kBlock + tid;
-        const bool valid = m < p.in.M;
+        const bool valid = m < in.M;
         const uint32_t w = in_w[i];
         int64_t x, y, z;
         if (RAW_KEYS) {
@@ -97,9 +91,9 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
             y = (int64_t)in_c[i][1];
             z = (int64_t)in_c[i][2];
         } else {
-            x = coord_clamp_dev(__longlong_as_double((long long)in_c[i][0]), tv.sf, p.in.si);
-            y = coord_clamp_dev(__longlong_as_double((long long)in_c[i][1]), tv.sf, p.in.si);
-            z = coord_clamp_dev(__longlong_as_double((long long)in_c[i][2]), tv.sf, p.in.si);
+            x = coord_clamp_dev(__longlong_as_double((long long)in_c[i][0]), tv.sf, in.si);
+            y = coord_clamp_dev(__longlong_as_double((long long)in_c[i][1]), tv.sf, in.si);
+            z = coord_clamp_dev(__longlong_as_double((long long)in_c[i][2]), tv.sf, in.si);
         }
         pk[i] = 0;
         const bool reg = pack_key(w, x, y, z, tv.sf, &pk[i]);
@@ -136,7 +130,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
         c0[i] = recs4[(uint64_t)sl[i] * 8];
-        c1[i] = recs4[(uint64_t)sl[i] * 8 + 1];
+        c1[i] = (DBG & 1) ? c0[i] : recs4[(uint64_t)sl[i] * 8 + 1];
     }
     uint32_t cnt[IPT], loff[IPT], lt[IPT], vc[IPT];
     bool has[IPT];
@@ -162,17 +156,10 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
                     if (cnt[i] && in_rp[i] != WQ_REPL_INCLUDING_SELF) {
                         const uint64_t sig = ((uint64_t)c1[i].y << 32) | c1[i].x;
                         const uint64_t bits = peer_sig(me);
-                        if ((sig & bits) == bits) {  // maybe subscribed: verify
-                            if (cnt[i] <= (uint32_t)kInline) {
-                                // p0, p1 are in chunk 1; the rest from chunk 2 on
-                                const bool in0 = c1[i].z == me, in1 = cnt[i] > 1 && c1[i].w == me;
-                                lt[i] = (c1[i].z < me ? 1u : 0u) + ((cnt[i] > 1 && c1[i].w < me) ? 1u : 0u);
-                                has[i] = in0 | in1;
-                                const bool stop = has[i] || c1[i].z > me || (cnt[i] > 1 && c1[i].w > me);
-                                if (!stop && cnt[i] > 2) {
-                                    st[i] = kStVerify;
-                                    vc[i] = 2;
-                                }
+                        if (!(DBG & 3) && (sig & bits) == bits) {  // maybe subscribed: verify
+                            if (cnt[i] <= (uint32_t)kInline) {  // inline peers from chunk 2 on
+                                st[i] = kStVerify;
+                                vc[i] = 2;
                             } else {  // > kInline peers: binary search of the full list (rare in C2)
                                 const uint32_t* lp = tv.list + loff[i] + 1;
                                 lt[i] = lower_bound_dev(lp, cnt[i], me);
@@ -184,10 +171,10 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
                     sl[i] = (sl[i] + 1) & (uint32_t)tv.rec_mask;
                 }
             } else if (st[i] == kStVerify) {
-                // chunks vc, vc+1 hold peers 4*vc-6 .. 4*vc+1; the list is ascending, so the first
+                // chunks vc, vc+1 hold peers 4*vc-8 .. 4*vc-1; the list is ascending, so the first
                 // peer >= me ends the search
                 const uint32_t v[8] = {c0[i].x, c0[i].y, c0[i].z, c0[i].w, c1[i].x, c1[i].y, c1[i].z, c1[i].w};
-                const uint32_t b = 4 * vc[i] - 6;
+                const uint32_t b = 4 * vc[i] - kInlineWord0;
                 bool stop = false;
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
@@ -197,7 +184,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
                     stop |= in & (v[q] >= me);
                 }
                 vc[i] += 2;
-                if (stop || 4 * vc[i] - 6 >= cnt[i]) st[i] = kStDone;
+                if (stop || 4 * vc[i] - kInlineWord0 >= cnt[i]) st[i] = kStDone;
             }
             pending |= st[i] != kStDone;
         }
@@ -213,16 +200,39 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
 
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
-        const uint32_t m = m0 + i * kBlock + tid;
-        if (m >= p.in.M) continue;
         if (via_rec[i]) {
             finish_message(cnt[i], in_rp[i], cnt[i] <= (uint32_t)kInline, sl[i], loff[i], lt[i], has[i], &e_out[i],
                            &inf_out[i]);
             F_local += cnt[i];
             E_local += e_out[i];
         }
-        p.e[m] = e_out[i];
-        p.info[m] = inf_out[i];
+    }
+}
+
+template <bool RAW_KEYS, int IPT, int MINW, int DBG = 0>
+__global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
+    __shared__ uint64_t wave_F[kWaves];
+    __shared__ uint64_t wave_E[kWaves];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (blockIdx.x == 0 && tid == 0) {
+        p.cnt_next->n_pairs = 0;
+        p.cnt_next->n_candidates = 0;
+        p.cnt_next->overflow = 0;
+        p.cnt_next->error = 0;
+    }
+    const uint32_t m0 = blockIdx.x * (kBlock * IPT);
+    uint64_t F_local = 0;
+    uint32_t E_local = 0;
+    uint32_t e_out[IPT];
+    uint2 inf_out[IPT];
+    count_rows<RAW_KEYS, IPT, DBG>(p.in, p.t, m0, e_out, inf_out, F_local, E_local);
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+        const uint32_t m = m0 + i * kBlock + tid;
+        if (m < p.in.M) {
+            p.e[m] = e_out[i];
+            p.info[m] = inf_out[i];
+        }
     }
 
     const uint64_t Fw = wave_sum_u64(F_local);
@@ -239,9 +249,11 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
             Fb += wave_F[w];
             Eb += wave_E[w];
         }
-        if (Fb) atomicAdd(reinterpret_cast<unsigned long long*>(&p.cnt->n_candidates), (unsigned long long)Fb);
+        p.tile_F[blockIdx.x] = Fb > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Fb;
         p.tile_total[blockIdx.x] = Eb > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Eb;
+        if (Eb > 0xFFFFFFFFull) atomicOr(&p.cnt->error, 2u);
     }
 }
 
 }  // namespace wq
+

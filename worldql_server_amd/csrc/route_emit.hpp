@@ -1,7 +1,5 @@
 // route_emit.hpp — pass 3 of the tick: emit_kernel (see wq_route.hip).
 #pragma once
-#include <type_traits>
-
 #include "route_common.hpp"
 
 namespace wq {
@@ -23,185 +21,185 @@ struct EmitParams {
     uint64_t capacity;
 };
 
-template <int IPT, int STAGE>
-struct EmitSmem {
-    using Om = typename std::conditional<IPT == 1, uint8_t, uint16_t>::type;
-    uint32_t op[STAGE];             // window of the tile's output: peers, in output order
-    Om om[STAGE];                   // ... and the tile-local index of each output's message
-    uint32_t start[kBlock * IPT];   // tile-local first output of the message
-    uint32_t slot[kBlock * IPT];    // inline record slot, or kNone
-    uint32_t meta[kBlock * IPT];    // inline: count | skipped index << 8 (0xFF: none)
-    uint32_t gq_j[kBlock * IPT];    // messages whose list is read from `list` (> kInline peers)
-    uint32_t gq_off[kBlock * IPT];  // ... its list offset (first peer)
-    uint32_t gq_skip[kBlock * IPT]; // ... skipped list index or kNone
-    uint32_t gq_e[kBlock * IPT];    // ... outputs
+// LDS of one emit row (256 messages): an image of a window of the row's output, aligned to
+// 16-byte quads of the global output, and the messages whose list is read from `list`.
+template <int STAGE>
+struct EmitRowSmem {
+    alignas(16) uint32_t op[STAGE];  // peers of window positions, in output order
+    alignas(16) uint8_t om[STAGE];   // ... and the row-local index of each position's message
+    uint32_t gq_j[kBlock];    // messages with more than kInline peers (or a full-key slot-table cube)
+    uint32_t gq_off[kBlock];  // ... index of the list's first peer in `list`
+    uint32_t gq_skip[kBlock]; // ... skipped list index or kNone
+    uint32_t gq_e[kBlock];    // ... outputs
+    uint32_t gq_st[kBlock];   // ... row-local first output
     uint32_t n_gq;
-    uint32_t wave_tot[kWaves];
-    uint32_t rowt[IPT + 1][kWaves]; // per-row wave totals of e (+ earlier messages of the count block)
 };
 
-// Pass 3. The tile's outputs [0, T) are produced in windows of STAGE positions: every message's
-// peers are written straight into an LDS image of the window IN OUTPUT ORDER (the sender's own
-// entry skipped while staging), together with the message's tile-local index, and the window is
-// then copied out with coalesced stores. C2 tiles (256 messages, ~2,560 outputs) take one window.
-//   inline records (<= kInline peers): eight lanes per record line, lane `part` reading chunk
-//     `part` (peers 4*part-6 .. 4*part-3) only if it holds one of the message's peers;
-//   longer lists: the block copies the list slice that falls in the window from `list`;
-//   OnlySelf: the sender itself, written by the message's own lane.
-template <int IPT, int STAGE, int U, int DBG = 0>
-__global__ __launch_bounds__(kBlock) void emit_kernel(EmitParams p) {
-    constexpr int TILE = kBlock * IPT;
-    static_assert(IPT == 1 || IPT == 2, "tile-local message index must fit EmitSmem::Om");
-    __shared__ EmitSmem<IPT, STAGE> sm;
+struct EmitOut {
+    const uint32_t* sender;
+    uint32_t* peers;
+    uint32_t* msgs;
+    uint64_t capacity;
+};
+
+// Kernel (3) for one row of 256 messages m0 + threadIdx.x whose filtered counts e, locators inf
+// and row-local first outputs st the caller holds; the row's outputs go to [g0, g0 + T).
+// The outputs are assembled in LDS in output order, in windows of STAGE positions aligned to the
+// global output's 16-byte quads, then written with one 16-byte store per lane per array (the
+// row's first and last quads, shared with the neighbouring rows, word by word).
+//   inline records (<= kInline peers): eight lanes per record line, lane `part` < 6 reading chunk
+//     2 + part = peers 4*part .. 4*part+3 only if it holds one of the message's peers; all 64
+//     messages of a wave in flight at once; the sender's own entry is dropped while staging;
+//   longer lists: the block copies the window's slice of each from `list`;
+//   OnlySelf: the sender, by its own lane.
+// Every thread of the block must call it (it contains barriers); it ends with a barrier.
+template <int STAGE>
+__device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView& tv, const EmitOut& o, uint32_t m0,
+                                         uint32_t e, uint2 inf, uint32_t st, uint64_t g0, uint32_t T) {
+    static_assert(STAGE % 1024 == 0, "STAGE: whole quads for every lane");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const TableView& tv = p.t;
-    const uint32_t m0 = blockIdx.x * TILE;
-
-    // ---- A0: CSR offsets of the tile — count-block prefix + block-local scan in message order ----
-    uint32_t e[IPT], st[IPT];
-    uint2 inf[IPT];
-    uint32_t g0 = 0, T = 0;  // global offset of the tile's first output; outputs in the tile
     if (tid == 0) sm.n_gq = 0;
-    {
-        uint32_t incl[IPT];
-        // the locators are loaded with the counts, ahead of the offset stores (gfx9: a later
-        // load-wait would otherwise also wait for those stores)
-#pragma unroll
-        for (int i = 0; i < IPT; ++i) {
-            const uint32_t m = m0 + i * kBlock + tid;
-            e[i] = m < p.M ? p.e[m] : 0u;
-            inf[i] = (p.peers && m < p.M) ? p.info[m] : make_uint2(0, kNone);
+    lds_barrier();
+    uint32_t sl = kNone, cnt = 0, skip = kNone;
+    const bool self = e && (inf.x & kLocSelf);
+    const uint32_t self_peer = self ? o.sender[m0 + tid] : 0u;
+    if (e && !self) {
+        if (inf.x & kLocGlobal) {
+            const uint32_t q = atomicAdd(&sm.n_gq, 1u);
+            sm.gq_j[q] = tid;
+            sm.gq_off[q] = (inf.x & ~kLocGlobal) + 1;
+            sm.gq_skip[q] = inf.y;
+            sm.gq_e[q] = e;
+            sm.gq_st[q] = st;
+        } else {
+            const uint32_t s24 = inf.y & kSkipNone24;
+            sl = inf.x;
+            cnt = inf.y >> 24;
+            skip = s24 == kSkipNone24 ? kNone : s24;
         }
-#pragma unroll
-        for (int i = 0; i < IPT; ++i) {
-            incl[i] = wave_incl_scan_add(e[i], lane);
-            if (lane == 63) sm.rowt[i][wave] = incl[i];
-        }
-        const uint32_t ct0 = (m0 / p.count_tile) * p.count_tile;
-        uint32_t part = 0;
-        for (uint32_t m = ct0 + tid; m < m0; m += kBlock) part += p.e[m];
-        part = (uint32_t)wave_sum_u64(part);
-        if (lane == 0) sm.rowt[IPT][wave] = part;
-        lds_barrier();
-        uint32_t g = p.tile_prefix[m0 / p.count_tile], rows = 0;
-#pragma unroll
-        for (int u = 0; u < kWaves; ++u) g += sm.rowt[IPT][u];
-#pragma unroll
-        for (int i = 0; i < IPT; ++i) {
-            uint32_t before = 0, tot = 0;
-#pragma unroll
-            for (int u = 0; u < kWaves; ++u) {
-                const uint32_t t = sm.rowt[i][u];
-                if (u < wave) before += t;
-                tot += t;
-            }
-            st[i] = rows + before + incl[i] - e[i];
-            rows += tot;
-            const uint32_t m = m0 + i * kBlock + tid;
-            if (m < p.M && !(DBG & 4)) p.offsets[m] = g + st[i];
-        }
-        g0 = g;
-        T = rows;
     }
-    if (!p.peers) return;  // counts-only call: offsets are all that is asked for
-
-    // ---- A: per message — what to stage, and from where ----
-    bool self[IPT];
-    uint32_t self_peer[IPT];
+    // record chunks of the wave's 64 messages: message q by lanes 8*(q%8) .. +7, round q/8
+    const int grp = lane >> 3, part = lane & 7;
+    const uint4* recs4 = reinterpret_cast<const uint4*>(tv.recs);
+    uint4 v[8];
+    uint32_t q_cnt[8], q_skip[8], q_st[8];
 #pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-        const uint32_t j = i * kBlock + tid;
-        uint32_t slot = kNone, meta = 0;
-        self[i] = e[i] && (inf[i].x & kLocSelf);
-        self_peer[i] = self[i] ? p.sender[m0 + j] : 0u;
-        if (e[i] && !(inf[i].x & kLocSelf)) {
-            if (inf[i].x & kLocGlobal) {
-                const uint32_t q = atomicAdd(&sm.n_gq, 1u);
-                sm.gq_j[q] = j;
-                sm.gq_off[q] = (inf[i].x & ~kLocGlobal) + 1;
-                sm.gq_skip[q] = inf[i].y;
-                sm.gq_e[q] = e[i];
-            } else {
-                const uint32_t s24 = inf[i].y & kSkipNone24;
-                slot = inf[i].x;
-                meta = (inf[i].y >> 24) | ((s24 == kSkipNone24 ? 0xFFu : s24) << 8);
-            }
-        }
-        sm.start[j] = st[i];
-        sm.slot[j] = slot;
-        sm.meta[j] = meta;
+    for (int u = 0; u < 8; ++u) {
+        const int src = 8 * u + grp;
+        const uint32_t qs = __shfl(sl, src, 64);
+        q_cnt[u] = __shfl(cnt, src, 64);
+        q_skip[u] = __shfl(skip, src, 64);
+        q_st[u] = __shfl(st, src, 64);
+        if (part < 6 && qs != kNone && 4u * part < q_cnt[u]) v[u] = recs4[(uint64_t)qs * 8 + 2 + part];
+        else q_cnt[u] = 0;  // nothing to stage from this lane
     }
     lds_barrier();
     const uint32_t n_gq = sm.n_gq;
-
-    const int grp = lane >> 3, part = lane & 7;
-    const uint4* recs4 = reinterpret_cast<const uint4*>(tv.recs);
-    const uint32_t first = part <= 1 ? 0u : 4u * part - 6u;  // first peer index in chunk `part`
-    for (uint32_t w0 = 0; w0 < T; w0 += STAGE) {
-        const uint32_t w1 = T - w0 < (uint32_t)STAGE ? T : w0 + STAGE;
-        // OnlySelf: the message's own lane
+    // window w covers global outputs [gA + w0, gA + w0 + STAGE), gA = g0 rounded down to a quad
+    const uint64_t gA = g0 & ~3ull;
+    const uint32_t lead = (uint32_t)(g0 - gA);  // row output r sits at image index lead + r - w0
+    const uint32_t span = lead + T;
+    for (uint32_t w0 = 0; w0 < span; w0 += STAGE) {
+        const uint32_t w1 = span - w0 < (uint32_t)STAGE ? span : w0 + STAGE;
+        if (self && lead + st >= w0 && lead + st < w1) {
+            sm.op[lead + st - w0] = self_peer;
+            sm.om[lead + st - w0] = (uint8_t)tid;
+        }
 #pragma unroll
-        for (int i = 0; i < IPT; ++i)
-            if (self[i] && st[i] >= w0 && st[i] < w1) {
-                sm.op[st[i] - w0] = self_peer[i];
-                sm.om[st[i] - w0] = (typename EmitSmem<IPT, STAGE>::Om)(i * kBlock + tid);
+        for (int u = 0; u < 8; ++u) {
+            if (!q_cnt[u]) continue;
+            const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            const uint8_t j = (uint8_t)(wave * 64 + 8 * u + grp);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t idx = 4u * part + i;  // peer index in the cube's list
+                if (idx >= q_cnt[u] || idx == q_skip[u]) continue;
+                const uint32_t pos = lead + q_st[u] + idx - (idx > q_skip[u] && q_skip[u] != kNone ? 1u : 0u);
+                if (pos >= w0 && pos < w1) {
+                    sm.op[pos - w0] = vv[i];
+                    sm.om[pos - w0] = j;
+                }
             }
-        // inline records: eight lanes per line, U lines per lane in flight
-        for (int r0 = 0; r0 < 8 * IPT; r0 += U) {
-            uint4 v[U];
-            uint32_t jj[U], sp[U], mt[U];
-            bool act[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                jj[u] = wave_msg<IPT>(wave, 8 * (r0 + u) + grp);
-                const uint32_t sl = sm.slot[jj[u]];
-                sp[u] = sm.start[jj[u]];
-                mt[u] = sm.meta[jj[u]];
-                const uint32_t cnt = mt[u] & 0xFF, skip = mt[u] >> 8;
-                const uint32_t ej = cnt - (skip != 0xFFu ? 1u : 0u);
-                act[u] = sl != kNone && part >= 1 && first < cnt && sp[u] < w1 && sp[u] + ej > w0;
-                if (act[u]) v[u] = (DBG & 1) ? make_uint4(sl, part, 0, 0) : recs4[(uint64_t)sl * 8 + part];
+        }
+        for (uint32_t q = 0; q < n_gq; ++q) {
+            const uint32_t j = sm.gq_j[q], s0 = lead + sm.gq_st[q], ej = sm.gq_e[q];
+            const uint32_t lo = s0 > w0 ? s0 : w0, hi = s0 + ej < w1 ? s0 + ej : w1;
+            const uint32_t off = sm.gq_off[q], sk = sm.gq_skip[q];
+            for (uint32_t k = lo + tid; k < hi; k += kBlock) {
+                const uint32_t oi = k - s0;
+                sm.op[k - w0] = tv.list[off + oi + (oi >= sk ? 1u : 0u)];
+                sm.om[k - w0] = (uint8_t)j;
             }
+        }
+        lds_barrier();
+        // copy-out, quad t of the window by thread t % 256
+        for (uint32_t qd = w0 + 4u * tid; qd < w1; qd += 4u * kBlock) {
+            const uint4 pv = *reinterpret_cast<const uint4*>(&sm.op[qd - w0]);
+            const uint32_t mv = *reinterpret_cast<const uint32_t*>(&sm.om[qd - w0]);
+            const uint64_t out0 = gA + qd;
+            const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+            const uint32_t mw[4] = {m0 + (mv & 0xFF), m0 + ((mv >> 8) & 0xFF), m0 + ((mv >> 16) & 0xFF), m0 + (mv >> 24)};
+            if (qd >= lead && qd + 4 <= span && out0 + 4 <= o.capacity) {
+                *reinterpret_cast<uint4*>(o.peers + out0) = pv;
+                if (o.msgs) *reinterpret_cast<uint4*>(o.msgs + out0) = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+            } else {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (!act[u]) continue;
-                const uint32_t cnt = mt[u] & 0xFF, skip = mt[u] >> 8;
-                const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                for (int e4 = 0; e4 < 4; ++e4) {
-                    const int idx = 4 * part + e4 - kInlineWord0;
-                    if (idx < 0 || (uint32_t)idx >= cnt || (uint32_t)idx == skip) continue;
-                    const uint32_t pos = sp[u] + (uint32_t)idx - ((uint32_t)idx > skip && skip != 0xFFu ? 1u : 0u);
-                    if (pos >= w0 && pos < w1) {
-                        sm.op[pos - w0] = vv[e4];
-                        sm.om[pos - w0] = (typename EmitSmem<IPT, STAGE>::Om)jj[u];
+                for (uint32_t i = 0; i < 4; ++i) {
+                    if (qd + i >= lead && qd + i < span && out0 + i < o.capacity) {
+                        o.peers[out0 + i] = pw[i];
+                        if (o.msgs) o.msgs[out0 + i] = mw[i];
                     }
                 }
             }
         }
-        // long lists: the block copies each one's slice of the window from `list`
-        for (uint32_t q = 0; q < n_gq; ++q) {
-            const uint32_t j = sm.gq_j[q], s0 = sm.start[j], ej = sm.gq_e[q];
-            const uint32_t lo = s0 > w0 ? s0 : w0, hi = s0 + ej < w1 ? s0 + ej : w1;
-            const uint32_t off = sm.gq_off[q], skip = sm.gq_skip[q];
-            for (uint32_t k = lo + tid; k < hi; k += kBlock) {
-                const uint32_t o = k - s0;
-                sm.op[k - w0] = tv.list[off + o + (o >= skip ? 1u : 0u)];
-                sm.om[k - w0] = (typename EmitSmem<IPT, STAGE>::Om)j;
-            }
-        }
-        lds_barrier();
-        // copy-out: one coalesced stream per array
-        const uint32_t n = w1 - w0;
-        for (uint32_t k = tid; k < n; k += kBlock) {
-            const uint64_t out = (uint64_t)g0 + w0 + k;
-            if (out < p.capacity && !(DBG & 2)) {
-                p.peers[out] = sm.op[k];
-                if (p.msgs) p.msgs[out] = m0 + sm.om[k];
-            }
-        }
-        if (w1 < T) lds_barrier();  // the next window reuses the image
+        lds_barrier();  // the next window (or the caller's next row) reuses the image
     }
+}
+
+// Row-local exclusive scan of e over the block's 256 threads; returns this thread's start and
+// the row total.
+__device__ __forceinline__ uint32_t row_scan(uint32_t e, uint32_t* wave_tot, uint32_t* total) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t incl = wave_incl_scan_add(e, lane);
+    if (lane == 63) wave_tot[wave] = incl;
+    lds_barrier();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int u = 0; u < kWaves; ++u) {
+        const uint32_t t = wave_tot[u];
+        if (u < wave) before += t;
+        tot += t;
+    }
+    *total = tot;
+    return before + incl - e;
+}
+
+// Pass 3 of the three-launch tick: one 256-message row per block. CSR offsets = count-block
+// prefix (tile_scan) + the in-block prefix, then emit_row.
+template <int STAGE>
+__global__ __launch_bounds__(kBlock) void emit_kernel(EmitParams p) {
+    __shared__ EmitRowSmem<STAGE> sm;
+    __shared__ uint32_t wave_tot[kWaves];
+    __shared__ uint32_t part_tot[kWaves];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t m0 = blockIdx.x * kBlock;
+    const uint32_t m = m0 + tid;
+    const uint32_t e = m < p.M ? p.e[m] : 0u;
+    const uint2 inf = (p.peers && m < p.M) ? p.info[m] : make_uint2(0, kNone);
+    const uint32_t ct0 = (m0 / p.count_tile) * p.count_tile;
+    uint32_t g = p.tile_prefix[m0 / p.count_tile];
+    // earlier rows of the same count block
+    uint32_t part = 0;
+    for (uint32_t k = ct0 + tid; k < m0; k += kBlock) part += p.e[k];
+    part = (uint32_t)wave_sum_u64(part);
+    if (lane == 0) part_tot[wave] = part;
+    uint32_t T;
+    const uint32_t st = row_scan(e, wave_tot, &T);  // (its barrier also publishes part_tot)
+#pragma unroll
+    for (int u = 0; u < kWaves; ++u) g += part_tot[u];
+    if (m < p.M) p.offsets[m] = g + st;
+    if (!p.peers) return;  // counts-only call: offsets are all that is asked for
+    emit_row<STAGE>(sm, p.t, EmitOut{p.sender, p.peers, p.msgs, p.capacity}, m0, e, inf, st, g, T);
 }
 
 }  // namespace wq

@@ -14,6 +14,7 @@ constexpr int kScanWaves = kScanThreads / 64;
 
 struct TileScanParams {
     const uint32_t* tile_total;
+    const uint32_t* tile_F;
     uint32_t* tile_prefix;
     uint32_t n_tiles;
     uint32_t* offsets;  // offsets[M] = P
@@ -33,8 +34,12 @@ __device__ __forceinline__ uint64_t wave_incl_scan_add64(uint64_t v, int lane) {
 
 __global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScanParams p) {
     __shared__ uint64_t s_wave[kScanWaves];
+    __shared__ uint64_t s_F[kScanWaves];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint64_t carry = 0;
+    uint64_t carry = 0, F = 0;
+    for (uint32_t i = tid; i < p.n_tiles; i += kScanThreads) F += p.tile_F[i];
+    F = wave_sum_u64(F);
+    if (lane == 0) s_F[wave] = F;
     for (uint32_t b = 0; b < p.n_tiles; b += kScanThreads) {
         const uint32_t i = b + tid;
         const uint64_t x = i < p.n_tiles ? p.tile_total[i] : 0u;
@@ -53,6 +58,10 @@ __global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScanParams 
         __syncthreads();
     }
     if (tid == 0) {
+        uint64_t Ft = 0;
+#pragma unroll
+        for (int u = 0; u < kScanWaves; ++u) Ft += s_F[u];
+        p.cnt->n_candidates = Ft;
         const uint64_t P = carry;
         p.offsets[p.M] = (uint32_t)P;
         p.cnt->n_pairs = P;

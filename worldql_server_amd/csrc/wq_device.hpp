@@ -88,15 +88,16 @@ __host__ __device__ __forceinline__ uint32_t shard_of(uint32_t w, int64_t x, int
 //   pk = (world + 1) << 54 | (ax + 2^17) << 36 | (ay + 2^17) << 18 | (az + 2^17)   (pk != 0).
 // Every key a Vector3 can produce for coordinates within +-2^17 cubes of the origin is regular.
 // Regular cubes live in 128-byte records (one cache line: one fabric request per lookup):
-//   chunk 0 (bytes 0-15)  pk, peer count, offset of the cube's full list in `list`
-//   chunk 1 (16-31)       sig: 64-bit Bloom signature of the cube's peers (peer_sig), p0, p1
-//   chunks 2-7 (32-127)   p2 .. p25
-// so peer i sits in word 6 + i. The count pass reads chunks 0-1 only unless the signature says
+//   chunk 0 (bytes 0-15)   pk, peer count, offset of the cube's full list in `list`
+//   chunk 1 (16-31)        sig: 64-bit Bloom signature of the cube's peers (peer_sig), 8 B unused
+//   chunks 2-7 (32-127)    p0 .. p23, four per chunk
+// so peer i sits in word 8 + i: output quad q of a message without a skipped sender is chunk
+// 2 + q verbatim (route_emit.hpp). The count pass reads chunks 0-1 only unless the signature says
 // the sender may be subscribed (route_count.hpp).
 // Everything else (raw off-grid keys, NaN/inf/huge coordinates, world ids >= 1023) lives in the
 // 32-byte full-key Slot table. Both tables are exact; a key is in exactly one of them.
-constexpr int kInline = 26;
-constexpr int kInlineWord0 = 6;
+constexpr int kInline = 24;
+constexpr int kInlineWord0 = 8;
 constexpr uint32_t kAxisBias = 1u << 17;
 
 struct __attribute__((aligned(128))) Record {
@@ -104,6 +105,7 @@ struct __attribute__((aligned(128))) Record {
     uint32_t count;    // peers subscribed to the cube
     uint32_t list_off; // list[list_off] = count, list[list_off+1 ..] = ascending peers
     uint64_t sig;      // OR of peer_sig over the cube's peers
+    uint32_t unused[2];
     uint32_t peers[kInline];  // the first min(count, kInline) peers, ascending; rest 0xFFFFFFFF
 };
 // Two of the 64 signature bits per peer (one multiply): with ~10 peers per cube about 7% of

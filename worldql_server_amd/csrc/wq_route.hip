@@ -27,6 +27,7 @@
 #include "route_count.hpp"
 #include "route_emit.hpp"
 #include "route_scan.hpp"
+#include "route_tick.hpp"
 
 namespace wq {
 
@@ -35,43 +36,57 @@ namespace wq {
 // ------------------------------------------------------------------------------------------
 namespace {
 struct Cfg {
-    int count_ipt;
-    int emit_ipt;
+    int count_tile;  // messages per tile_total entry
     void (*count)(const CountParams&, hipStream_t, unsigned);
-    void (*emit)(const EmitParams&, hipStream_t, unsigned);
+    int emit_stage;  // emit window positions (4096 or 8192)
+    // single-launch tick (route_tick.hpp): messages per block, or 0 for none
+    int tick_rc;
+    void (*tick)(const TickParams&, hipStream_t, unsigned);
+    const void* tick_fn;  // for the occupancy query
 };
 
-template <int IPT, int MINW>
+template <int IPT, int MINW, int DBG = 0>
 void launch_count(const CountParams& p, hipStream_t s, unsigned grid) {
     if (p.in.keys)
-        hipLaunchKernelGGL((count_kernel<true, IPT, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL((count_kernel<true, IPT, MINW, DBG>), dim3(grid), dim3(kBlock), 0, s, p);
     else
-        hipLaunchKernelGGL((count_kernel<false, IPT, MINW>), dim3(grid), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL((count_kernel<false, IPT, MINW, DBG>), dim3(grid), dim3(kBlock), 0, s, p);
 }
 
-template <int IPT, int STAGE, int U, int DBG = 0>
-void launch_emit(const EmitParams& p, hipStream_t s, unsigned grid) {
-    hipLaunchKernelGGL((emit_kernel<IPT, STAGE, U, DBG>), dim3(grid), dim3(kBlock), 0, s, p);
+template <int RC>
+void launch_tick(const TickParams& p, hipStream_t s, unsigned grid) {
+    if (p.in.keys)
+        hipLaunchKernelGGL((tick_kernel<true, RC, 4096>), dim3(grid), dim3(kBlock), 0, s, p);
+    else
+        hipLaunchKernelGGL((tick_kernel<false, RC, 4096>), dim3(grid), dim3(kBlock), 0, s, p);
 }
 
-#define WQ_CFG(cipt, minw, eipt, stage, eu) \
-    {cipt, eipt, &launch_count<cipt, minw>, &launch_emit<eipt, stage, eu>}
-// count: (messages per lane, min waves per SIMD); emit: (messages per thread, window positions,
-// record lines per lane in flight)
+#define WQ_CFG3(cipt, minw, stage) {kBlock * cipt, &launch_count<cipt, minw>, stage, 0, nullptr, nullptr}
+#define WQ_CFG1(rc)                                                        \
+    {kBlock * 4, &launch_count<4, 2>, 4096, rc, &launch_tick<rc>,          \
+     reinterpret_cast<const void*>(&tick_kernel<false, rc, 4096>)}
+// Three launches: count (messages per lane, min waves per SIMD) / tile_scan / emit. One launch:
+// messages per block; its three-launch fallback (too many blocks to be resident) is count 4/2.
 const Cfg kCfgs[] = {
-    WQ_CFG(4, 2, 1, 4096, 8),  // 0: default
-    WQ_CFG(4, 2, 1, 3072, 8),  // 1
-    WQ_CFG(4, 2, 2, 6144, 8),  // 2
-    WQ_CFG(2, 4, 1, 4096, 8),  // 3
-    WQ_CFG(4, 2, 1, 2048, 8),  // 4
-    WQ_CFG(4, 2, 1, 4096, 4),  // 5
-    {4, 1, &launch_count<4, 2>, &launch_emit<1, 3072, 8, 1>},  // 6 timing only: no record loads
-    {4, 1, &launch_count<4, 2>, &launch_emit<1, 3072, 8, 2>},  // 7 timing only: no output stores
-    {4, 1, &launch_count<4, 2>, &launch_emit<1, 3072, 8, 4>},  // 8 timing only: no offset stores
-    {4, 1, &launch_count<4, 2>, &launch_emit<1, 3072, 8, 7>},  // 9 timing only: none
+    WQ_CFG3(1, 8, 4096),   // 0: default
+    WQ_CFG1(1024),         // 1: single launch
+    WQ_CFG3(1, 8, 8192),   // 2
+    WQ_CFG3(2, 4, 4096),   // 3
+    WQ_CFG3(1, 4, 4096),   // 4
+    WQ_CFG3(4, 2, 4096),   // 5
 };
-#undef WQ_CFG
+#undef WQ_CFG1
+#undef WQ_CFG3
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+
+// Blocks of `fn` the device keeps resident at once (0 if unknown).
+uint32_t resident_blocks(int device, const void* fn) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, 0) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+    per_cu = per_cu > 8 ? 8 : per_cu;
+    return (uint32_t)(per_cu * cus);
+}
 }  // namespace
 
 int route_config_count() { return kNumCfgs; }
@@ -100,14 +115,6 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         rw.calls++;
         return WQ_OK;
     }
-    const uint32_t count_tile = kBlock * cfg.count_ipt;
-    const uint32_t n_count = (uint32_t)((M + count_tile - 1) / count_tile);
-    WQ_ALLOC(h, rw.info, M * sizeof(uint2));
-    WQ_ALLOC(h, rw.e, M * 4);
-    WQ_ALLOC(h, rw.tiles, (uint64_t)n_count * 8);
-    uint32_t* tile_total = rw.tiles.as<uint32_t>();
-    uint32_t* tile_prefix = tile_total + n_count;
-
     const TableView tv = table_view(h);
     ProfileEvents& pr = h->prof;
     if (pr.enabled) {
@@ -120,13 +127,57 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         }
         WQ_HIP(h, hipEventRecord(pr.start[pr.used], s));
     }
+    const RouteIn in{d_pos, d_keys, d_world, d_sender, d_repl, (uint32_t)M, (int64_t)h->cube_size};
+
+    if (cfg.tick) {
+        const uint64_t nb = (M + cfg.tick_rc - 1) / cfg.tick_rc;
+        if (rw.resident_cfg != h->route_cfg) {
+            rw.resident = resident_blocks(h->device, cfg.tick_fn);
+            rw.resident_cfg = h->route_cfg;
+        }
+        if (nb <= rw.resident) {
+            WQ_ALLOC(h, rw.agg, 2 * nb * 8);
+            if (rw.agg_zeroed < 2 * nb) {  // fresh granules: tag 0 never matches a call's tag
+                WQ_HIP(h, hipMemsetAsync(rw.agg.p, 0, rw.agg.bytes, s));
+                rw.agg_zeroed = rw.agg.bytes / 8;
+            }
+            TickParams tp;
+            tp.in = in;
+            tp.t = tv;
+            tp.offsets = d_offsets;
+            tp.out = EmitOut{d_sender, capacity ? d_peers : nullptr, d_msgs, capacity};
+            tp.agg = rw.agg.as<uint64_t>();
+            tp.tag = (uint32_t)(rw.calls % 0xFFFFFFFFull) + 1u;
+            tp.cnt = cur;
+            tp.cnt_next = nxt;
+            tp.stamps = rw.stamps;
+            cfg.tick(tp, s, (unsigned)nb);
+            WQ_HIP(h, hipGetLastError());
+            if (pr.enabled) {
+                WQ_HIP(h, hipEventRecord(pr.stop[pr.used], s));
+                pr.used++;
+            }
+            rw.calls++;
+            return WQ_OK;
+        }
+    }
+
+    const uint32_t count_tile = cfg.count_tile;
+    const uint32_t n_count = (uint32_t)((M + count_tile - 1) / count_tile);
+    WQ_ALLOC(h, rw.info, M * sizeof(uint2));
+    WQ_ALLOC(h, rw.e, M * 4);
+    WQ_ALLOC(h, rw.tiles, (uint64_t)n_count * 12);
+    uint32_t* tile_total = rw.tiles.as<uint32_t>();
+    uint32_t* tile_prefix = tile_total + n_count;
+    uint32_t* tile_F = tile_prefix + n_count;
 
     CountParams cp;
-    cp.in = RouteIn{d_pos, d_keys, d_world, d_sender, d_repl, (uint32_t)M, (int64_t)h->cube_size};
+    cp.in = in;
     cp.t = tv;
     cp.e = rw.e.as<uint32_t>();
     cp.info = rw.info.as<uint2>();
     cp.tile_total = tile_total;
+    cp.tile_F = tile_F;
     cp.cnt = cur;
     cp.cnt_next = nxt;
     cfg.count(cp, s, n_count);
@@ -134,6 +185,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
 
     TileScanParams sp;
     sp.tile_total = tile_total;
+    sp.tile_F = tile_F;
     sp.tile_prefix = tile_prefix;
     sp.n_tiles = n_count;
     sp.offsets = d_offsets;
@@ -155,8 +207,11 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     ep.peers = capacity ? d_peers : nullptr;
     ep.msgs = d_msgs;
     ep.capacity = capacity;
-    const uint32_t emit_tile = kBlock * cfg.emit_ipt;
-    cfg.emit(ep, s, (unsigned)((M + emit_tile - 1) / emit_tile));
+    const dim3 eg((unsigned)((M + kBlock - 1) / kBlock));
+    if (cfg.emit_stage == 8192)
+        hipLaunchKernelGGL(emit_kernel<8192>, eg, dim3(kBlock), 0, s, ep);
+    else
+        hipLaunchKernelGGL(emit_kernel<4096>, eg, dim3(kBlock), 0, s, ep);
     WQ_HIP(h, hipGetLastError());
     if (pr.enabled) {
         WQ_HIP(h, hipEventRecord(pr.stop[pr.used], s));

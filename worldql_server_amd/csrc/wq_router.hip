@@ -128,9 +128,17 @@ int wq_get_stats(wq_router* h, wq_stats* out) {
     return WQ_OK;
 }
 
+int wq_debug_route_config_count(void) { return route_config_count(); }
+
 int wq_debug_set_route_config(wq_router* h, int cfg) {
     if (!h || cfg < 0 || cfg >= route_config_count()) return WQ_E_INVALID;
     h->route_cfg = cfg;
+    return WQ_OK;
+}
+
+int wq_debug_set_timeline(wq_router* h, uint64_t* d_stamps) {
+    if (!h) return WQ_E_INVALID;
+    h->rws.stamps = d_stamps;
     return WQ_OK;
 }
 

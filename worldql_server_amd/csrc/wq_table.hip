@@ -175,6 +175,7 @@ __global__ void k_insert_cubes(EvView st, const uint32_t* __restrict__ cube_star
         uint64_t sig = 0;
         for (uint32_t i = 0; i < cnt; ++i) sig |= peer_sig(st.p[j + i]);
         r.sig = sig;
+        r.unused[0] = r.unused[1] = 0xFFFFFFFFu;
 #pragma unroll 2
         for (int i = 0; i < kInline; ++i) r.peers[i] = (uint32_t)i < cnt ? st.p[j + i] : 0xFFFFFFFFu;
         return;

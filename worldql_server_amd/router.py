@@ -63,6 +63,8 @@ def load_library(build_if_missing: bool = True):
         "wq_profile_read": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)], i32),
         "wq_debug_set_hash_bits": ([vp, i32], i32),
         "wq_debug_set_route_config": ([vp, i32], i32),
+        "wq_debug_route_config_count": ([], i32),
+        "wq_debug_set_timeline": ([vp, vp], i32),
         "wq_shard_ops": ([vp, vp, sz, u32, vp], i32),
         "wq_shard_messages_device": ([vp, vp, vp, vp, vp, vp, sz, u32, vp, vp], i32),
         "wq_route_records_device": ([vp, vp, sz, vp, vp, vp, sz, vp], i32),
@@ -222,6 +224,9 @@ class Router:
         out = np.zeros(max(n.value, 1), dtype=np.uint32)
         self._check(self.lib.wq_world_peers(self.h, world, _p(out), n.value, ctypes.byref(n)))
         return out[: n.value]
+
+    def route_config_count(self) -> int:
+        return int(self.lib.wq_debug_route_config_count())
 
     def set_route_config(self, cfg: int) -> None:
         self._check(self.lib.wq_debug_set_route_config(self.h, cfg))
