@@ -37,7 +37,7 @@ def main():
         print(k)
         for c, v in sorted(means.items()):
             print(f"    {c:28s} {v:16.1f}   (n={len(cs[c])})")
-        if any(s in k for s in ("count_kernel", "count_lpm_kernel", "tile_scan_kernel", "emit_kernel")):
+        if any(s in k for s in ("count_kernel", "tile_scan_kernel", "emit_kernel", "tick_kernel")):
             route[k] = means
     if a.json and route:
         # gfx950: FETCH_SIZE tallies 128-B line requests as 64 B (MI355X_MICROARCH.md §HBM) -> x2

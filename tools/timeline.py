@@ -23,6 +23,7 @@ def main():
     w = synth.config_c2(scale=a.scale)
     M = len(w.world)
     r = Router(16, 0)
+    r.set_stream(torch.cuda.current_stream(dev).cuda_stream)  # stamps are zeroed on this stream
     r.set_route_config(a.cfg)
     r.apply_ops(w.ops)
     pos = torch.from_numpy(w.pos).to(dev)
@@ -65,7 +66,7 @@ def main():
     print("count phase by block octile:", " ".join(f"{cnt[i].mean():5.1f}" for i in q))
     print("start by block octile:", " ".join(f"{st[i].mean():5.1f}" for i in q))
     if a.dump:
-        np.save(a.dump, np.stack(raw))
+        np.save(a.dump, raw[-1])
 
 
 if __name__ == "__main__":

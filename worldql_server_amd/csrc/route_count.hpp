@@ -54,10 +54,12 @@ constexpr uint32_t kStDone = 0, kStProbe = 1, kStVerify = 2;
 
 // Messages m0 + i*kBlock + threadIdx.x, i < IPT: filtered count and locator of each (zero for
 // m >= in.M), with F (candidates) and E (recipients) accumulated into the caller's sums.
-template <bool RAW_KEYS, int IPT, int DBG = 0>
+// FULL: the whole record line is read in the first round (the sender filter then needs no extra
+// round) and its peer chunks 2-7 are handed back in peers_out (FULL only; valid for inline records).
+template <bool RAW_KEYS, int IPT, int DBG = 0, bool FULL = false>
 __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& tv, uint32_t m0,
                                            uint32_t (&e_out)[IPT], uint2 (&inf_out)[IPT], uint64_t& F_local,
-                                           uint32_t& E_local) {
+                                           uint32_t& E_local, uint4 (*peers_out)[6] = nullptr) {
     const int tid = threadIdx.x;
 
     // ---- A: inputs (all loads first), quantise (kernel 1), packed key, home slot ----
@@ -127,10 +129,14 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
     // ---- B: rounds of two 16-byte loads per pending message ----
     const uint4* recs4 = reinterpret_cast<const uint4*>(tv.recs);
     uint4 c0[IPT], c1[IPT];
+    uint4 pc[IPT][FULL ? 6 : 1];  // FULL: the inline peers (chunks 2-7) ride along in the first round
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
         c0[i] = recs4[(uint64_t)sl[i] * 8];
         c1[i] = (DBG & 1) ? c0[i] : recs4[(uint64_t)sl[i] * 8 + 1];
+        if (FULL)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) pc[i][q] = recs4[(uint64_t)sl[i] * 8 + 2 + q];
     }
     uint32_t cnt[IPT], loff[IPT], lt[IPT], vc[IPT];
     bool has[IPT];
@@ -157,7 +163,20 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
                         const uint64_t sig = ((uint64_t)c1[i].y << 32) | c1[i].x;
                         const uint64_t bits = peer_sig(me);
                         if (!(DBG & 3) && (sig & bits) == bits) {  // maybe subscribed: verify
-                            if (cnt[i] <= (uint32_t)kInline) {  // inline peers from chunk 2 on
+                            if (FULL && cnt[i] <= (uint32_t)kInline) {  // peers already in registers
+                                uint32_t l = 0;
+                                bool h = false;
+#pragma unroll
+                                for (int q = 0; q < kInline; ++q) {
+                                    const uint4 c = pc[i][q / 4];
+                                    const uint32_t w = (q & 3) == 0 ? c.x : (q & 3) == 1 ? c.y : (q & 3) == 2 ? c.z : c.w;
+                                    const bool in = (uint32_t)q < cnt[i];
+                                    l += (in & (w < me)) ? 1u : 0u;
+                                    h |= in & (w == me);
+                                }
+                                lt[i] = l;
+                                has[i] = h;
+                            } else if (cnt[i] <= (uint32_t)kInline) {  // inline peers from chunk 2 on
                                 st[i] = kStVerify;
                                 vc[i] = 2;
                             } else {  // > kInline peers: binary search of the full list (rare in C2)
@@ -195,6 +214,9 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
             const uint32_t q = st[i] == kStProbe ? 0u : vc[i];  // vc <= 6: chunks q, q+1 <= 7
             c0[i] = recs4[(uint64_t)sl[i] * 8 + q];
             c1[i] = recs4[(uint64_t)sl[i] * 8 + q + 1];
+            if (FULL && st[i] == kStProbe)
+#pragma unroll
+                for (int c = 0; c < 6; ++c) pc[i][c] = recs4[(uint64_t)sl[i] * 8 + 2 + c];
         }
     }
 
@@ -206,10 +228,13 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
             F_local += cnt[i];
             E_local += e_out[i];
         }
+        if (FULL && peers_out)
+#pragma unroll
+            for (int c = 0; c < 6; ++c) peers_out[i][c] = pc[i][c];
     }
 }
 
-template <bool RAW_KEYS, int IPT, int MINW, int DBG = 0>
+template <bool RAW_KEYS, int IPT, int MINW, int DBG = 0, bool FULL = false>
 __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
     __shared__ uint64_t wave_F[kWaves];
     __shared__ uint64_t wave_E[kWaves];
@@ -225,7 +250,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
     uint32_t E_local = 0;
     uint32_t e_out[IPT];
     uint2 inf_out[IPT];
-    count_rows<RAW_KEYS, IPT, DBG>(p.in, p.t, m0, e_out, inf_out, F_local, E_local);
+    count_rows<RAW_KEYS, IPT, DBG, FULL>(p.in, p.t, m0, e_out, inf_out, F_local, E_local);
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
         const uint32_t m = m0 + i * kBlock + tid;

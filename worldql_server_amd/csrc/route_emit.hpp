@@ -53,7 +53,7 @@ struct EmitOut {
 //   longer lists: the block copies the window's slice of each from `list`;
 //   OnlySelf: the sender, by its own lane.
 // Every thread of the block must call it (it contains barriers); it ends with a barrier.
-template <int STAGE>
+template <int STAGE, int U = 8>
 __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView& tv, const EmitOut& o, uint32_t m0,
                                          uint32_t e, uint2 inf, uint32_t st, uint64_t g0, uint32_t T) {
     static_assert(STAGE % 1024 == 0, "STAGE: whole quads for every lane");
@@ -78,21 +78,10 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
             skip = s24 == kSkipNone24 ? kNone : s24;
         }
     }
-    // record chunks of the wave's 64 messages: message q by lanes 8*(q%8) .. +7, round q/8
+    // record chunks of the wave's 64 messages: message q by lanes 8*(q%8) .. +7, round q/8,
+    // U rounds of loads in flight at a time
     const int grp = lane >> 3, part = lane & 7;
     const uint4* recs4 = reinterpret_cast<const uint4*>(tv.recs);
-    uint4 v[8];
-    uint32_t q_cnt[8], q_skip[8], q_st[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-        const int src = 8 * u + grp;
-        const uint32_t qs = __shfl(sl, src, 64);
-        q_cnt[u] = __shfl(cnt, src, 64);
-        q_skip[u] = __shfl(skip, src, 64);
-        q_st[u] = __shfl(st, src, 64);
-        if (part < 6 && qs != kNone && 4u * part < q_cnt[u]) v[u] = recs4[(uint64_t)qs * 8 + 2 + part];
-        else q_cnt[u] = 0;  // nothing to stage from this lane
-    }
     lds_barrier();
     const uint32_t n_gq = sm.n_gq;
     // window w covers global outputs [gA + w0, gA + w0 + STAGE), gA = g0 rounded down to a quad
@@ -105,19 +94,34 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
             sm.op[lead + st - w0] = self_peer;
             sm.om[lead + st - w0] = (uint8_t)tid;
         }
+#pragma unroll 1
+        for (int r0 = 0; r0 < 8; r0 += U) {
+            uint4 v[U];
+            uint32_t q_cnt[U], q_skip[U], q_st[U];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            if (!q_cnt[u]) continue;
-            const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-            const uint8_t j = (uint8_t)(wave * 64 + 8 * u + grp);
+            for (int u = 0; u < U; ++u) {
+                const int src = 8 * (r0 + u) + grp;
+                const uint32_t qs = __shfl(sl, src, 64);
+                q_cnt[u] = __shfl(cnt, src, 64);
+                q_skip[u] = __shfl(skip, src, 64);
+                q_st[u] = __shfl(st, src, 64);
+                if (part < 6 && qs != kNone && 4u * part < q_cnt[u]) v[u] = recs4[(uint64_t)qs * 8 + 2 + part];
+                else q_cnt[u] = 0;  // nothing to stage from this lane
+            }
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint32_t idx = 4u * part + i;  // peer index in the cube's list
-                if (idx >= q_cnt[u] || idx == q_skip[u]) continue;
-                const uint32_t pos = lead + q_st[u] + idx - (idx > q_skip[u] && q_skip[u] != kNone ? 1u : 0u);
-                if (pos >= w0 && pos < w1) {
-                    sm.op[pos - w0] = vv[i];
-                    sm.om[pos - w0] = j;
+            for (int u = 0; u < U; ++u) {
+                if (!q_cnt[u]) continue;
+                const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                const uint8_t j = (uint8_t)(wave * 64 + 8 * (r0 + u) + grp);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t idx = 4u * part + i;  // peer index in the cube's list
+                    if (idx >= q_cnt[u] || idx == q_skip[u]) continue;
+                    const uint32_t pos = lead + q_st[u] + idx - (idx > q_skip[u] && q_skip[u] != kNone ? 1u : 0u);
+                    if (pos >= w0 && pos < w1) {
+                        sm.op[pos - w0] = vv[i];
+                        sm.om[pos - w0] = j;
+                    }
                 }
             }
         }
@@ -176,7 +180,7 @@ __device__ __forceinline__ uint32_t row_scan(uint32_t e, uint32_t* wave_tot, uin
 
 // Pass 3 of the three-launch tick: one 256-message row per block. CSR offsets = count-block
 // prefix (tile_scan) + the in-block prefix, then emit_row.
-template <int STAGE>
+template <int STAGE, int U>
 __global__ __launch_bounds__(kBlock) void emit_kernel(EmitParams p) {
     __shared__ EmitRowSmem<STAGE> sm;
     __shared__ uint32_t wave_tot[kWaves];
@@ -199,7 +203,7 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(EmitParams p) {
     for (int u = 0; u < kWaves; ++u) g += part_tot[u];
     if (m < p.M) p.offsets[m] = g + st;
     if (!p.peers) return;  // counts-only call: offsets are all that is asked for
-    emit_row<STAGE>(sm, p.t, EmitOut{p.sender, p.peers, p.msgs, p.capacity}, m0, e, inf, st, g, T);
+    emit_row<STAGE, U>(sm, p.t, EmitOut{p.sender, p.peers, p.msgs, p.capacity}, m0, e, inf, st, g, T);
 }
 
 }  // namespace wq

@@ -1,20 +1,25 @@
-// route_tick.hpp — the whole tick in ONE launch (see wq_route.hip).
+// route_tick.hpp — the whole tick in ONE launch and ONE pass over the record lines.
 //
-// Block b owns messages [b*RC, (b+1)*RC). It
-//   1. counts them (count_rows: quantise, probe, sender filter), keeping e_m and the locators in
-//      LDS — nothing of the count pass goes through HBM;
-//   2. publishes its total as one tagged 8-byte granule {tag, total} (a relaxed agent-scope
-//      store: the value is the whole hand-off, so it needs no fence);
-//   3. sums the totals of blocks 0..b-1, polling each granule until it carries this call's tag
-//      (relaxed agent-scope loads, which bypass the non-coherent L1; bounded, see below);
-//   4. emits its rows (emit_row) at that global offset.
-// A block waits only on LOWER-numbered blocks, which were dispatched before it: they are resident
-// or finished, so the chain always drains (the launcher also sizes the grid to the resident
-// capacity). Every poll is bounded: a block that gives up sets counters.error bit 2 and emits at a
-// wrong offset instead of hanging the GPU.
-// Compared with count / tile_scan / emit launches this removes the e / locator round trip through
-// HBM (12 B per message), the scan launch and one launch gap; the tick's only inter-block
-// traffic is one 8-byte granule per block (C2: 977 blocks).
+// The three-launch tick (count / tile_scan / emit) reads every message's record line twice; at
+// ~50 G random lines/s that second pass alone costs ~20 us of a C2 tick. Here block b owns the
+// 256 messages [256b, 256b + 256) and
+//   1. counts them, one lane per message (count_rows: quantise, probe, sender filter);
+//   2. scans e over the block (row-local output positions) and publishes its total as a tagged
+//      8-byte granule {tag, A, total} — decoupled look-back, Merrill & Garland;
+//   3. stages its outputs in LDS in output order while that granule propagates: the count read
+//      each message's whole record line in one round (lane per message), so the lane already
+//      holds the peers and writes each quad of them with one 16-byte and one 4-byte LDS store
+//      (the four peers and their message index); the sender's skipped entry, long lists (the
+//      block copies them from `list`) and OnlySelf take slower paths;
+//   4. looks back over the lower blocks' granules, 64 per wave instruction, summing aggregates
+//      until the nearest inclusive prefix, and publishes its own inclusive prefix {tag, P, ...};
+//   5. writes CSR offsets and copies the image out in 16-byte quads aligned to the global
+//      output (the block's first and last quads, shared with its neighbours, word by word).
+// A block waits only on LOWER-numbered blocks, dispatched before it and therefore resident or
+// finished, so the chain always drains. Every poll is bounded: a block that gives up sets
+// counters.error bit 2 and writes at a wrong offset instead of hanging the GPU.
+// A block whose outputs exceed the LDS image (skewed fan-out) emits through emit_row, which
+// re-reads its records window by window — exact either way.
 #pragma once
 #include "route_count.hpp"
 #include "route_emit.hpp"
@@ -26,8 +31,9 @@ struct TickParams {
     TableView t;
     uint32_t* offsets;  // out: CSR offsets[0 .. M]
     EmitOut out;        // peers == nullptr: offsets only
-    uint64_t* agg;      // [2 * gridDim.x] tagged block totals, then tagged block candidate counts
-    uint32_t tag;       // this call's tag (non-zero, differs from the previous call's)
+    uint64_t* look;     // [gridDim.x] look-back granules
+    uint64_t* fgran;    // [gridDim.x] tagged per-block candidate counts (summed by the last block)
+    uint32_t tag;       // this call's tag, 1 .. 2^30-1, differs from the previous call's
     wq_route_counters* cnt;
     wq_route_counters* cnt_next;
     uint64_t* stamps;   // diagnostics (wq_debug_set_timeline) or nullptr
@@ -35,37 +41,63 @@ struct TickParams {
 
 constexpr uint32_t kErrSpin = 4u;
 constexpr uint32_t kSpinLimit = 1u << 21;  // x s_sleep(2) ~ 0.1 s, far beyond any tick
+constexpr uint32_t kFlagA = 1u, kFlagP = 2u;
 
-__device__ __forceinline__ uint32_t wait_granule(const uint64_t* g, uint32_t tag, bool* gave_up) {
+// granule: [tag:30][flag:2][value:32]
+__device__ __forceinline__ uint64_t granule(uint32_t tag, uint32_t flag, uint32_t v) {
+    return ((uint64_t)((tag << 2) | flag) << 32) | v;
+}
+
+__device__ __forceinline__ uint64_t poll_granule(const uint64_t* g, uint32_t tag, bool* gave_up) {
     for (uint32_t it = 0;; ++it) {
         const uint64_t v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)(v >> 32) == tag) return (uint32_t)v;
+        if ((uint32_t)(v >> 34) == tag) return v;
         if (it >= kSpinLimit) {
             *gave_up = true;
-            return 0u;
+            return granule(tag, kFlagP, 0);
         }
         __builtin_amdgcn_s_sleep(2);
     }
 }
 
-template <int RC>
+// Exclusive prefix of block b's total over blocks 0 .. b-1 (called by one whole wave; b > 0).
+__device__ __forceinline__ uint64_t look_back(const uint64_t* look, uint32_t b, uint32_t tag, bool* gave_up) {
+    const int lane = threadIdx.x & 63;
+    uint64_t acc = 0;
+    for (int64_t hi = (int64_t)b - 1; hi >= 0; hi -= 64) {
+        const int64_t idx = hi - lane;  // lane 0 = the nearest block
+        uint64_t v = 0;
+        if (idx >= 0) v = poll_granule(look + idx, tag, gave_up);
+        const uint32_t flag = (uint32_t)(v >> 32) & 3u;
+        const uint64_t pm = __ballot(idx >= 0 && flag == kFlagP);
+        const int first = pm ? __builtin_ctzll(pm) : 64;  // nearest inclusive prefix
+        const uint64_t x = (lane <= first && idx >= 0) ? (uint32_t)v : 0u;
+        acc += wave_sum_u64(x);
+        if (pm) break;
+    }
+    return acc;
+}
+
+template <int STAGE>
 struct TickSmem {
-    uint32_t e[RC];
-    uint2 info[RC];
-    uint64_t wave_u64[2][kWaves];
+    EmitRowSmem<STAGE> es;  // image (op / om) + long-list queue; also the fallback's LDS
     uint32_t wave_tot[kWaves];
+    uint64_t wave_u64[kWaves];
+    uint64_t pre;
 };
 
-template <bool RAW_KEYS, int RC, int STAGE>
+typedef uint32_t u32x4_lds __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32_a1 __attribute__((aligned(1)));
+
+template <bool RAW_KEYS, int STAGE, int U>
 __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
-    constexpr int ROWS = RC / kBlock;
-    constexpr int G = ROWS < 4 ? ROWS : 4;  // rows counted together (messages per lane)
-    static_assert(RC % (G * kBlock) == 0, "RC: whole groups of rows");
-    __shared__ TickSmem<RC> sm;
-    __shared__ EmitRowSmem<STAGE> es;
+    // U: record lines in flight per lane in the fallback emit_row
+    static_assert(STAGE % 1024 == 0, "STAGE: whole quads for every lane");
+    __shared__ TickSmem<STAGE> sm;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t b = blockIdx.x;
-    const uint32_t base = b * RC;
+    const TableView& tv = p.t;
+    const uint32_t b = blockIdx.x, NB = gridDim.x;
+    const uint32_t m0 = b * kBlock, m = m0 + tid;
     const bool stamp = p.stamps && tid == 0;
     if (stamp) p.stamps[4 * b] = __builtin_amdgcn_s_memrealtime();
     if (b == 0 && tid == 0) {
@@ -74,94 +106,160 @@ __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
         p.cnt_next->overflow = 0;
         p.cnt_next->error = 0;
     }
+    if (tid == 0) sm.es.n_gq = 0;
 
-    // ---- 1. count, G rows at a time ----
+    // ---- 1. count ----
     uint64_t F_local = 0;
     uint32_t E_local = 0;
-#pragma unroll 1
-    for (int r0 = 0; r0 < ROWS; r0 += G) {
-        uint32_t e_out[G];
-        uint2 inf_out[G];
-        count_rows<RAW_KEYS, G>(p.in, p.t, base + r0 * kBlock, e_out, inf_out, F_local, E_local);
+    uint32_t e1[1];
+    uint2 inf1[1];
+    uint4 pc[1][6];  // the message's peer chunks (inline records): staged from registers below
+    count_rows<RAW_KEYS, 1, 0, true>(p.in, tv, m0, e1, inf1, F_local, E_local, pc);
+    const uint32_t e = e1[0];
+    const uint2 inf = inf1[0];
+
+    // ---- 2. row scan, publish the aggregate ----
+    const uint64_t Fw = wave_sum_u64(F_local);
+    if (lane == 0) sm.wave_u64[wave] = Fw;
+    uint32_t T;
+    const uint32_t st = row_scan(e, sm.wave_tot, &T);
+    if (tid == 0) {
+        uint64_t Fb = 0;
 #pragma unroll
-        for (int i = 0; i < G; ++i) {
-            sm.e[(r0 + i) * kBlock + tid] = e_out[i];
-            sm.info[(r0 + i) * kBlock + tid] = inf_out[i];
+        for (int u = 0; u < kWaves; ++u) Fb += sm.wave_u64[u];
+        __hip_atomic_store(p.fgran + b, granule(p.tag, kFlagA, Fb > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Fb),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p.look + b, granule(p.tag, b == 0 ? kFlagP : kFlagA, T), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (stamp) p.stamps[4 * b + 1] = __builtin_amdgcn_s_memrealtime();
+
+    // ---- 3. stage the block's outputs in LDS (if they fit) ----
+    const bool fits = T <= (uint32_t)STAGE && p.out.peers;  // block-uniform
+    const bool self = e && (inf.x & kLocSelf);
+    if (fits) {
+        uint32_t slot = kNone, meta = 0;
+        if (e && !self) {
+            if (inf.x & kLocGlobal) {
+                const uint32_t q = atomicAdd(&sm.es.n_gq, 1u);
+                sm.es.gq_j[q] = tid;
+                sm.es.gq_off[q] = (inf.x & ~kLocGlobal) + 1;
+                sm.es.gq_skip[q] = inf.y;
+                sm.es.gq_e[q] = e;
+                sm.es.gq_st[q] = st;
+            } else {
+                const uint32_t s24 = inf.y & kSkipNone24;
+                slot = inf.x;
+                meta = (inf.y >> 24) | ((s24 == kSkipNone24 ? 0xFFu : s24) << 8);
+            }
+        }
+        if (self) {
+            sm.es.op[st] = p.out.sender[m];
+            sm.es.om[st] = (uint8_t)tid;
+        }
+        if (slot != kNone) {  // inline record: the peers are in this lane's registers
+            const uint32_t cnt = meta & 0xFF, skip = meta >> 8;
+            const uint8_t j = (uint8_t)tid;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const uint32_t i0 = 4u * k;  // first peer index of chunk 2 + k
+                if (i0 >= cnt) continue;
+                const uint4 c = pc[0][k];
+                if (i0 + 4 <= cnt && (skip == 0xFFu || skip < i0)) {
+                    // four peers, none of them the sender: one quad
+                    const uint32_t pos = st + i0 - (skip != 0xFFu ? 1u : 0u);
+                    *reinterpret_cast<u32x4_lds*>(&sm.es.op[pos]) = u32x4_lds{c.x, c.y, c.z, c.w};
+                    *reinterpret_cast<u32_a1*>(&sm.es.om[pos]) = 0x01010101u * j;
+                } else {
+                    const uint32_t vv[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint32_t idx = i0 + i;
+                        if (idx >= cnt || idx == skip) continue;
+                        const uint32_t pos = st + idx - (skip != 0xFFu && idx > skip ? 1u : 0u);
+                        sm.es.op[pos] = vv[i];
+                        sm.es.om[pos] = j;
+                    }
+                }
+            }
+        }
+        lds_barrier();  // the long-list queue is complete
+        const uint32_t n_gq = sm.es.n_gq;
+        for (uint32_t q = 0; q < n_gq; ++q) {
+            const uint32_t j = sm.es.gq_j[q], s0 = sm.es.gq_st[q], ej = sm.es.gq_e[q];
+            const uint32_t off = sm.es.gq_off[q], sk = sm.es.gq_skip[q];
+            for (uint32_t k = tid; k < ej; k += kBlock) {
+                sm.es.op[s0 + k] = tv.list[off + k + (k >= sk ? 1u : 0u)];
+                sm.es.om[s0 + k] = (uint8_t)j;
+            }
         }
     }
-    const uint64_t Fw = wave_sum_u64(F_local);
-    const uint64_t Ew = wave_sum_u64(E_local);
-    if (lane == 0) {
-        sm.wave_u64[0][wave] = Fw;
-        sm.wave_u64[1][wave] = Ew;
-    }
-    lds_barrier();
-    uint64_t Fb = 0, Eb = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-        Fb += sm.wave_u64[0][w];
-        Eb += sm.wave_u64[1][w];
-    }
-    bool gave_up = false;
-    if (stamp) p.stamps[4 * b + 1] = __builtin_amdgcn_s_memrealtime();
-    // ---- 2. publish ----
-    if (tid == 0) {
-        if (Eb > 0xFFFFFFFFull) atomicOr(&p.cnt->error, 2u);  // a block total past u32: offsets cannot hold it
-        const uint64_t g = ((uint64_t)p.tag << 32) | (Eb & 0xFFFFFFFFull);
-        __hip_atomic_store(p.agg + b, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t f = ((uint64_t)p.tag << 32) | (Fb > 0xFFFFFFFFull ? 0xFFFFFFFFull : Fb);
-        __hip_atomic_store(p.agg + gridDim.x + b, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // ---- 3. prefix over lower blocks ----
-    // (the last block also sums every block's candidate count for the counters)
-    const bool last = b == gridDim.x - 1;
-    uint64_t pre = 0, Fall = 0;
-    for (uint32_t k = tid; k < b; k += kBlock) pre += wait_granule(p.agg + k, p.tag, &gave_up);
-    if (last)
-        for (uint32_t k = tid; k < gridDim.x; k += kBlock) Fall += wait_granule(p.agg + gridDim.x + k, p.tag, &gave_up);
-    pre = wave_sum_u64(pre);
-    Fall = wave_sum_u64(Fall);
-    lds_barrier();  // wave_u64 reuse
-    if (lane == 0) {
-        sm.wave_u64[0][wave] = pre;
-        sm.wave_u64[1][wave] = Fall;
-    }
-    const bool any_gave_up = __syncthreads_or(gave_up);
-    pre = 0;
-    Fall = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-        pre += sm.wave_u64[0][w];
-        Fall += sm.wave_u64[1][w];
-    }
-    if (tid == 0) {
-        if (any_gave_up) atomicOr(&p.cnt->error, kErrSpin);
-        if (last) {  // the last block knows P and F
-            const uint64_t P = pre + Eb;
-            p.cnt->n_candidates = Fall;
+
+    // ---- 4. look-back (wave 0), publish the inclusive prefix ----
+    if (wave == 0) {
+        bool gave_up = false;
+        uint64_t pre = 0;
+        if (b > 0) {
+            pre = look_back(p.look, b, p.tag, &gave_up);
+            if (lane == 0) {
+                __hip_atomic_store(p.look + b, granule(p.tag, kFlagP, (uint32_t)(pre + T)), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (b == NB - 1 && lane == 0) {  // the last block knows P
+            const uint64_t P = pre + T;
             p.offsets[p.in.M] = (uint32_t)P;
             p.cnt->n_pairs = P;
             if (P > p.out.capacity) atomicOr(&p.cnt->overflow, 1u);
             if (P > 0xFFFFFFFFull) atomicOr(&p.cnt->error, 2u);  // u32 CSR offsets cannot hold it
         }
+        if (__any(gave_up) && lane == 0) atomicOr(&p.cnt->error, kErrSpin);
+        if (lane == 0) sm.pre = pre;
     }
-
+    if (b == NB - 1) {  // ... and sums every block's candidate count, all four waves polling
+        bool gave_up = false;
+        uint64_t F = 0;
+        for (uint32_t k = tid; k < NB; k += kBlock) F += (uint32_t)poll_granule(p.fgran + k, p.tag, &gave_up);
+        F = wave_sum_u64(F);
+        if (lane == 0) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(&p.cnt->n_candidates), (unsigned long long)F);
+            if (__any(gave_up)) atomicOr(&p.cnt->error, kErrSpin);
+        }
+    }
+    lds_barrier();
+    const uint64_t g0 = sm.pre;
     if (stamp) p.stamps[4 * b + 2] = __builtin_amdgcn_s_memrealtime();
-    // ---- 4. offsets and emit, one row of 256 messages at a time ----
-    uint64_t g = pre;
-#pragma unroll 1
-    for (int r = 0; r < ROWS; ++r) {
-        const uint32_t m0 = base + r * kBlock;
-        if (m0 >= p.in.M) break;  // block-uniform
-        const uint32_t m = m0 + tid;
-        const uint32_t e = sm.e[r * kBlock + tid];
-        const uint2 inf = sm.info[r * kBlock + tid];
-        uint32_t T;
-        const uint32_t st = row_scan(e, sm.wave_tot, &T);
-        if (m < p.in.M) p.offsets[m] = (uint32_t)(g + st);
-        if (p.out.peers) emit_row<STAGE>(es, p.t, p.out, m0, e, inf, st, g, T);
-        else lds_barrier();  // wave_tot reuse
-        g += T;
+
+    // ---- 5. offsets, copy-out ----
+    if (m < p.in.M) p.offsets[m] = (uint32_t)(g0 + st);
+    if (p.out.peers) {
+        if (fits) {
+            const uint64_t gA = g0 & ~3ull;
+            const uint32_t lead = (uint32_t)(g0 - gA);
+            const uint32_t span = lead + T;
+            for (uint32_t qd = 4u * tid; qd < span; qd += 4u * kBlock) {
+                // image index of global output gA + qd + i is qd + i - lead
+                const uint64_t out0 = gA + qd;
+                if (qd >= lead && qd + 4 <= span && out0 + 4 <= p.out.capacity) {
+                    const u32x4_lds pv = *reinterpret_cast<const u32x4_lds*>(&sm.es.op[qd - lead]);
+                    const uint32_t mv = *reinterpret_cast<const u32_a1*>(&sm.es.om[qd - lead]);
+                    *reinterpret_cast<uint4*>(p.out.peers + out0) = make_uint4(pv.x, pv.y, pv.z, pv.w);
+                    if (p.out.msgs)
+                        *reinterpret_cast<uint4*>(p.out.msgs + out0) = make_uint4(
+                            m0 + (mv & 0xFF), m0 + ((mv >> 8) & 0xFF), m0 + ((mv >> 16) & 0xFF), m0 + (mv >> 24));
+                } else {
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) {
+                        if (qd + i >= lead && qd + i < span && out0 + i < p.out.capacity) {
+                            p.out.peers[out0 + i] = sm.es.op[qd + i - lead];
+                            if (p.out.msgs) p.out.msgs[out0 + i] = m0 + sm.es.om[qd + i - lead];
+                        }
+                    }
+                }
+            }
+        } else {
+            emit_row<STAGE, U>(sm.es, tv, p.out, m0, e, inf, st, g0, T);
+        }
     }
     if (stamp) p.stamps[4 * b + 3] = __builtin_amdgcn_s_memrealtime();
 }

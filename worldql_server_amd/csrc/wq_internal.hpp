@@ -67,10 +67,8 @@ struct RouteWs {
     DevBuf info;   // uint2[M]: locators, count pass -> emit pass
     DevBuf e;      // u32[M]: filtered counts
     DevBuf tiles;  // u32[2 * n_count_blocks]: block totals, then their exclusive prefix
-    DevBuf agg;    // u64[blocks]: tagged block totals of the single-launch tick
+    DevBuf agg;    // u64[2 * blocks]: look-back and candidate granules of the single-launch tick
     uint64_t agg_zeroed = 0;
-    uint32_t resident = 0;  // resident blocks of the configured single-launch tick kernel
-    int resident_cfg = -1;
     uint64_t* stamps = nullptr;  // wq_debug_set_timeline
     uint64_t calls = 0;
     wq_route_counters* last = nullptr;  // counters of the most recent call (device)

@@ -39,54 +39,43 @@ struct Cfg {
     int count_tile;  // messages per tile_total entry
     void (*count)(const CountParams&, hipStream_t, unsigned);
     int emit_stage;  // emit window positions (4096 or 8192)
-    // single-launch tick (route_tick.hpp): messages per block, or 0 for none
-    int tick_rc;
+    // single-launch tick (route_tick.hpp): its LDS image positions, or 0 for three launches
+    int tick_stage;
     void (*tick)(const TickParams&, hipStream_t, unsigned);
-    const void* tick_fn;  // for the occupancy query
+    const void* unused;
 };
 
-template <int IPT, int MINW, int DBG = 0>
+template <int IPT, int MINW, bool FULL = false>
 void launch_count(const CountParams& p, hipStream_t s, unsigned grid) {
     if (p.in.keys)
-        hipLaunchKernelGGL((count_kernel<true, IPT, MINW, DBG>), dim3(grid), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL((count_kernel<true, IPT, MINW, 0, FULL>), dim3(grid), dim3(kBlock), 0, s, p);
     else
-        hipLaunchKernelGGL((count_kernel<false, IPT, MINW, DBG>), dim3(grid), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL((count_kernel<false, IPT, MINW, 0, FULL>), dim3(grid), dim3(kBlock), 0, s, p);
 }
 
-template <int RC>
+template <int STAGE, int U>
 void launch_tick(const TickParams& p, hipStream_t s, unsigned grid) {
     if (p.in.keys)
-        hipLaunchKernelGGL((tick_kernel<true, RC, 4096>), dim3(grid), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL((tick_kernel<true, STAGE, U>), dim3(grid), dim3(kBlock), 0, s, p);
     else
-        hipLaunchKernelGGL((tick_kernel<false, RC, 4096>), dim3(grid), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL((tick_kernel<false, STAGE, U>), dim3(grid), dim3(kBlock), 0, s, p);
 }
 
 #define WQ_CFG3(cipt, minw, stage) {kBlock * cipt, &launch_count<cipt, minw>, stage, 0, nullptr, nullptr}
-#define WQ_CFG1(rc)                                                        \
-    {kBlock * 4, &launch_count<4, 2>, 4096, rc, &launch_tick<rc>,          \
-     reinterpret_cast<const void*>(&tick_kernel<false, rc, 4096>)}
+#define WQ_CFG1(stage, u) {kBlock, &launch_count<1, 8>, 4096, stage, &launch_tick<stage, u>, nullptr}
 // Three launches: count (messages per lane, min waves per SIMD) / tile_scan / emit. One launch:
 // messages per block; its three-launch fallback (too many blocks to be resident) is count 4/2.
 const Cfg kCfgs[] = {
-    WQ_CFG3(1, 8, 4096),   // 0: default
-    WQ_CFG1(1024),         // 1: single launch
-    WQ_CFG3(1, 8, 8192),   // 2
-    WQ_CFG3(2, 4, 4096),   // 3
-    WQ_CFG3(1, 4, 4096),   // 4
-    WQ_CFG3(4, 2, 4096),   // 5
+    WQ_CFG1(3072, 2),         // 0: default, single launch (63 us on C2)
+    WQ_CFG3(1, 8, 4096 + 2),  // 1: three launches (73 us on C2)
+    WQ_CFG1(4096, 2),         // 2
+    WQ_CFG3(1, 8, 4096 + 8),  // 3
+    WQ_CFG3(4, 2, 4096 + 2),  // 4
 };
 #undef WQ_CFG1
 #undef WQ_CFG3
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
-// Blocks of `fn` the device keeps resident at once (0 if unknown).
-uint32_t resident_blocks(int device, const void* fn) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, 0) != hipSuccess) return 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
-    per_cu = per_cu > 8 ? 8 : per_cu;
-    return (uint32_t)(per_cu * cus);
-}
 }  // namespace
 
 int route_config_count() { return kNumCfgs; }
@@ -129,37 +118,32 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     }
     const RouteIn in{d_pos, d_keys, d_world, d_sender, d_repl, (uint32_t)M, (int64_t)h->cube_size};
 
-    if (cfg.tick) {
-        const uint64_t nb = (M + cfg.tick_rc - 1) / cfg.tick_rc;
-        if (rw.resident_cfg != h->route_cfg) {
-            rw.resident = resident_blocks(h->device, cfg.tick_fn);
-            rw.resident_cfg = h->route_cfg;
+    if (cfg.tick) {  // single launch: one block per 256 messages, decoupled look-back
+        const uint64_t nb = (M + kBlock - 1) / kBlock;
+        WQ_ALLOC(h, rw.agg, 2 * nb * 8);
+        if (rw.agg_zeroed < 2 * nb) {  // fresh granules: tag 0 never matches a call's tag
+            WQ_HIP(h, hipMemsetAsync(rw.agg.p, 0, rw.agg.bytes, s));
+            rw.agg_zeroed = rw.agg.bytes / 8;
         }
-        if (nb <= rw.resident) {
-            WQ_ALLOC(h, rw.agg, 2 * nb * 8);
-            if (rw.agg_zeroed < 2 * nb) {  // fresh granules: tag 0 never matches a call's tag
-                WQ_HIP(h, hipMemsetAsync(rw.agg.p, 0, rw.agg.bytes, s));
-                rw.agg_zeroed = rw.agg.bytes / 8;
-            }
-            TickParams tp;
-            tp.in = in;
-            tp.t = tv;
-            tp.offsets = d_offsets;
-            tp.out = EmitOut{d_sender, capacity ? d_peers : nullptr, d_msgs, capacity};
-            tp.agg = rw.agg.as<uint64_t>();
-            tp.tag = (uint32_t)(rw.calls % 0xFFFFFFFFull) + 1u;
-            tp.cnt = cur;
-            tp.cnt_next = nxt;
-            tp.stamps = rw.stamps;
-            cfg.tick(tp, s, (unsigned)nb);
-            WQ_HIP(h, hipGetLastError());
-            if (pr.enabled) {
-                WQ_HIP(h, hipEventRecord(pr.stop[pr.used], s));
-                pr.used++;
-            }
-            rw.calls++;
-            return WQ_OK;
+        TickParams tp;
+        tp.in = in;
+        tp.t = tv;
+        tp.offsets = d_offsets;
+        tp.out = EmitOut{d_sender, capacity ? d_peers : nullptr, d_msgs, capacity};
+        tp.look = rw.agg.as<uint64_t>();
+        tp.fgran = tp.look + nb;
+        tp.tag = (uint32_t)(rw.calls % ((1ull << 30) - 1)) + 1u;
+        tp.cnt = cur;
+        tp.cnt_next = nxt;
+        tp.stamps = rw.stamps;
+        cfg.tick(tp, s, (unsigned)nb);
+        WQ_HIP(h, hipGetLastError());
+        if (pr.enabled) {
+            WQ_HIP(h, hipEventRecord(pr.stop[pr.used], s));
+            pr.used++;
         }
+        rw.calls++;
+        return WQ_OK;
     }
 
     const uint32_t count_tile = cfg.count_tile;
@@ -208,10 +192,12 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     ep.msgs = d_msgs;
     ep.capacity = capacity;
     const dim3 eg((unsigned)((M + kBlock - 1) / kBlock));
-    if (cfg.emit_stage == 8192)
-        hipLaunchKernelGGL(emit_kernel<8192>, eg, dim3(kBlock), 0, s, ep);
+    if (cfg.emit_stage == 4096 + 2)
+        hipLaunchKernelGGL((emit_kernel<4096, 2>), eg, dim3(kBlock), 0, s, ep);
+    else if (cfg.emit_stage == 4096 + 4)
+        hipLaunchKernelGGL((emit_kernel<4096, 4>), eg, dim3(kBlock), 0, s, ep);
     else
-        hipLaunchKernelGGL(emit_kernel<4096>, eg, dim3(kBlock), 0, s, ep);
+        hipLaunchKernelGGL((emit_kernel<4096, 8>), eg, dim3(kBlock), 0, s, ep);
     WQ_HIP(h, hipGetLastError());
     if (pr.enabled) {
         WQ_HIP(h, hipEventRecord(pr.stop[pr.used], s));
