@@ -125,6 +125,18 @@ int wq_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_key
                          size_t n_msgs, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs,
                          size_t capacity, wq_route_counters* d_counters);
 
+/* ---- C5: exact radius filter after the cube broadphase ----
+ * An extension the reference does not have (it stores no peer positions). With a radius > 0 set,
+ * every subsequent tick keeps a (message, peer) pair only if additionally
+ *     dx = mx - px; dy = my - py; dz = mz - pz;   (dx*dx + dy*dy) + dz*dz <= radius*radius
+ * evaluated left to right in f64 without FMA contraction, m = the message position, p = the
+ * peer's position from the latest wq_set_peer_positions; a peer id >= n_peers has no position and
+ * is dropped. Ticks with the filter on take message positions (keys must be NULL).
+ * radius <= 0 or NaN turns the filter off. */
+int wq_set_peer_positions(wq_router* h, const double* pos, size_t n_peers);
+int wq_set_peer_positions_device(wq_router* h, const double* d_pos, size_t n_peers);
+int wq_set_radius(wq_router* h, double radius);
+
 /* ---- queries (the reference uses these in its unit tests, area_map.rs:33-67) ---- */
 /* AreaMap::is_peer_subscribed(uuid, cube), batched; key_or_pos is n x 3 (int64 if key_is_raw). */
 int wq_is_subscribed(wq_router* h, size_t n, const uint32_t* world, const uint32_t* peer,

@@ -124,6 +124,10 @@ def load_c_oracle():
     lib.wqo_route.restype = sz
     lib.wqo_counts.argtypes = [vp, vp, vp]
     lib.wqo_counts.restype = None
+    lib.wqo_route_radius.argtypes = [vp, vp, vp, vp, vp, sz, vp, sz, ctypes.c_double, vp, vp, sz, vp]
+    lib.wqo_route_radius.restype = sz
+    lib.wqo_route_global.argtypes = [vp, vp, vp, vp, sz, vp, vp, sz]
+    lib.wqo_route_global.restype = sz
     _lib = lib
     return lib
 
@@ -217,6 +221,39 @@ class COracle:
         peers = peers[:P]
         sort_within_segments(offsets, peers)
         return offsets, peers, F.value
+
+
+    def route_radius(self, pos, world, sender, repl, peer_pos, radius: float):
+        """C5: route() intersected with the exact radius predicate (wq_oracle.c wqo_route_radius)."""
+        world = np.ascontiguousarray(world, dtype=np.uint32)
+        M = len(world)
+        sender = np.ascontiguousarray(sender, dtype=np.uint32)
+        repl = np.ascontiguousarray(repl, dtype=np.uint8)
+        pos_a = np.ascontiguousarray(pos, dtype=np.float64).reshape(-1, 3)
+        pp = np.ascontiguousarray(peer_pos, dtype=np.float64).reshape(-1, 3)
+        offsets = np.zeros(M + 1, dtype=np.uint32)
+        F = ctypes.c_uint64()
+        args = (self.h, _ptr(pos_a), _ptr(world), _ptr(sender), _ptr(repl), M, _ptr(pp), len(pp), float(radius))
+        P = self.lib.wqo_route_radius(*args, _ptr(offsets), None, 0, ctypes.byref(F))
+        peers = np.zeros(max(P, 1), dtype=np.uint32)
+        self.lib.wqo_route_radius(*args, _ptr(offsets), _ptr(peers), P, None)
+        peers = peers[:P]
+        sort_within_segments(offsets, peers)
+        return offsets, peers, F.value
+
+    def route_global(self, world, sender, repl):
+        """GlobalMessage to named worlds (global_message.rs:36-84)."""
+        world = np.ascontiguousarray(world, dtype=np.uint32)
+        M = len(world)
+        sender = np.ascontiguousarray(sender, dtype=np.uint32)
+        repl = np.ascontiguousarray(repl, dtype=np.uint8)
+        offsets = np.zeros(M + 1, dtype=np.uint32)
+        P = self.lib.wqo_route_global(self.h, _ptr(world), _ptr(sender), _ptr(repl), M, _ptr(offsets), None, 0)
+        peers = np.zeros(max(P, 1), dtype=np.uint32)
+        self.lib.wqo_route_global(self.h, _ptr(world), _ptr(sender), _ptr(repl), M, _ptr(offsets), _ptr(peers), P)
+        peers = peers[:P]
+        sort_within_segments(offsets, peers)
+        return offsets, peers
 
 
 def sort_within_segments(offsets: np.ndarray, values: np.ndarray) -> None:

@@ -475,6 +475,73 @@ size_t wqo_route(const wqo_world_map* wm, const double* pos, const int64_t* keys
     return P;
 }
 
+/* C5 (an extension the reference does not have): handle_local_message's
+ * recipients (wqo_route) intersected with the exact Euclidean radius predicate
+ *   dx = mx - px; dy = my - py; dz = mz - pz; keep iff (dx*dx + dy*dy) + dz*dz <= r*r
+ * evaluated left to right in f64 with no FMA contraction (this file is built -ffp-contract=off).
+ * peer_pos holds n_pos peers x 3; a peer id >= n_pos (no known position) is never within range,
+ * and NaN compares false. Messages carry positions (no raw keys). */
+size_t wqo_route_radius(const wqo_world_map* wm, const double* pos, const uint32_t* world, const uint32_t* sender,
+                        const uint8_t* repl, size_t M, const double* peer_pos, size_t n_pos, double radius,
+                        uint32_t* offsets, uint32_t* peers, size_t cap, uint64_t* n_candidates) {
+    size_t P = 0;
+    uint64_t F = 0;
+    const double r2 = radius * radius;
+    for (size_t m = 0; m < M; ++m) {
+        if (offsets) offsets[m] = (uint32_t)P;
+        const area_map* am = wm_get(wm, world[m]);
+        if (!am) continue;
+        int64_t k[3];
+        to_cube_area(0, pos + 3 * m, wm->cube_size, k);
+        const cube_slot* c = cm_find(&am->map, k);
+        if (!c) continue;
+        const uint32_t me = sender[m];
+        const uint8_t r = repl[m];
+        F += c->set.n;
+        for (uint32_t i = 0; i < c->set.n; ++i) {
+            const uint32_t p = c->set.v[i];
+            int keep = (r == 1) ? 1 : (r == 2) ? (p == me) : (p != me);
+            if (!keep || p >= n_pos) continue;
+            const double dx = pos[3 * m] - peer_pos[3 * (size_t)p];
+            const double dy = pos[3 * m + 1] - peer_pos[3 * (size_t)p + 1];
+            const double dz = pos[3 * m + 2] - peer_pos[3 * (size_t)p + 2];
+            const double d2 = dx * dx + dy * dy + dz * dz;
+            if (!(d2 <= r2)) continue;
+            if (peers && P < cap) peers[P] = p;
+            P++;
+        }
+    }
+    if (offsets) offsets[M] = (uint32_t)P;
+    if (n_candidates) *n_candidates = F;
+    return P;
+}
+
+/* handle_global_message for a named world (global_message.rs:36-84): the recipients are
+ * AreaMap::get_subscribed_any_peers (area_map.rs:65-67) of the world, if it exists, under the same
+ * replication filter as a LocalMessage. (The "@global" broadcast to every connected peer,
+ * global_message.rs:18-35, is a PeerMap operation outside the subscription table.) */
+size_t wqo_route_global(const wqo_world_map* wm, const uint32_t* world, const uint32_t* sender, const uint8_t* repl,
+                        size_t M, uint32_t* offsets, uint32_t* peers, size_t cap) {
+    size_t P = 0;
+    for (size_t m = 0; m < M; ++m) {
+        if (offsets) offsets[m] = (uint32_t)P;
+        const area_map* am = wm_get(wm, world[m]);
+        if (!am) continue; /* :50-54 */
+        const uint32_t me = sender[m];
+        const uint8_t r = repl[m];
+        for (size_t i = 0; i < am->subscribed_peers.cap; ++i) {
+            if (am->subscribed_peers.st[i] != SLOT_FULL) continue;
+            const uint32_t p = am->subscribed_peers.key[i];
+            int keep = (r == 1) ? 1 : (r == 2) ? (p == me) : (p != me);
+            if (!keep) continue;
+            if (peers && P < cap) peers[P] = p;
+            P++;
+        }
+    }
+    if (offsets) offsets[M] = (uint32_t)P;
+    return P;
+}
+
 void wqo_counts(const wqo_world_map* wm, uint64_t* n_entries, uint64_t* n_cubes) {
     uint64_t e = 0, c = 0;
     for (size_t i = 0; i < wm->cap; ++i) {

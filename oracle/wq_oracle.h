@@ -61,6 +61,16 @@ size_t wqo_route(const wqo_world_map* wm, const double* pos, const int64_t* keys
                  const uint32_t* world, const uint32_t* sender, const uint8_t* repl, size_t M,
                  uint32_t* offsets, uint32_t* peers, size_t cap, uint64_t* n_candidates);
 
+/* C5 extension: wqo_route's recipients with the exact radius predicate
+ * (dx*dx + dy*dy) + dz*dz <= r*r in f64, d = message position - peer position; peers >= n_pos
+ * have no position and are dropped. */
+size_t wqo_route_radius(const wqo_world_map* wm, const double* pos, const uint32_t* world, const uint32_t* sender,
+                        const uint8_t* repl, size_t M, const double* peer_pos, size_t n_pos, double radius,
+                        uint32_t* offsets, uint32_t* peers, size_t cap, uint64_t* n_candidates);
+/* GlobalMessage to a named world, global_message.rs:36-84 (get_subscribed_any_peers + replication). */
+size_t wqo_route_global(const wqo_world_map* wm, const uint32_t* world, const uint32_t* sender, const uint8_t* repl,
+                        size_t M, uint32_t* offsets, uint32_t* peers, size_t cap);
+
 /* Stats for tests: number of live (world,cube,peer) entries and of non-empty cubes. */
 void wqo_counts(const wqo_world_map* wm, uint64_t* n_entries, uint64_t* n_cubes);
 

@@ -9,6 +9,8 @@ namespace wq {
 // ------------------------------------------------------------------------------------------
 struct EmitParams {
     const uint32_t* sender;
+    const double* pos;    // radius mode only
+    const uint8_t* repl;  // radius mode only
     uint32_t M;
     TableView t;
     const uint32_t* e;            // filtered counts (count pass)
@@ -29,9 +31,11 @@ struct EmitRowSmem {
     alignas(16) uint8_t om[STAGE];   // ... and the row-local index of each position's message
     uint32_t gq_j[kBlock];    // messages with more than kInline peers (or a full-key slot-table cube)
     uint32_t gq_off[kBlock];  // ... index of the list's first peer in `list`
-    uint32_t gq_skip[kBlock]; // ... skipped list index or kNone
+    uint32_t gq_skip[kBlock]; // ... skipped list index or kNone (radius mode: the list length)
     uint32_t gq_e[kBlock];    // ... outputs
     uint32_t gq_st[kBlock];   // ... row-local first output
+    uint32_t gq_pre[kBlock + 1];  // ... prefix of their slices of the current window
+    uint32_t scan_tot[kWaves];
     uint32_t n_gq;
 };
 
@@ -40,7 +44,31 @@ struct EmitOut {
     uint32_t* peers;
     uint32_t* msgs;
     uint64_t capacity;
+    const double* pos;     // message positions (radius mode)
+    const uint8_t* repl;   // replication codes (radius mode)
 };
+
+__device__ __forceinline__ bool repl_keeps(uint8_t rp, uint32_t peer, uint32_t me) {
+    return rp == WQ_REPL_INCLUDING_SELF ? true : rp == WQ_REPL_ONLY_SELF ? (peer == me) : (peer != me);
+}
+
+// Row-local exclusive scan of e over the block's 256 threads; returns this thread's start and
+// the row total.
+__device__ __forceinline__ uint32_t row_scan(uint32_t e, uint32_t* wave_tot, uint32_t* total) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t incl = wave_incl_scan_add(e, lane);
+    if (lane == 63) wave_tot[wave] = incl;
+    lds_barrier();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int u = 0; u < kWaves; ++u) {
+        const uint32_t t = wave_tot[u];
+        if (u < wave) before += t;
+        tot += t;
+    }
+    *total = tot;
+    return before + incl - e;
+}
 
 // Kernel (3) for one row of 256 messages m0 + threadIdx.x whose filtered counts e, locators inf
 // and row-local first outputs st the caller holds; the row's outputs go to [g0, g0 + T).
@@ -48,20 +76,23 @@ struct EmitOut {
 // global output's 16-byte quads, then written with one 16-byte store per lane per array (the
 // row's first and last quads, shared with the neighbouring rows, word by word).
 //   inline records (<= kInline peers): eight lanes per record line, lane `part` < 6 reading chunk
-//     2 + part = peers 4*part .. 4*part+3 only if it holds one of the message's peers; all 64
-//     messages of a wave in flight at once; the sender's own entry is dropped while staging;
-//   longer lists: the block copies the window's slice of each from `list`;
+//     2 + part = peers 4*part .. 4*part+3 only if it holds one of the message's peers; U rounds
+//     of the wave's 64 messages in flight at once; the sender's own entry (radius mode: every
+//     peer outside the locator's survivor mask) is dropped while staging;
+//   longer lists: the window's slices of all of them are copied from `list` as one flat,
+//     block-strided range (coalesced loads, four in flight per thread); in radius mode each list
+//     is re-filtered chunk by chunk with a block-wide compaction;
 //   OnlySelf: the sender, by its own lane.
 // Every thread of the block must call it (it contains barriers); it ends with a barrier.
-template <int STAGE, int U = 8>
+template <int STAGE, int U = 8, bool RADIUS = false>
 __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView& tv, const EmitOut& o, uint32_t m0,
                                          uint32_t e, uint2 inf, uint32_t st, uint64_t g0, uint32_t T) {
     static_assert(STAGE % 1024 == 0, "STAGE: whole quads for every lane");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid == 0) sm.n_gq = 0;
     lds_barrier();
-    uint32_t sl = kNone, cnt = 0, skip = kNone;
-    const bool self = e && (inf.x & kLocSelf);
+    uint32_t sl = kNone, cnt = 0, skip = kNone;  // radius mode: skip holds the survivor mask
+    const bool self = !RADIUS && e && (inf.x & kLocSelf);
     const uint32_t self_peer = self ? o.sender[m0 + tid] : 0u;
     if (e && !self) {
         if (inf.x & kLocGlobal) {
@@ -75,7 +106,7 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
             const uint32_t s24 = inf.y & kSkipNone24;
             sl = inf.x;
             cnt = inf.y >> 24;
-            skip = s24 == kSkipNone24 ? kNone : s24;
+            skip = RADIUS ? s24 : (s24 == kSkipNone24 ? kNone : s24);
         }
     }
     // record chunks of the wave's 64 messages: message q by lanes 8*(q%8) .. +7, round q/8,
@@ -116,8 +147,14 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const uint32_t idx = 4u * part + i;  // peer index in the cube's list
-                    if (idx >= q_cnt[u] || idx == q_skip[u]) continue;
-                    const uint32_t pos = lead + q_st[u] + idx - (idx > q_skip[u] && q_skip[u] != kNone ? 1u : 0u);
+                    uint32_t pos;
+                    if (RADIUS) {
+                        if (idx >= q_cnt[u] || !((q_skip[u] >> idx) & 1u)) continue;
+                        pos = lead + q_st[u] + (uint32_t)__popc(q_skip[u] & ((1u << idx) - 1u));
+                    } else {
+                        if (idx >= q_cnt[u] || idx == q_skip[u]) continue;
+                        pos = lead + q_st[u] + idx - (idx > q_skip[u] && q_skip[u] != kNone ? 1u : 0u);
+                    }
                     if (pos >= w0 && pos < w1) {
                         sm.op[pos - w0] = vv[i];
                         sm.om[pos - w0] = j;
@@ -125,14 +162,71 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
                 }
             }
         }
-        for (uint32_t q = 0; q < n_gq; ++q) {
-            const uint32_t j = sm.gq_j[q], s0 = lead + sm.gq_st[q], ej = sm.gq_e[q];
-            const uint32_t lo = s0 > w0 ? s0 : w0, hi = s0 + ej < w1 ? s0 + ej : w1;
-            const uint32_t off = sm.gq_off[q], sk = sm.gq_skip[q];
-            for (uint32_t k = lo + tid; k < hi; k += kBlock) {
-                const uint32_t oi = k - s0;
-                sm.op[k - w0] = tv.list[off + oi + (oi >= sk ? 1u : 0u)];
-                sm.om[k - w0] = (uint8_t)j;
+        if (n_gq) {
+            if (RADIUS) {
+                // re-filter each long list chunk by chunk, compacting survivors block-wide
+                for (uint32_t q = 0; q < n_gq; ++q) {
+                    const uint32_t j = sm.gq_j[q], s0 = lead + sm.gq_st[q], ej = sm.gq_e[q];
+                    if (s0 >= w1 || s0 + ej <= w0) continue;  // block-uniform
+                    const uint32_t off = sm.gq_off[q], len = sm.gq_skip[q];
+                    const uint32_t m = m0 + j, me = o.sender[m];
+                    const uint8_t rp = o.repl[m];
+                    const double mx = o.pos[3ull * m], my = o.pos[3ull * m + 1], mz = o.pos[3ull * m + 2];
+                    uint32_t run = 0;
+                    for (uint32_t b = 0; b < len; b += kBlock) {
+                        const uint32_t i = b + tid;
+                        const uint32_t peer = i < len ? tv.list[off + i] : 0u;
+                        const bool ok = i < len && repl_keeps(rp, peer, me) && within_radius(tv, mx, my, mz, peer);
+                        uint32_t tot;
+                        const uint32_t at = row_scan(ok ? 1u : 0u, sm.scan_tot, &tot);
+                        const uint32_t pos = s0 + run + at;
+                        if (ok && pos >= w0 && pos < w1) {
+                            sm.op[pos - w0] = peer;
+                            sm.om[pos - w0] = (uint8_t)j;
+                        }
+                        run += tot;
+                        lds_barrier();  // scan_tot reuse
+                    }
+                }
+            } else {
+                // the window's slices of every long list as one flat, block-strided range
+                if (tid == 0) {
+                    uint32_t acc = 0;
+                    for (uint32_t q = 0; q < n_gq; ++q) {
+                        const uint32_t s0 = lead + sm.gq_st[q], ej = sm.gq_e[q];
+                        const uint32_t lo = s0 > w0 ? s0 : w0, hi = s0 + ej < w1 ? s0 + ej : w1;
+                        sm.gq_pre[q] = acc;
+                        acc += hi > lo ? hi - lo : 0u;
+                    }
+                    sm.gq_pre[n_gq] = acc;
+                }
+                lds_barrier();
+                const uint32_t W = sm.gq_pre[n_gq];
+                uint32_t q = 0;
+                for (uint32_t k0 = tid; k0 < W; k0 += 4 * kBlock) {
+                    uint32_t val[4], dst[4], jj[4];
+                    bool ok[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t k = k0 + u * kBlock;
+                        ok[u] = k < W;
+                        if (!ok[u]) continue;
+                        while (sm.gq_pre[q + 1] <= k) ++q;  // owners ascend with k
+                        const uint32_t s0 = lead + sm.gq_st[q];
+                        const uint32_t lo = s0 > w0 ? s0 : w0;
+                        const uint32_t posn = lo + (k - sm.gq_pre[q]);  // image-space position
+                        const uint32_t oi = posn - s0, sk = sm.gq_skip[q];
+                        val[u] = tv.list[sm.gq_off[q] + oi + (oi >= sk ? 1u : 0u)];
+                        dst[u] = posn - w0;
+                        jj[u] = sm.gq_j[q];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (!ok[u]) continue;
+                        sm.op[dst[u]] = val[u];
+                        sm.om[dst[u]] = (uint8_t)jj[u];
+                    }
+                }
             }
         }
         lds_barrier();
@@ -160,27 +254,10 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
     }
 }
 
-// Row-local exclusive scan of e over the block's 256 threads; returns this thread's start and
-// the row total.
-__device__ __forceinline__ uint32_t row_scan(uint32_t e, uint32_t* wave_tot, uint32_t* total) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t incl = wave_incl_scan_add(e, lane);
-    if (lane == 63) wave_tot[wave] = incl;
-    lds_barrier();
-    uint32_t before = 0, tot = 0;
-#pragma unroll
-    for (int u = 0; u < kWaves; ++u) {
-        const uint32_t t = wave_tot[u];
-        if (u < wave) before += t;
-        tot += t;
-    }
-    *total = tot;
-    return before + incl - e;
-}
 
 // Pass 3 of the three-launch tick: one 256-message row per block. CSR offsets = count-block
 // prefix (tile_scan) + the in-block prefix, then emit_row.
-template <int STAGE, int U>
+template <int STAGE, int U, bool RADIUS = false>
 __global__ __launch_bounds__(kBlock) void emit_kernel(EmitParams p) {
     __shared__ EmitRowSmem<STAGE> sm;
     __shared__ uint32_t wave_tot[kWaves];
@@ -203,7 +280,8 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(EmitParams p) {
     for (int u = 0; u < kWaves; ++u) g += part_tot[u];
     if (m < p.M) p.offsets[m] = g + st;
     if (!p.peers) return;  // counts-only call: offsets are all that is asked for
-    emit_row<STAGE, U>(sm, p.t, EmitOut{p.sender, p.peers, p.msgs, p.capacity}, m0, e, inf, st, g, T);
+    emit_row<STAGE, U, RADIUS>(sm, p.t, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl}, m0, e, inf,
+                               st, g, T);
 }
 
 }  // namespace wq

@@ -186,7 +186,23 @@ struct TableView {
     uint64_t hash_mask;
     const uint32_t* list;
     double sf;
+    // C5 radius filter (wq_set_radius): peer positions (n_ppos x 3) and r^2; r2 < 0: off
+    const double* ppos;
+    uint32_t n_ppos;
+    double r2;
 };
+
+// C5: is peer p within the radius of message position (mx, my, mz)? f64, left to right, no FMA
+// (this file is compiled with contraction off), a peer without a position never is.
+__device__ __forceinline__ bool within_radius(const TableView& t, double mx, double my, double mz, uint32_t p) {
+    if (p >= t.n_ppos) return false;
+    const double* q = t.ppos + 3ull * p;
+    const double dx = mx - q[0];
+    const double dy = my - q[1];
+    const double dz = mz - q[2];
+    const double d2 = dx * dx + dy * dy + dz * dz;
+    return d2 <= t.r2;
+}
 
 // Header of the record probe sequence for pk: walks while the slot holds another key.
 __device__ __forceinline__ uint64_t find_record(const TableView& t, uint64_t pk, uint4* hdr) {

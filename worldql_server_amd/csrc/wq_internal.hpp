@@ -105,6 +105,10 @@ struct wq_router {
     int route_cfg = 0;  // route kernel shapes (wq_route.hip kCfgs)
     // host-pointer convenience buffers
     wq::DevBuf h_in, h_out;
+    // C5 radius filter (wq_set_radius / wq_set_peer_positions)
+    wq::DevBuf ppos;
+    uint64_t n_ppos = 0;
+    double radius = 0.0;
     wq::ProfileEvents prof;
 };
 
@@ -120,6 +124,9 @@ inline TableView table_view(const wq_router* h) {
     v.hash_mask = h->hash_mask;
     v.list = h->tab.list.as<uint32_t>();
     v.sf = (double)h->cube_size;
+    v.ppos = h->ppos.as<double>();
+    v.n_ppos = (uint32_t)h->n_ppos;
+    v.r2 = h->radius > 0.0 ? h->radius * h->radius : -1.0;
     return v;
 }
 // wq_route.hip

@@ -28,6 +28,7 @@
 #include "route_emit.hpp"
 #include "route_scan.hpp"
 #include "route_tick.hpp"
+#include "route_radius.hpp"
 
 namespace wq {
 
@@ -118,7 +119,9 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     }
     const RouteIn in{d_pos, d_keys, d_world, d_sender, d_repl, (uint32_t)M, (int64_t)h->cube_size};
 
-    if (cfg.tick) {  // single launch: one block per 256 messages, decoupled look-back
+    const bool radius = h->radius > 0.0;
+    if (radius && !d_pos) return set_error(h, WQ_E_INVALID, "the radius filter needs message positions");
+    if (cfg.tick && !radius) {  // single launch: one block per 256 messages, decoupled look-back
         const uint64_t nb = (M + kBlock - 1) / kBlock;
         WQ_ALLOC(h, rw.agg, 2 * nb * 8);
         if (rw.agg_zeroed < 2 * nb) {  // fresh granules: tag 0 never matches a call's tag
@@ -129,7 +132,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         tp.in = in;
         tp.t = tv;
         tp.offsets = d_offsets;
-        tp.out = EmitOut{d_sender, capacity ? d_peers : nullptr, d_msgs, capacity};
+        tp.out = EmitOut{d_sender, capacity ? d_peers : nullptr, d_msgs, capacity, d_pos, d_repl};
         tp.look = rw.agg.as<uint64_t>();
         tp.fgran = tp.look + nb;
         tp.tag = (uint32_t)(rw.calls % ((1ull << 30) - 1)) + 1u;
@@ -146,7 +149,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         return WQ_OK;
     }
 
-    const uint32_t count_tile = cfg.count_tile;
+    const uint32_t count_tile = radius ? (uint32_t)kBlock : (uint32_t)cfg.count_tile;
     const uint32_t n_count = (uint32_t)((M + count_tile - 1) / count_tile);
     WQ_ALLOC(h, rw.info, M * sizeof(uint2));
     WQ_ALLOC(h, rw.e, M * 4);
@@ -164,7 +167,10 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     cp.tile_F = tile_F;
     cp.cnt = cur;
     cp.cnt_next = nxt;
-    cfg.count(cp, s, n_count);
+    if (radius)
+        hipLaunchKernelGGL(count_radius_kernel, dim3(n_count), dim3(kBlock), 0, s, cp);
+    else
+        cfg.count(cp, s, n_count);
     WQ_HIP(h, hipGetLastError());
 
     TileScanParams sp;
@@ -181,6 +187,8 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
 
     EmitParams ep;
     ep.sender = d_sender;
+    ep.pos = d_pos;
+    ep.repl = d_repl;
     ep.M = (uint32_t)M;
     ep.t = tv;
     ep.e = rw.e.as<uint32_t>();
@@ -192,7 +200,9 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     ep.msgs = d_msgs;
     ep.capacity = capacity;
     const dim3 eg((unsigned)((M + kBlock - 1) / kBlock));
-    if (cfg.emit_stage == 4096 + 2)
+    if (radius)
+        hipLaunchKernelGGL((emit_kernel<4096, 2, true>), eg, dim3(kBlock), 0, s, ep);
+    else if (cfg.emit_stage == 4096 + 2)
         hipLaunchKernelGGL((emit_kernel<4096, 2>), eg, dim3(kBlock), 0, s, ep);
     else if (cfg.emit_stage == 4096 + 4)
         hipLaunchKernelGGL((emit_kernel<4096, 4>), eg, dim3(kBlock), 0, s, ep);

@@ -130,6 +130,30 @@ int wq_get_stats(wq_router* h, wq_stats* out) {
 
 int wq_debug_route_config_count(void) { return route_config_count(); }
 
+static int set_peer_positions(wq_router* h, const double* pos, size_t n, hipMemcpyKind kind) {
+    if (!h || (n && !pos) || n > 0xFFFFFFFFull) return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    WQ_ALLOC(h, h->ppos, (n ? n : 1) * 24);
+    if (n) WQ_HIP(h, hipMemcpyAsync(h->ppos.p, pos, n * 24, kind, h->stream));
+    if (kind == hipMemcpyHostToDevice) WQ_HIP(h, hipStreamSynchronize(h->stream));
+    h->n_ppos = n;
+    return WQ_OK;
+}
+
+int wq_set_peer_positions(wq_router* h, const double* pos, size_t n_peers) {
+    return set_peer_positions(h, pos, n_peers, hipMemcpyHostToDevice);
+}
+
+int wq_set_peer_positions_device(wq_router* h, const double* d_pos, size_t n_peers) {
+    return set_peer_positions(h, d_pos, n_peers, hipMemcpyDeviceToDevice);
+}
+
+int wq_set_radius(wq_router* h, double radius) {
+    if (!h) return WQ_E_INVALID;
+    h->radius = (radius > 0.0) ? radius : 0.0;  // NaN compares false: off
+    return WQ_OK;
+}
+
 int wq_debug_set_route_config(wq_router* h, int cfg) {
     if (!h || cfg < 0 || cfg >= route_config_count()) return WQ_E_INVALID;
     h->route_cfg = cfg;

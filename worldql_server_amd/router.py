@@ -65,6 +65,9 @@ def load_library(build_if_missing: bool = True):
         "wq_debug_set_route_config": ([vp, i32], i32),
         "wq_debug_route_config_count": ([], i32),
         "wq_debug_set_timeline": ([vp, vp], i32),
+        "wq_set_peer_positions": ([vp, vp, sz], i32),
+        "wq_set_peer_positions_device": ([vp, vp, sz], i32),
+        "wq_set_radius": ([vp, ctypes.c_double], i32),
         "wq_shard_ops": ([vp, vp, sz, u32, vp], i32),
         "wq_shard_messages_device": ([vp, vp, vp, vp, vp, vp, sz, u32, vp, vp], i32),
         "wq_route_records_device": ([vp, vp, sz, vp, vp, vp, sz, vp], i32),
@@ -195,6 +198,17 @@ class Router:
         self._check(self.lib.wq_route_records_device(self.h, recs_ptr or None, n_msgs, offsets_ptr,
                                                      peers_ptr or None, msgs_ptr or None, capacity,
                                                      counters_ptr or None))
+
+    # ---- C5 radius filter (include/wq_router.h) ----
+    def set_peer_positions(self, pos) -> None:
+        p = np.ascontiguousarray(pos, dtype=np.float64).reshape(-1, 3)
+        self._check(self.lib.wq_set_peer_positions(self.h, _p(p), len(p)))
+
+    def set_peer_positions_device(self, pos_ptr: int, n_peers: int) -> None:
+        self._check(self.lib.wq_set_peer_positions_device(self.h, pos_ptr or None, n_peers))
+
+    def set_radius(self, radius: float) -> None:
+        self._check(self.lib.wq_set_radius(self.h, float(radius)))
 
     def set_stream(self, stream_ptr: int | None) -> None:
         self._check(self.lib.wq_set_stream(self.h, stream_ptr or None))
