@@ -85,7 +85,7 @@ typedef struct wq_route_counters {
     uint64_t n_pairs;      /* P: (message, peer) pairs after the replication filter */
     uint64_t n_candidates; /* F: peers read from the probed buckets before the filter */
     uint32_t overflow;     /* 1 if P exceeded the caller's capacity (outputs truncated) */
-    uint32_t error;        /* non-zero if a bounded spin gave up (WQ_E_TIMEOUT) */
+    uint32_t error;        /* 4: a bounded spin gave up (WQ_E_TIMEOUT); 2: P > 2^32-1 (WQ_E_CAPACITY) */
 } wq_route_counters;
 
 /* ---- lifetime: replaces WorldMap::new (world_map.rs:17-22) ---- */
@@ -136,6 +136,21 @@ int wq_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_key
 int wq_set_peer_positions(wq_router* h, const double* pos, size_t n_peers);
 int wq_set_peer_positions_device(wq_router* h, const double* d_pos, size_t n_peers);
 int wq_set_radius(wq_router* h, double radius);
+
+/* ---- F1: GlobalMessage to a named world (worldql_server/src/processing/global_message.rs:36-84)
+ * Message m goes to every peer subscribed to at least one cube of world[m]
+ * (AreaMap::get_subscribed_any_peers, area_map.rs:65-67), in ascending peer order, filtered by
+ * repl[m] like LocalMessage: ExceptSelf drops sender[m], OnlySelf keeps only sender[m] (if it is
+ * subscribed in that world), IncludingSelf keeps every peer. A world with no subscriptions yields
+ * nothing (global_message.rs:50-54). Output, capacity and counters as wq_route_tick. The "@global"
+ * broadcast to every connected peer (global_message.rs:18-35) is a peer-map operation and has no
+ * table entry point. */
+int wq_route_global(wq_router* h, const uint32_t* world, const uint32_t* sender, const uint8_t* repl,
+                    size_t n_msgs, uint32_t* offsets, uint32_t* peers, uint32_t* msgs, size_t capacity,
+                    size_t* n_pairs);
+int wq_route_global_device(wq_router* h, const uint32_t* d_world, const uint32_t* d_sender,
+                           const uint8_t* d_repl, size_t n_msgs, uint32_t* d_offsets, uint32_t* d_peers,
+                           uint32_t* d_msgs, size_t capacity, wq_route_counters* d_counters);
 
 /* ---- queries (the reference uses these in its unit tests, area_map.rs:33-67) ---- */
 /* AreaMap::is_peer_subscribed(uuid, cube), batched; key_or_pos is n x 3 (int64 if key_is_raw). */

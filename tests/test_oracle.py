@@ -137,3 +137,39 @@ def test_oracle_replication_semantics():
     segs = [peers[offs[i]:offs[i + 1]].tolist() for i in range(6)]
     assert segs == [[3, 9], [3, 5, 9], [5], [3, 5, 9], [], [3, 9]]
     assert F == 18
+
+
+def test_oracle_global_message_semantics():
+    """global_message.rs:36-84 on hand-made worlds: the recipients are the world's subscribed-any
+    peers (area_map.rs:65-67) under the replication filter; an absent world yields nothing."""
+    o = orc.COracle(16)
+    for w, p, k in [(1, 3, 16), (1, 5, 32), (1, 5, 48), (1, 9, -16), (2, 5, 16), (2, 4, 16)]:
+        o.add_subscription(w, p, True, np.array([k, 16, 16]))
+    world = np.array([1, 1, 1, 1, 1, 2, 7, 2, 2], np.uint32)
+    sender = np.array([5, 5, 5, 7, 7, 5, 5, 3, 3], np.uint32)
+    repl = np.array([0, 1, 2, 0, 2, 0, 1, 2, 200], np.uint8)
+    offs, peers = o.route_global(world, sender, repl)
+    segs = [peers[offs[i]:offs[i + 1]].tolist() for i in range(len(world))]
+    assert segs == [[3, 9], [3, 5, 9], [5], [3, 5, 9], [], [4], [], [], [4, 5]]
+
+
+def test_oracle_global_matches_world_peers():
+    """route_global against the subscribed-any sets on a random table (python restatement)."""
+    rng = np.random.default_rng(7)
+    o = orc.COracle(16)
+    n = 3000
+    ops = abi.ops_array(rng.integers(0, 6, n).astype(np.uint32), rng.integers(0, 400, n).astype(np.uint32),
+                        np.where(rng.random(n) < 0.8, abi.OP_SUBSCRIBE, abi.OP_UNSUBSCRIBE).astype(np.uint8),
+                        pos=rng.uniform(-64, 64, (n, 3)))
+    o.apply_ops(ops)
+    M = 500
+    world = rng.integers(0, 8, M).astype(np.uint32)
+    sender = rng.integers(0, 420, M).astype(np.uint32)
+    repl = rng.integers(0, 4, M).astype(np.uint8)
+    offs, peers = o.route_global(world, sender, repl)
+    wp = {w: o.world_peers(w).tolist() for w in range(8)}
+    for i in range(M):
+        s, r = int(sender[i]), int(repl[i])
+        all_ = wp[int(world[i])]
+        want = [q for q in all_ if q == s] if r == 2 else (all_ if r == 1 else [q for q in all_ if q != s])
+        assert peers[offs[i]:offs[i + 1]].tolist() == want

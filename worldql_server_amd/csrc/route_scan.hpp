@@ -32,7 +32,7 @@ __device__ __forceinline__ uint64_t wave_incl_scan_add64(uint64_t v, int lane) {
     return v;
 }
 
-__global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScanParams p) {
+static __global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScanParams p) {
     __shared__ uint64_t s_wave[kScanWaves];
     __shared__ uint64_t s_F[kScanWaves];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;

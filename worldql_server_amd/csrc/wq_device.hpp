@@ -50,7 +50,7 @@ __host__ __device__ __forceinline__ int64_t coord_clamp_dev(double c, double sf,
     const double a = fabs(c);
     const double q = a / sf;
     // exact multiple (and not +-0): the reference returns `c as i64` (cube_area.rs:30-32)
-    const bool is_mult = (q == trunc(q)) & (fma(q, sf, -a) == 0.0) & (c != 0.0);
+    const bool is_mult = (q == trunc(q)) && (fma(q, sf, -a) == 0.0) && (c != 0.0);
     const double r = (a == 0.0) ? sf : ceil(q) * sf;  // round_by_multiple(a, s)
     int64_t res = sat_i64(is_mult ? c : r);
     const bool add = !is_mult & !(r > c);             // `if r > c {r} else {r + size}`, wrapping

@@ -1,0 +1,213 @@
+// wq_global.hip — GlobalMessage to a named world, on the same table.
+//
+// Replaces worldql_server/src/processing/global_message.rs:36-84: for a world that exists, the
+// recipients are AreaMap::get_subscribed_any_peers (worldql_server/src/subscriptions/area_map.rs:65-67) — every peer holding at
+// least one cube in that world — under the LocalMessage replication filter (ExceptSelf drops the
+// sender, OnlySelf keeps only the sender, IncludingSelf keeps everyone). The "@global" broadcast
+// (global_message.rs:18-35) goes to every connected peer, a PeerMap operation outside the table.
+//
+// The table keeps the sorted unique (world << 32 | peer) keys ("any-keys", wq_table.hip), so a
+// world's peer set is one contiguous range of it. A tick of GlobalMessages is
+//   count   one lane per message: two binary searches give the world's range and the sender's
+//           rank inside it; e and a locator {range start, skipped rank};
+//   scan    tile_scan_kernel over the 256-message tiles (route_scan.hpp);
+//   emit    one block per tile: CSR offsets, then the tile's outputs as one flat block-strided
+//           range (owner by a forward walk over the tile's starts), copied from the any-keys with
+//           coalesced loads and stores — a world's range is contiguous, so a 50k-peer world is a
+//           streaming copy.
+#include "route_scan.hpp"
+#include "wq_internal.hpp"
+
+namespace wq {
+
+namespace {
+
+__device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t* a, uint64_t n, uint64_t v) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (a[mid] < v)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+struct GlobalParams {
+    const uint32_t* world;
+    const uint32_t* sender;
+    const uint8_t* repl;
+    uint32_t M;
+    const uint64_t* any;
+    uint64_t n_any;
+    uint32_t* e;
+    uint2* info;  // {first any-key index of the world, skipped rank or kNone} (OnlySelf: kLocSelf)
+    uint32_t* tile_total;
+    uint32_t* tile_F;
+    uint32_t* tile_prefix;
+    uint32_t* offsets;
+    uint32_t* peers;
+    uint32_t* msgs;
+    uint64_t capacity;
+    wq_route_counters* cnt_next;
+};
+
+__global__ __launch_bounds__(kBlock) void global_count_kernel(GlobalParams p) {
+    __shared__ uint64_t wave_F[kWaves];
+    __shared__ uint64_t wave_E[kWaves];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (blockIdx.x == 0 && tid == 0) {
+        p.cnt_next->n_pairs = 0;
+        p.cnt_next->n_candidates = 0;
+        p.cnt_next->overflow = 0;
+        p.cnt_next->error = 0;
+    }
+    const uint32_t m = blockIdx.x * kBlock + tid;
+    uint32_t e = 0, cnt = 0;
+    uint2 info = make_uint2(0, kNone);
+    if (m < p.M) {
+        const uint64_t w = p.world[m], me = p.sender[m];
+        const uint8_t rp = p.repl[m];
+        const uint64_t lo = lower_bound_u64(p.any, p.n_any, w << 32);
+        const uint64_t hi = lower_bound_u64(p.any, p.n_any, (w + 1) << 32);
+        cnt = (uint32_t)(hi - lo);
+        const uint64_t at = lower_bound_u64(p.any, p.n_any, (w << 32) | me);
+        const bool has = at < hi && p.any[at] == ((w << 32) | me);
+        if (rp == WQ_REPL_INCLUDING_SELF) {
+            e = cnt;
+            info = make_uint2((uint32_t)lo, kNone);
+        } else if (rp == WQ_REPL_ONLY_SELF) {
+            e = has ? 1u : 0u;
+            info = make_uint2(kLocSelf, kNone);
+        } else {  // ExceptSelf and unknown codes (replication.rs:40)
+            e = cnt - (has ? 1u : 0u);
+            info = make_uint2((uint32_t)lo, has ? (uint32_t)(at - lo) : kNone);
+        }
+        p.e[m] = e;
+        p.info[m] = info;
+    }
+    const uint64_t Fw = wave_sum_u64(cnt);
+    const uint64_t Ew = wave_sum_u64(e);
+    if (lane == 0) {
+        wave_F[wave] = Fw;
+        wave_E[wave] = Ew;
+    }
+    lds_barrier();
+    if (tid == 0) {
+        uint64_t Fb = 0, Eb = 0;
+#pragma unroll
+        for (int u = 0; u < kWaves; ++u) {
+            Fb += wave_F[u];
+            Eb += wave_E[u];
+        }
+        p.tile_F[blockIdx.x] = Fb > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Fb;
+        p.tile_total[blockIdx.x] = Eb > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Eb;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void global_emit_kernel(GlobalParams p) {
+    __shared__ uint32_t s_st[kBlock + 1];
+    __shared__ uint2 s_inf[kBlock];
+    __shared__ uint32_t s_wave[kWaves];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t m0 = blockIdx.x * kBlock, m = m0 + tid;
+    const uint32_t e = m < p.M ? p.e[m] : 0u;
+    const uint2 inf = (m < p.M && p.peers) ? p.info[m] : make_uint2(0, kNone);
+    const uint32_t g0 = p.tile_prefix[blockIdx.x];
+    const uint32_t incl = wave_incl_scan_add(e, lane);
+    if (lane == 63) s_wave[wave] = incl;
+    lds_barrier();
+    uint32_t before = 0, T = 0;
+#pragma unroll
+    for (int u = 0; u < kWaves; ++u) {
+        if (u < wave) before += s_wave[u];
+        T += s_wave[u];
+    }
+    const uint32_t st = before + incl - e;
+    if (m < p.M) p.offsets[m] = g0 + st;
+    if (!p.peers) return;
+    s_st[tid] = st;
+    s_inf[tid] = inf;
+    if (tid == 0) s_st[kBlock] = T;
+    lds_barrier();
+    uint32_t j = 0;
+    for (uint32_t k0 = tid; k0 < T; k0 += 4 * kBlock) {
+        uint32_t val[4], own[4];
+        bool ok[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t k = k0 + u * kBlock;
+            ok[u] = k < T;
+            if (!ok[u]) continue;
+            while (s_st[j + 1] <= k) ++j;  // owners ascend with k (empty messages are skipped)
+            const uint2 f = s_inf[j];
+            const uint32_t oi = k - s_st[j];
+            if (f.x == kLocSelf) {
+                val[u] = p.sender[m0 + j];
+            } else {
+                val[u] = (uint32_t)p.any[(uint64_t)f.x + oi + (oi >= f.y ? 1u : 0u)];
+            }
+            own[u] = m0 + j;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t out = (uint64_t)g0 + k0 + u * kBlock;
+            if (!ok[u] || out >= p.capacity) continue;
+            p.peers[out] = val[u];
+            if (p.msgs) p.msgs[out] = own[u];
+        }
+    }
+}
+
+}  // namespace
+
+// wq_route_global(_device) body; wq_router.hip validates the arguments.
+int launch_route_global(wq_router* h, const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
+                        size_t M, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity) {
+    hipStream_t s = h->stream;
+    RouteWs& rw = h->rws;
+    wq_route_counters *cur, *nxt;
+    int rc = route_counters(h, M, d_offsets, &cur, &nxt);
+    if (rc || !cur) return rc;
+    const uint32_t n_tiles = (uint32_t)((M + kBlock - 1) / kBlock);
+    WQ_ALLOC(h, rw.info, M * sizeof(uint2));
+    WQ_ALLOC(h, rw.e, M * 4);
+    WQ_ALLOC(h, rw.tiles, (uint64_t)n_tiles * 12);
+    GlobalParams gp;
+    gp.world = d_world;
+    gp.sender = d_sender;
+    gp.repl = d_repl;
+    gp.M = (uint32_t)M;
+    gp.any = h->tab.any.as<uint64_t>();
+    gp.n_any = h->tab.n_any;
+    gp.e = rw.e.as<uint32_t>();
+    gp.info = rw.info.as<uint2>();
+    gp.tile_total = rw.tiles.as<uint32_t>();
+    gp.tile_prefix = gp.tile_total + n_tiles;
+    gp.tile_F = gp.tile_prefix + n_tiles;
+    gp.offsets = d_offsets;
+    gp.peers = capacity ? d_peers : nullptr;
+    gp.msgs = d_msgs;
+    gp.capacity = capacity;
+    gp.cnt_next = nxt;
+    hipLaunchKernelGGL(global_count_kernel, dim3(n_tiles), dim3(kBlock), 0, s, gp);
+    WQ_HIP(h, hipGetLastError());
+    TileScanParams sp;
+    sp.tile_total = gp.tile_total;
+    sp.tile_F = gp.tile_F;
+    sp.tile_prefix = gp.tile_prefix;
+    sp.n_tiles = n_tiles;
+    sp.offsets = d_offsets;
+    sp.M = (uint32_t)M;
+    sp.capacity = capacity;
+    sp.cnt = cur;
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, sp);
+    WQ_HIP(h, hipGetLastError());
+    hipLaunchKernelGGL(global_emit_kernel, dim3(n_tiles), dim3(kBlock), 0, s, gp);
+    WQ_HIP(h, hipGetLastError());
+    rw.calls++;
+    return WQ_OK;
+}
+
+}  // namespace wq

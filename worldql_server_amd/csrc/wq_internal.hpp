@@ -131,6 +131,9 @@ inline TableView table_view(const wq_router* h) {
 }
 // wq_route.hip
 int route_config_count();
+// The tick's counter slots (this call's, the next call's); *cur == nullptr when M == 0 (offsets[0]
+// and both slots zeroed, nothing left to launch).
+int route_counters(wq_router* h, size_t M, uint32_t* d_offsets, wq_route_counters** cur, wq_route_counters** nxt);
 // wq_table.hip
 int table_apply_segment(wq_router* h, const wq_op* ops, size_t n);
 // keys: sorted unique (world << 32 | peer); world == WQ_WORLD_INVALID removes the peer everywhere.

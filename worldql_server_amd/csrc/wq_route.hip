@@ -81,12 +81,10 @@ constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
 int route_config_count() { return kNumCfgs; }
 
-int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
-                 const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t* d_offsets,
-                 uint32_t* d_peers, uint32_t* d_msgs, size_t capacity) {
+int route_counters(wq_router* h, size_t M, uint32_t* d_offsets, wq_route_counters** cur_out,
+                   wq_route_counters** nxt_out) {
     hipStream_t s = h->stream;
     RouteWs& rw = h->rws;
-    const Cfg& cfg = kCfgs[h->route_cfg];
     // workspace: [pad 64][counters x2 (32 B each)] — each call's count pass zeroes the next slot
     if (!rw.buf.p) {
         WQ_ALLOC(h, rw.buf, 128);
@@ -98,13 +96,27 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     wq_route_counters* cur = ring + (rw.calls & 1);
     wq_route_counters* nxt = ring + ((rw.calls + 1) & 1);
     rw.last = cur;
+    *cur_out = cur;
+    *nxt_out = nxt;
     if (M == 0) {
         WQ_HIP(h, hipMemsetAsync(d_offsets, 0, 4, s));
         WQ_HIP(h, hipMemsetAsync(cur, 0, sizeof(wq_route_counters), s));
         WQ_HIP(h, hipMemsetAsync(nxt, 0, sizeof(wq_route_counters), s));
         rw.calls++;
-        return WQ_OK;
+        *cur_out = nullptr;  // nothing to launch
     }
+    return WQ_OK;
+}
+
+int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                 const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t* d_offsets,
+                 uint32_t* d_peers, uint32_t* d_msgs, size_t capacity) {
+    hipStream_t s = h->stream;
+    RouteWs& rw = h->rws;
+    const Cfg& cfg = kCfgs[h->route_cfg];
+    wq_route_counters *cur, *nxt;
+    int rc0 = route_counters(h, M, d_offsets, &cur, &nxt);
+    if (rc0 || !cur) return rc0;
     const TableView tv = table_view(h);
     ProfileEvents& pr = h->prof;
     if (pr.enabled) {

@@ -24,6 +24,8 @@ int launch_shard_messages(wq_router* h, const double* d_pos, const int64_t* d_ke
 int launch_op_owner(wq_router* h, const wq_op* d_ops, size_t n, uint32_t G, uint32_t* d_owner);
 int launch_route_records(wq_router* h, const wq_msg_rec* d_recs, size_t M, uint32_t* d_offsets, uint32_t* d_peers,
                          uint32_t* d_msgs, size_t capacity);
+int launch_route_global(wq_router* h, const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
+                        size_t M, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity);
 }  // namespace wq
 
 using namespace wq;
@@ -57,6 +59,29 @@ int check_device(int device, std::string* why) {
 
 // Host-staging helper: copies `bytes` from host into h->h_in at `offset` (aligned 256).
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// Reads a host-form tick's CSR back (offsets at dout, peers at dout + op, msgs at dout + om).
+int read_back(wq_router* h, size_t M, const char* dout, size_t op, size_t om, size_t cap, size_t capacity,
+              uint32_t* offsets, uint32_t* peers, uint32_t* msgs, size_t* n_pairs) {
+    hipStream_t s = h->stream;
+    wq_route_counters cnt;
+    WQ_HIP(h, hipMemcpyAsync(&cnt, h->rws.last, sizeof(cnt), hipMemcpyDeviceToHost, s));
+    WQ_HIP(h, hipStreamSynchronize(s));
+    if (M == 0) cnt.n_pairs = 0;
+    *n_pairs = cnt.n_pairs;
+    if (cnt.error & 4u) return set_error(h, WQ_E_TIMEOUT, "route look-back spin gave up");
+    if (cnt.n_pairs > 0xFFFFFFFFull || cnt.error) return set_error(h, WQ_E_CAPACITY, "more than 2^32-1 pairs in one tick");
+    const size_t P = cnt.n_pairs;
+    WQ_HIP(h, hipMemcpyAsync(offsets, dout, (M + 1) * 4, hipMemcpyDeviceToHost, s));
+    const size_t ncopy = std::min(P, cap);
+    if (ncopy) {
+        WQ_HIP(h, hipMemcpyAsync(peers, dout + op, ncopy * 4, hipMemcpyDeviceToHost, s));
+        if (msgs) WQ_HIP(h, hipMemcpyAsync(msgs, dout + om, ncopy * 4, hipMemcpyDeviceToHost, s));
+    }
+    WQ_HIP(h, hipStreamSynchronize(s));
+    if (P > capacity) return set_error(h, WQ_E_CAPACITY, "output capacity too small (required size in *n_pairs)");
+    return WQ_OK;
+}
 
 }  // namespace
 
@@ -261,23 +286,51 @@ int wq_route_tick(wq_router* h, const double* pos, const int64_t* keys, const ui
                           cap ? reinterpret_cast<uint32_t*>(dout + op) : nullptr,
                           (msgs && cap) ? reinterpret_cast<uint32_t*>(dout + om) : nullptr, cap);
     if (rc) return rc;
-    wq_route_counters cnt;
-    WQ_HIP(h, hipMemcpyAsync(&cnt, h->rws.last, sizeof(cnt), hipMemcpyDeviceToHost, s));
-    WQ_HIP(h, hipStreamSynchronize(s));
-    if (M == 0) cnt.n_pairs = 0;
-    *n_pairs = cnt.n_pairs;
-    if (cnt.error) return set_error(h, WQ_E_TIMEOUT, "route look-back spin gave up");
-    if (cnt.n_pairs > 0xFFFFFFFFull) return set_error(h, WQ_E_CAPACITY, "more than 2^32-1 pairs in one tick");
-    const size_t P = cnt.n_pairs;
-    WQ_HIP(h, hipMemcpyAsync(offsets, dout + oo, (M + 1) * 4, hipMemcpyDeviceToHost, s));
-    const size_t ncopy = std::min(P, cap);
-    if (ncopy) {
-        WQ_HIP(h, hipMemcpyAsync(peers, dout + op, ncopy * 4, hipMemcpyDeviceToHost, s));
-        if (msgs) WQ_HIP(h, hipMemcpyAsync(msgs, dout + om, ncopy * 4, hipMemcpyDeviceToHost, s));
-    }
-    WQ_HIP(h, hipStreamSynchronize(s));
-    if (P > capacity) return set_error(h, WQ_E_CAPACITY, "output capacity too small (required size in *n_pairs)");
+    return read_back(h, M, dout, op, om, cap, capacity, offsets, peers, msgs, n_pairs);
+}
+
+int wq_route_global_device(wq_router* h, const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
+                           size_t n_msgs, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity,
+                           wq_route_counters* d_counters) {
+    if (!h || !d_offsets || (n_msgs && (!d_world || !d_sender || !d_repl)) || (capacity && !d_peers))
+        return WQ_E_INVALID;
+    if (n_msgs >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
+    if (capacity > 0xFFFFFFFFull) capacity = 0xFFFFFFFFull;
+    WQ_HIP(h, hipSetDevice(h->device));
+    int rc = launch_route_global(h, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs, capacity);
+    if (rc) return rc;
+    if (d_counters)
+        WQ_HIP(h, hipMemcpyAsync(d_counters, h->rws.last, sizeof(wq_route_counters), hipMemcpyDeviceToDevice,
+                                 h->stream));
     return WQ_OK;
+}
+
+int wq_route_global(wq_router* h, const uint32_t* world, const uint32_t* sender, const uint8_t* repl, size_t M,
+                    uint32_t* offsets, uint32_t* peers, uint32_t* msgs, size_t capacity, size_t* n_pairs) {
+    if (!h || !offsets || !n_pairs || (M && (!world || !sender || !repl)) || (capacity && !peers))
+        return WQ_E_INVALID;
+    if (M >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
+    WQ_HIP(h, hipSetDevice(h->device));
+    const size_t o_w = 0, o_s = align256(M * 4), o_r = align256(o_s + M * 4), n_in = align256(o_r + M + 1);
+    WQ_ALLOC(h, h->h_in, n_in);
+    char* din = h->h_in.as<char>();
+    hipStream_t s = h->stream;
+    if (M) {
+        WQ_HIP(h, hipMemcpyAsync(din + o_w, world, M * 4, hipMemcpyHostToDevice, s));
+        WQ_HIP(h, hipMemcpyAsync(din + o_s, sender, M * 4, hipMemcpyHostToDevice, s));
+        WQ_HIP(h, hipMemcpyAsync(din + o_r, repl, M, hipMemcpyHostToDevice, s));
+    }
+    const size_t cap = std::min<size_t>(capacity, 0xFFFFFFFFull);
+    const size_t op = align256((M + 1) * 4), om = align256(op + cap * 4), n_out = align256(om + (msgs ? cap * 4 : 0));
+    WQ_ALLOC(h, h->h_out, n_out + 256);
+    char* dout = h->h_out.as<char>();
+    int rc = launch_route_global(h, reinterpret_cast<const uint32_t*>(din + o_w),
+                                 reinterpret_cast<const uint32_t*>(din + o_s),
+                                 reinterpret_cast<const uint8_t*>(din + o_r), M, reinterpret_cast<uint32_t*>(dout),
+                                 cap ? reinterpret_cast<uint32_t*>(dout + op) : nullptr,
+                                 (msgs && cap) ? reinterpret_cast<uint32_t*>(dout + om) : nullptr, cap);
+    if (rc) return rc;
+    return read_back(h, M, dout, op, om, cap, capacity, offsets, peers, msgs, n_pairs);
 }
 
 int wq_shard_ops(wq_router* h, const wq_op* ops, size_t n, uint32_t n_shards, uint32_t* owner) {

@@ -54,6 +54,8 @@ def load_library(build_if_missing: bool = True):
         "wq_remove_peers": ([vp, vp, sz], i32),
         "wq_route_tick": ([vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, ctypes.POINTER(sz)], i32),
         "wq_route_tick_device": ([vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, vp], i32),
+        "wq_route_global": ([vp, vp, vp, vp, sz, vp, vp, vp, sz, ctypes.POINTER(sz)], i32),
+        "wq_route_global_device": ([vp, vp, vp, vp, sz, vp, vp, vp, sz, vp], i32),
         "wq_is_subscribed": ([vp, sz, vp, vp, i32, vp, vp], i32),
         "wq_is_subscribed_any": ([vp, sz, vp, vp, vp], i32),
         "wq_world_peers": ([vp, u32, vp, sz, ctypes.POINTER(sz)], i32),
@@ -176,6 +178,35 @@ class Router:
         self._check(self.lib.wq_route_tick_device(self.h, pos_ptr or None, keys_ptr or None, world_ptr, sender_ptr,
                                                   repl_ptr, n_msgs, offsets_ptr, peers_ptr or None,
                                                   msgs_ptr or None, capacity, counters_ptr or None))
+
+    def route_global(self, world, sender, repl, with_msgs: bool = False, capacity: int | None = None):
+        """A tick of GlobalMessages to named worlds (global_message.rs:36-84) on host arrays.
+        Returns (offsets[M+1], peers[P], msgs[P] or None); peers per message ascending."""
+        world = np.ascontiguousarray(world, dtype=np.uint32)
+        M = len(world)
+        sender = np.ascontiguousarray(sender, dtype=np.uint32)
+        repl = np.ascontiguousarray(repl, dtype=np.uint8)
+        cap = capacity if capacity is not None else max(1024, 16 * M)
+        while True:
+            offsets = np.empty(M + 1, dtype=np.uint32)
+            peers = np.empty(max(cap, 1), dtype=np.uint32)
+            msgs = np.empty(max(cap, 1), dtype=np.uint32) if with_msgs else None
+            n = ctypes.c_size_t()
+            rc = self.lib.wq_route_global(self.h, _p(world), _p(sender), _p(repl), M, _p(offsets), _p(peers),
+                                          _p(msgs), cap, ctypes.byref(n))
+            if rc == abi.WQ_E_CAPACITY and n.value > cap and capacity is None:
+                cap = n.value
+                continue
+            self._check(rc)
+            P = n.value
+            return offsets, peers[:P], (msgs[:P] if with_msgs else None)
+
+    def route_global_device(self, world_ptr: int, sender_ptr: int, repl_ptr: int, n_msgs: int, offsets_ptr: int,
+                            peers_ptr: int | None, msgs_ptr: int | None, capacity: int,
+                            counters_ptr: int | None = None) -> None:
+        self._check(self.lib.wq_route_global_device(self.h, world_ptr, sender_ptr, repl_ptr, n_msgs, offsets_ptr,
+                                                    peers_ptr or None, msgs_ptr or None, capacity,
+                                                    counters_ptr or None))
 
     # ---- multi-GPU (cube-hash ownership; driven by sharded.py) ----
     def shard_ops(self, ops: np.ndarray, n_shards: int) -> np.ndarray:
