@@ -1,0 +1,185 @@
+"""GPU parity for incremental table updates (wq_delta.hip, SURVEY.md §8(d) C4 churn): small op
+batches against a built table are applied in place; every tick is compared with the C
+restatement (oracle/) — routing CSR, membership queries, any-sets and counts — and the tests
+check that the incremental path (not the rebuild) is the one that ran."""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from worldql_server_amd import abi, synth, synth_ext
+
+pytestmark = pytest.mark.gpu
+
+
+def mk_router(cube_size=16, hash_bits=64):
+    from worldql_server_amd.router import Router
+    return Router(cube_size, 0, hash_bits=hash_bits)
+
+
+def _check(r, o, pos, world, sender, repl):
+    got = r.route(pos, world, sender, repl)
+    want = o.route(pos, world, sender, repl)
+    assert (got[0] == want[0]).all()
+    assert (got[1] == want[1]).all()
+    st = r.stats()
+    e, c = o.counts()
+    assert st["n_entries"] == e and st["n_cubes"] == c
+    return len(got[1])
+
+
+def _random_ops(rng, n, worlds, peers, half, sub_frac):
+    return abi.ops_array(rng.integers(0, worlds, n).astype(np.uint32), rng.integers(0, peers, n).astype(np.uint32),
+                         np.where(rng.random(n) < sub_frac, abi.OP_SUBSCRIBE, abi.OP_UNSUBSCRIBE).astype(np.uint8),
+                         pos=rng.uniform(-half, half, (n, 3)))
+
+
+@pytest.mark.parametrize("hash_bits,f", [(64, 1.0), (6, 0.05)])
+def test_delta_random_churn_vs_oracle(hash_bits, f):
+    """Random sub / unsub batches (duplicates, unsubs of absent triples, new and emptied cubes,
+    lists that outgrow their capacity) — incremental every tick. hash_bits 6 puts every record
+    on one probe sequence (f scales the sizes down for it)."""
+    rng = np.random.default_rng(5 + hash_bits)
+    r, o = mk_router(hash_bits=hash_bits), orc.COracle(16)
+    half = 160.0 * f ** (1 / 3)
+    base = _random_ops(rng, int(60000 * f), 3, 4000, half, 1.0)
+    r.apply_ops(base)
+    o.apply_ops(base)
+    M = 4000
+    for tick in range(8):
+        # concentrated batches: a few hot cubes gain many peers (relocation), others churn
+        ops = _random_ops(rng, int(4000 * f), 3, 4500, half, 0.55)
+        nh = int(600 * f)
+        hot = abi.ops_array(np.zeros(nh, np.uint32), rng.integers(0, 4500, nh).astype(np.uint32),
+                            np.zeros(nh, np.uint8), pos=np.tile([[8.0 + 16 * tick, 8.0, 8.0]], (nh, 1)))
+        # re-issue some ops of this batch in reverse kind: last op wins per triple
+        nf = int(500 * f)
+        flip = ops[:nf].copy()
+        flip["kind"] = 1 - flip["kind"]
+        batch = abi.concat_ops([ops, hot, flip, ops[nf // 2:nf]])
+        r.apply_ops(batch)
+        o.apply_ops(batch)
+        pos = rng.uniform(-half - 10, half + 10, (M, 3))
+        pos[:200] = [8.0 + 16 * tick, 8.0, 8.0]
+        world = rng.integers(0, 4, M).astype(np.uint32)
+        sender = rng.integers(0, 4500, M).astype(np.uint32)
+        repl = rng.integers(0, 3, M).astype(np.uint8)
+        assert _check(r, o, pos, world, sender, repl) > 0
+    inc, fb = r.update_counts()
+    assert inc == 8 and fb == 0
+    # membership and any-sets after churn (regenerated from the records)
+    for w in range(4):
+        assert (r.world_peers(w) == o.world_peers(w)).all()
+    q = 3000
+    qw = rng.integers(0, 3, q).astype(np.uint32)
+    qp = rng.integers(0, 4500, q).astype(np.uint32)
+    qpos = rng.uniform(-half, half, (q, 3))
+    got = r.is_subscribed(qw, qp, False, qpos)
+    want = np.array([o.is_subscribed(int(a), int(b), False, c) for a, b, c in zip(qw, qp, qpos)])
+    assert (got == want).all()
+    got = r.is_subscribed_any(qw, qp)
+    want = np.array([o.is_subscribed_any(int(a), int(b)) for a, b in zip(qw, qp)])
+    assert (got == want).all()
+
+
+def test_delta_empty_and_revive_cubes():
+    """Cubes emptied by a batch keep a count-0 record; later batches revive them in place."""
+    r, o = mk_router(), orc.COracle(16)
+    peers = np.arange(4000, dtype=np.uint32)
+    cells = (peers % 200).astype(np.float64) * 16.0 + 8.0
+    pos = np.stack([cells, np.full(4000, 8.0), np.full(4000, 8.0)], 1)
+    base = abi.ops_array(np.zeros(4000, np.uint32), peers, np.zeros(4000, np.uint8), pos=pos)
+    r.apply_ops(base)
+    o.apply_ops(base)
+    mpos = np.stack([np.arange(200) * 16.0 + 8.0, np.full(200, 8.0), np.full(200, 8.0)], 1)
+    zeros = np.zeros(200, np.uint32)
+    sel = np.isin(peers % 200, np.arange(0, 200, 2))[:800]  # empty the even cells among peers < 800
+    for kind in (abi.OP_UNSUBSCRIBE, abi.OP_SUBSCRIBE):
+        b = abi.ops_array(np.zeros(800, np.uint32), peers[:800], np.full(800, kind, np.uint8), pos=pos[:800])
+        r.apply_ops(b)
+        o.apply_ops(b)
+        _check(r, o, mpos, zeros, np.arange(200, dtype=np.uint32), np.ones(200, np.uint8))
+    assert sel.any()
+    assert r.update_counts() == (2, 0)
+
+
+def test_delta_fallbacks_and_remove_peer():
+    """An irregular key in a small batch takes the rebuild; REMOVE_PEER after incremental
+    batches works from the regenerated state."""
+    rng = np.random.default_rng(9)
+    r, o = mk_router(), orc.COracle(16)
+    base = _random_ops(rng, 40000, 2, 3000, 128.0, 1.0)
+    r.apply_ops(base)
+    o.apply_ops(base)
+    M = 3000
+    args = lambda: (rng.uniform(-130, 130, (M, 3)), rng.integers(0, 2, M).astype(np.uint32),
+                    rng.integers(0, 3000, M).astype(np.uint32), rng.integers(0, 3, M).astype(np.uint8))
+    b = _random_ops(rng, 2000, 2, 3000, 128.0, 0.5)
+    r.apply_ops(b)
+    o.apply_ops(b)
+    _check(r, o, *args())
+    assert r.update_counts() == (1, 0)
+    # a raw off-grid key (not a multiple of the cube size) has no packed key: full rebuild
+    raw = abi.ops_array(np.zeros(3, np.uint32), np.array([1, 2, 3], np.uint32), np.zeros(3, np.uint8),
+                        key=np.array([[1, 2, 3], [16, 16, 17], [0, 0, 0]]))
+    b = abi.concat_ops([_random_ops(rng, 500, 2, 3000, 128.0, 0.5), raw])
+    r.apply_ops(b)
+    o.apply_ops(b)
+    _check(r, o, *args())
+    assert r.update_counts() == (1, 1)
+    # incremental again (the table now also holds full-key slot cubes), then REMOVE_PEER
+    b = _random_ops(rng, 1500, 2, 3000, 128.0, 0.5)
+    r.apply_ops(b)
+    o.apply_ops(b)
+    _check(r, o, *args())
+    assert r.update_counts() == (2, 1)
+    rm = abi.ops_array(np.full(40, abi.WORLD_INVALID, np.uint32), np.arange(0, 400, 10, dtype=np.uint32),
+                       np.full(40, abi.OP_REMOVE_PEER, np.uint8), pos=np.zeros((40, 3)))
+    r.apply_ops(rm)
+    o.apply_ops(rm)
+    _check(r, o, *args())
+    assert r.is_subscribed(np.zeros(1, np.uint32), np.array([1], np.uint32), True, np.array([[1, 2, 3]]))[0] == \
+        o.is_subscribed(0, 1, True, np.array([1, 2, 3]))
+
+
+def test_delta_list_space_exhaustion_rebuilds():
+    """Repeated growth of the same cubes relocates their lists until `list` runs out of room; the
+    batch that would overflow takes the rebuild, which compacts, and results stay exact."""
+    rng = np.random.default_rng(13)
+    r, o = mk_router(), orc.COracle(16)
+    base = _random_ops(rng, 30000, 1, 30000, 64.0, 1.0)
+    r.apply_ops(base)
+    o.apply_ops(base)
+    M = 2000
+    nxt = 30000
+    for tick in range(40):
+        n = 1500
+        peers = np.arange(nxt, nxt + n, dtype=np.uint32)
+        nxt += n
+        b = abi.ops_array(np.zeros(n, np.uint32), peers, np.zeros(n, np.uint8),
+                          pos=np.tile([[8.0, 8.0, 8.0], [24.0, 8.0, 8.0], [40.0, 8.0, 8.0]], (n // 3, 1)))
+        r.apply_ops(b)
+        o.apply_ops(b)
+        if tick % 8 == 7:
+            pos = rng.uniform(-64, 64, (M, 3))
+            pos[:30] = [8.0, 8.0, 8.0]
+            _check(r, o, pos, np.zeros(M, np.uint32), rng.integers(0, nxt, M).astype(np.uint32),
+                   rng.integers(0, 3, M).astype(np.uint8))
+    inc, fb = r.update_counts()
+    assert inc > 20 and fb >= 1
+
+
+def test_c4_scaled_churn_is_incremental():
+    c4 = synth_ext.config_c4(scale=0.02, worlds=range(0, 64, 8))
+    r, o = mk_router(), orc.COracle(16)
+    ops = c4.initial_ops()
+    r.apply_ops(ops)
+    o.apply_ops(ops)
+    for _ in range(5):
+        ops, pos, w, s, rp = c4.step()
+        r.apply_ops(ops)
+        o.apply_ops(ops)
+        rp = synth.stream(4, 3).below(3, len(w)).astype(np.uint8)
+        assert _check(r, o, pos, w, s, rp) > 0
+    assert r.update_counts() == (5, 0)
+    for wid in (0, 8, 56):
+        assert (r.world_peers(wid) == o.world_peers(wid)).all()

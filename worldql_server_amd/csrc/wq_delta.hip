@@ -1,0 +1,439 @@
+// wq_delta.hip — incremental subscribe / unsubscribe batches (SURVEY.md §8(d) C4 churn).
+//
+// Same semantics as the full rebuild in wq_table.hip — per (world, cube, peer) the last op of the
+// batch wins (AreaMap::add_subscription / remove_subscription, area_map.rs:72-119, applied in
+// order by thread.rs:122-146) — but the work is proportional to the batch and the cubes it
+// touches, not to the whole table:
+//   events   each op -> (packed cube key pk, peer, kind); an op whose cube has no packed key
+//            (raw off-grid keys, huge coordinates, world ids >= 1023) sends the batch to the rebuild
+//   sort     stable radix sort by (pk, peer): runs of one (cube, peer), the last op of a run wins
+//   plan     one lane per touched cube: find its record, merge-walk the cube's ascending list
+//            against its ascending changes, and count the effective adds and removes
+//   apply    one lane per changed cube: a list that still fits its capacity is edited in place
+//            (forward compaction of the removals, then a backward merge of the adds — both safe
+//            in place); a list that outgrows it moves to bump-allocated space past the used part
+//            of `list`, with 50% headroom; a new cube claims a record slot on its probe path.
+//            The record's count, list offset, capacity, Bloom signature and inline peers are
+//            rewritten from the final list.
+// A cube that empties keeps its record (count 0, key kept), so every probe sequence stays intact.
+// The sorted state `st` and the any-keys are left stale and regenerated from the records only
+// when something needs them (table_materialize / table_ensure_any): REMOVE_PEER, a full rebuild,
+// any-queries, GlobalMessage, stats. A batch falls back to the full rebuild (nothing changed) when
+// an op is not regular, the relocated lists would overflow `list`, or the record table would pass
+// load 1/4.
+#include <algorithm>
+
+#include "table_prims.hpp"
+
+namespace wq {
+
+namespace {
+
+struct DeltaSummary {
+    uint64_t d_entries;    // two's complement: adds - removes
+    uint64_t d_live;       // two's complement: cubes that became non-empty - cubes that emptied
+    uint64_t new_recs;     // records claimed
+    uint64_t reloc_words;  // list words to bump-allocate
+    uint32_t irregular;    // an op without a packed key
+    uint32_t n_dc;         // touched cubes
+};
+
+struct DeltaTable {
+    Record* recs;
+    uint32_t* rclaim;
+    uint64_t rmask;
+    int rshift;
+    uint64_t hmask;
+    uint32_t* list;
+};
+
+__device__ __forceinline__ void op_key(const wq_op& o, double sf, int64_t si, int64_t* k) {
+    if (o.key_is_raw) {  // impl ToCubeArea for CubeArea: identity (cube_area.rs:65-70)
+        k[0] = o.u.key[0];
+        k[1] = o.u.key[1];
+        k[2] = o.u.key[2];
+    } else {  // CubeArea::from_vector3 (cube_area.rs:50-56)
+        k[0] = coord_clamp_dev(o.u.pos[0], sf, si);
+        k[1] = coord_clamp_dev(o.u.pos[1], sf, si);
+        k[2] = coord_clamp_dev(o.u.pos[2], sf, si);
+    }
+}
+
+__global__ void k_delta_events(const wq_op* __restrict__ ops, uint32_t n, double sf, int64_t si, uint64_t* pk,
+                               uint32_t* peer, uint8_t* kind, DeltaSummary* sum) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const wq_op o = ops[i];
+    int64_t k[3];
+    op_key(o, sf, si, k);
+    uint64_t p = 0;
+    if (!pack_key(o.world, k[0], k[1], k[2], sf, &p)) atomicOr(&sum->irregular, 1u);
+    pk[i] = p;
+    peer[i] = o.peer;
+    kind[i] = o.kind == WQ_OP_SUBSCRIBE ? 1 : 0;
+}
+
+// Sorted order -> peer / kind columns and cube heads.
+__global__ void k_delta_mark(const uint32_t* __restrict__ order, const uint64_t* __restrict__ spk,
+                             const uint32_t* __restrict__ peer, const uint8_t* __restrict__ kind, uint32_t n,
+                             uint32_t* sp, uint8_t* skd, uint32_t* head) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t a = order[i];
+    sp[i] = peer[a];
+    skd[i] = kind[a];
+    head[i] = (i == 0 || spk[i] != spk[i - 1]) ? 1u : 0u;
+}
+
+__global__ void k_delta_cubes(const uint32_t* __restrict__ head, const uint32_t* __restrict__ cid, uint32_t n,
+                              uint32_t* cube_start, DeltaSummary* sum) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    if (head[i]) cube_start[cid[i] - 1] = i;
+    if (i == n - 1) {
+        sum->n_dc = cid[i];
+        cube_start[cid[i]] = n;
+    }
+}
+
+// Last index of the (cube, peer) run starting at t.
+__device__ __forceinline__ uint32_t run_last(const uint32_t* sp, uint32_t t, uint32_t s1) {
+    while (t + 1 < s1 && sp[t + 1] == sp[t]) ++t;
+    return t;
+}
+
+__device__ __forceinline__ uint32_t find_rec(const DeltaTable& tb, uint64_t pk) {
+    uint64_t i = slot_of(rec_hash(pk) & tb.hmask, tb.rshift);
+    for (;;) {
+        const uint64_t k = tb.recs[i].pk;
+        if (k == pk) return (uint32_t)i;
+        if (k == 0) return kNone;
+        i = (i + 1) & tb.rmask;
+    }
+}
+
+__device__ __forceinline__ uint32_t grown(uint32_t n) { return n + n / 2 + 4; }
+
+__global__ __launch_bounds__(kBlock) void k_delta_plan(DeltaTable tb, const uint32_t* __restrict__ cube_start,
+                                                       const uint64_t* __restrict__ spk,
+                                                       const uint32_t* __restrict__ sp,
+                                                       const uint8_t* __restrict__ skd, const DeltaSummary* sum,
+                                                       uint32_t n, uint4* plan, uint32_t* reloc, uint64_t* part) {
+    __shared__ unsigned long long acc[4];
+    if (threadIdx.x < 4) acc[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t n_dc = sum->n_dc;
+    uint32_t rw = 0;
+    if (c < n_dc) {
+        const uint32_t s0 = cube_start[c], s1 = cube_start[c + 1];
+        const uint64_t pk = spk[s0];
+        const uint32_t slot = find_rec(tb, pk);
+        uint32_t oc = 0, off = 0, cap = 0;
+        if (slot != kNone) {
+            const Record& r = tb.recs[slot];
+            oc = r.count;
+            off = r.list_off;
+            cap = r.unused[0];
+        }
+        const uint32_t* old = tb.list + off + 1;
+        uint32_t adds = 0, rms = 0, j = 0;
+        for (uint32_t t = s0; t < s1;) {
+            const uint32_t l = run_last(sp, t, s1);
+            const uint32_t q = sp[l];
+            while (j < oc && old[j] < q) ++j;
+            const bool present = j < oc && old[j] == q;
+            if (skd[l])
+                adds += present ? 0u : 1u;
+            else
+                rms += present ? 1u : 0u;
+            t = l + 1;
+        }
+        const uint32_t nc = oc + adds - rms;
+        const bool changed = (adds | rms) != 0;
+        if (changed && nc > cap) rw = 1 + grown(nc);
+        plan[c] = make_uint4(slot, nc, changed ? 1u : 0u, oc);
+        const int64_t de = (int64_t)adds - (int64_t)rms;
+        const int64_t dl = (int64_t)(oc == 0 && nc > 0) - (int64_t)(oc > 0 && nc == 0);
+        if (de) atomicAdd(&acc[0], (unsigned long long)de);
+        if (dl) atomicAdd(&acc[1], (unsigned long long)dl);
+        if (slot == kNone && nc > 0) atomicAdd(&acc[2], 1ull);
+        if (rw) atomicAdd(&acc[3], (unsigned long long)rw);
+    }
+    if (c < n) reloc[c] = rw;
+    __syncthreads();
+    if (threadIdx.x < 4) part[4ull * blockIdx.x + threadIdx.x] = acc[threadIdx.x];
+}
+
+__global__ __launch_bounds__(kBlock) void k_delta_reduce(const uint64_t* __restrict__ part, uint32_t nb,
+                                                         DeltaSummary* sum) {
+    __shared__ unsigned long long acc[4];
+    if (threadIdx.x < 4) acc[threadIdx.x] = 0;
+    __syncthreads();
+    unsigned long long v[4] = {0, 0, 0, 0};
+    for (uint32_t b = threadIdx.x; b < nb; b += kBlock)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] += part[4ull * b + k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (v[k]) atomicAdd(&acc[k], v[k]);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        sum->d_entries = acc[0];
+        sum->d_live = acc[1];
+        sum->new_recs = acc[2];
+        sum->reloc_words = acc[3];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_delta_apply(DeltaTable tb, const uint32_t* __restrict__ cube_start,
+                                                        const uint64_t* __restrict__ spk,
+                                                        const uint32_t* __restrict__ sp,
+                                                        const uint8_t* __restrict__ skd, const DeltaSummary* sum,
+                                                        const uint4* __restrict__ plan,
+                                                        const uint32_t* __restrict__ reloc,
+                                                        const uint32_t* __restrict__ reloc_off, uint64_t list_base) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= sum->n_dc) return;
+    const uint4 pl = plan[c];
+    if (!pl.z) return;
+    const uint32_t s0 = cube_start[c], s1 = cube_start[c + 1];
+    const uint64_t pk = spk[s0];
+    const uint32_t nc = pl.y, oc = pl.w;
+    uint64_t slot = pl.x;
+    uint32_t off = 0, cap = 0;
+    if (pl.x == kNone) {  // a new cube: the first unclaimed slot of its probe sequence
+        slot = slot_of(rec_hash(pk) & tb.hmask, tb.rshift);
+        while (atomicCAS(&tb.rclaim[slot], 0u, 1u) != 0u) slot = (slot + 1) & tb.rmask;
+    } else {
+        off = tb.recs[slot].list_off;
+        cap = tb.recs[slot].unused[0];
+    }
+    uint32_t* L = tb.list;
+    if (reloc[c]) {  // forward merge of the old list and the changes into new space
+        const uint32_t dst = (uint32_t)(list_base + reloc_off[c]);
+        const uint32_t* old = L + off + 1;
+        uint32_t* out = L + dst + 1;
+        uint32_t i = 0, w = 0, t = s0;
+        while (i < oc || t < s1) {
+            if (t < s1) {
+                const uint32_t l = run_last(sp, t, s1);
+                const uint32_t q = sp[l];
+                while (i < oc && old[i] < q) out[w++] = old[i++];
+                const bool present = i < oc && old[i] == q;
+                if (present) ++i;
+                if (skd[l]) out[w++] = q;  // subscribed after the batch (kept or added)
+                t = l + 1;
+            } else {
+                out[w++] = old[i++];
+            }
+        }
+        off = dst;
+        cap = reloc[c] - 1;
+    } else {  // in place: compact the removals forward, then merge the adds backward
+        uint32_t* a = L + off + 1;
+        uint32_t w = 0, t = s0;
+        for (uint32_t i = 0; i < oc; ++i) {
+            const uint32_t x = a[i];
+            while (t < s1 && sp[t] < x) t = run_last(sp, t, s1) + 1;
+            bool rm = false;
+            if (t < s1 && sp[t] == x) rm = skd[run_last(sp, t, s1)] == 0;
+            if (!rm) a[w++] = x;
+        }
+        int64_t i = (int64_t)w - 1;
+        uint32_t k = nc;
+        for (int64_t u = (int64_t)s1 - 1; u >= (int64_t)s0;) {
+            const uint32_t q = sp[u];
+            const bool sub = skd[u] != 0;  // u is the last op of its run
+            while (u >= (int64_t)s0 && sp[u] == q) --u;
+            if (!sub) continue;
+            while (i >= 0 && a[i] > q) a[--k] = a[i--];
+            if (i >= 0 && a[i] == q) continue;  // already subscribed
+            a[--k] = q;
+        }
+    }
+    L[off] = nc;
+    const uint32_t* a = L + off + 1;
+    uint64_t sig = 0;
+    for (uint32_t j = 0; j < nc; ++j) sig |= peer_sig(a[j]);
+    Record& r = tb.recs[slot];
+    r.pk = pk;
+    r.count = nc;
+    r.list_off = off;
+    r.sig = sig;
+    r.unused[0] = cap;
+    r.unused[1] = kNone;
+#pragma unroll 4
+    for (int j = 0; j < kInline; ++j) r.peers[j] = (uint32_t)j < nc ? a[j] : kNone;
+}
+
+// ---- materialize: the sorted-state arrays from the records and slots ---------------------------
+
+__device__ __forceinline__ void unpack_key(uint64_t pk, int64_t s, uint32_t* w, int64_t* k) {
+    *w = (uint32_t)(pk >> 54) - 1u;
+    k[0] = ((int64_t)((pk >> 36) & 0x3FFFFull) - (int64_t)kAxisBias) * s;
+    k[1] = ((int64_t)((pk >> 18) & 0x3FFFFull) - (int64_t)kAxisBias) * s;
+    k[2] = ((int64_t)(pk & 0x3FFFFull) - (int64_t)kAxisBias) * s;
+}
+
+__global__ void k_mat_count(const Record* __restrict__ recs, uint64_t rcap, const Slot* __restrict__ slots,
+                            uint64_t scap, const uint32_t* __restrict__ list, uint32_t* cnt) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < rcap) {
+        const uint4 h = *reinterpret_cast<const uint4*>(recs + i);
+        cnt[i] = (h.x | h.y) ? h.z : 0u;
+    } else if (i < rcap + scap) {
+        const SlotView s = load_slot(slots, i - rcap);
+        cnt[i] = s.world == kWorldEmpty ? 0u : list[s.off];
+    }
+}
+
+__global__ void k_mat_write(const Record* __restrict__ recs, uint64_t rcap, const Slot* __restrict__ slots,
+                            uint64_t scap, const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt,
+                            const uint32_t* __restrict__ pos, int64_t s, uint64_t hmask, uint64_t* st_h,
+                            uint32_t* st_w, int64_t* st_kx, int64_t* st_ky, int64_t* st_kz, uint32_t* st_p) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= rcap + scap) return;
+    const uint32_t n = cnt[i];
+    if (!n) return;
+    uint32_t w, off;
+    int64_t k[3];
+    if (i < rcap) {
+        const Record& r = recs[i];
+        unpack_key(r.pk, s, &w, k);
+        off = r.list_off;
+    } else {
+        const SlotView v = load_slot(slots, i - rcap);
+        w = v.world;
+        k[0] = v.k0;
+        k[1] = v.k1;
+        k[2] = v.k2;
+        off = v.off;
+    }
+    const uint64_t hh = cube_hash(w, k[0], k[1], k[2]) & hmask;
+    const uint32_t o = pos[i];
+    for (uint32_t j = 0; j < n; ++j) {
+        st_h[o + j] = hh;
+        st_w[o + j] = w;
+        st_kx[o + j] = k[0];
+        st_ky[o + j] = k[1];
+        st_kz[o + j] = k[2];
+        st_p[o + j] = list[off + 1 + j];
+    }
+}
+
+}  // namespace
+
+int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
+    *applied = false;
+    if (n_ops == 0) {
+        *applied = true;
+        return WQ_OK;
+    }
+    const uint32_t n = (uint32_t)n_ops;
+    DeltaWs& d = h->dws;
+    Table& t = h->tab;
+    hipStream_t s = h->stream;
+    const uint32_t nb = grid_for(n);
+    WQ_ALLOC(h, d.pk, (uint64_t)n * 8);
+    WQ_ALLOC(h, d.peer, (uint64_t)n * 4);
+    WQ_ALLOC(h, d.kind, n);
+    WQ_ALLOC(h, d.sp, (uint64_t)n * 4);
+    WQ_ALLOC(h, d.skd, n);
+    WQ_ALLOC(h, d.plan, (uint64_t)n * 16);
+    WQ_ALLOC(h, d.reloc, (uint64_t)n * 4);
+    WQ_ALLOC(h, d.reloc_off, (uint64_t)n * 4);
+    WQ_ALLOC(h, d.part, (uint64_t)nb * 32);
+    WQ_ALLOC(h, d.summ, sizeof(DeltaSummary));
+    WQ_ALLOC(h, h->idx_a, (uint64_t)n * 4);
+    WQ_ALLOC(h, h->idx_b, (uint64_t)n * 4);
+    WQ_ALLOC(h, h->key32_a, (uint64_t)n * 4);
+    WQ_ALLOC(h, h->key64_a, (uint64_t)n * 8);
+    WQ_ALLOC(h, h->key64_b, (uint64_t)n * 8);
+    WQ_ALLOC(h, h->flags, (uint64_t)n * 4);
+    WQ_ALLOC(h, h->scan, (uint64_t)n * 4);
+    WQ_ALLOC(h, h->cube_start, ((uint64_t)n + 1) * 4);
+    DeltaSummary* sum = d.summ.as<DeltaSummary>();
+    WQ_HIP(h, hipMemsetAsync(sum, 0, sizeof(DeltaSummary), s));
+    hipLaunchKernelGGL(k_delta_events, dim3(nb), dim3(kBlock), 0, s, h->d_ops.as<wq_op>(), n,
+                       (double)h->cube_size, (int64_t)h->cube_size, d.pk.as<uint64_t>(), d.peer.as<uint32_t>(),
+                       d.kind.as<uint8_t>(), sum);
+    // order = stable sort by (pk, peer): by peer, then stably by pk
+    uint32_t* idx_a = h->idx_a.as<uint32_t>();
+    uint32_t* idx_b = h->idx_b.as<uint32_t>();
+    hipLaunchKernelGGL(k_iota, dim3(nb), dim3(kBlock), 0, s, idx_a, (uint64_t)n);
+    int rc = sort_pairs<uint32_t>(h, d.peer.as<uint32_t>(), h->key32_a.as<uint32_t>(), idx_a, idx_b, n, 32);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_gather<uint64_t>, dim3(nb), dim3(kBlock), 0, s, d.pk.as<uint64_t>(), idx_b,
+                       h->key64_a.as<uint64_t>(), (uint64_t)n);
+    if ((rc = sort_pairs<uint64_t>(h, h->key64_a.as<uint64_t>(), h->key64_b.as<uint64_t>(), idx_b, idx_a, n, 64)))
+        return rc;
+    const uint64_t* spk = h->key64_b.as<uint64_t>();
+    uint32_t* head = h->flags.as<uint32_t>();
+    uint32_t* cid = h->scan.as<uint32_t>();
+    hipLaunchKernelGGL(k_delta_mark, dim3(nb), dim3(kBlock), 0, s, idx_a, spk, d.peer.as<uint32_t>(),
+                       d.kind.as<uint8_t>(), n, d.sp.as<uint32_t>(), d.skd.as<uint8_t>(), head);
+    if ((rc = scan_u32(h, head, cid, n, true))) return rc;
+    uint32_t* cube_start = h->cube_start.as<uint32_t>();
+    hipLaunchKernelGGL(k_delta_cubes, dim3(nb), dim3(kBlock), 0, s, head, cid, n, cube_start, sum);
+    DeltaTable tb{t.recs.as<Record>(), t.rclaim.as<uint32_t>(), t.rec_cap - 1, t.rec_shift, h->hash_mask,
+                  t.list.as<uint32_t>()};
+    hipLaunchKernelGGL(k_delta_plan, dim3(nb), dim3(kBlock), 0, s, tb, cube_start, spk, d.sp.as<uint32_t>(),
+                       d.skd.as<uint8_t>(), sum, n, d.plan.as<uint4>(), d.reloc.as<uint32_t>(),
+                       d.part.as<uint64_t>());
+    hipLaunchKernelGGL(k_delta_reduce, dim3(1), dim3(kBlock), 0, s, d.part.as<uint64_t>(), nb, sum);
+    if ((rc = scan_u32(h, d.reloc.as<uint32_t>(), d.reloc_off.as<uint32_t>(), n, false))) return rc;
+    WQ_HIP(h, hipGetLastError());
+    DeltaSummary hs;
+    WQ_HIP(h, hipMemcpyAsync(&hs, sum, sizeof(hs), hipMemcpyDeviceToHost, s));
+    WQ_HIP(h, hipStreamSynchronize(s));
+    const uint64_t list_limit = std::min<uint64_t>(t.list_cap, 0xFFFFFFFFull);
+    if (hs.irregular || t.list_used + hs.reloc_words > list_limit || 4 * (t.n_recs + hs.new_recs) > t.rec_cap) {
+        h->n_delta_fallbacks++;
+        return WQ_OK;  // nothing was modified: the caller rebuilds
+    }
+    hipLaunchKernelGGL(k_delta_apply, dim3(nb), dim3(kBlock), 0, s, tb, cube_start, spk, d.sp.as<uint32_t>(),
+                       d.skd.as<uint8_t>(), sum, d.plan.as<uint4>(), d.reloc.as<uint32_t>(),
+                       d.reloc_off.as<uint32_t>(), t.list_used);
+    WQ_HIP(h, hipGetLastError());
+    t.list_used += hs.reloc_words;
+    h->st.n = (uint64_t)((int64_t)h->st.n + (int64_t)hs.d_entries);
+    t.n_cubes = (uint64_t)((int64_t)t.n_cubes + (int64_t)hs.d_live);
+    t.n_recs += hs.new_recs;
+    h->st_stale = true;
+    h->any_stale = true;
+    h->n_delta_applies++;
+    *applied = true;
+    return WQ_OK;
+}
+
+int table_materialize(wq_router* h) {
+    if (!h->st_stale) return WQ_OK;
+    Table& t = h->tab;
+    hipStream_t s = h->stream;
+    const uint64_t D = t.rec_cap + t.cap;
+    if (D >= 0xFFFFFFFFull) return set_error(h, WQ_E_INVALID, "table too large to materialize");
+    WQ_ALLOC(h, h->flags, D * 4);
+    WQ_ALLOC(h, h->scan, D * 4);
+    uint32_t* cnt = h->flags.as<uint32_t>();
+    uint32_t* pos = h->scan.as<uint32_t>();
+    hipLaunchKernelGGL(k_mat_count, dim3(grid_for(D)), dim3(kBlock), 0, s, t.recs.as<Record>(), t.rec_cap,
+                       t.slots.as<Slot>(), t.cap, t.list.as<uint32_t>(), cnt);
+    int rc = scan_u32(h, cnt, pos, D, false);
+    if (rc) return rc;
+    uint32_t lp = 0, lc = 0;
+    if ((rc = read_u32(h, pos, D - 1, &lp))) return rc;
+    if ((rc = read_u32(h, cnt, D - 1, &lc))) return rc;
+    const uint64_t S = (uint64_t)lp + lc;
+    if (S != h->st.n) return set_error(h, WQ_E_HIP, "materialize: entry count disagrees with the table");
+    if ((rc = ensure_state(h, h->st, S))) return rc;
+    hipLaunchKernelGGL(k_mat_write, dim3(grid_for(D)), dim3(kBlock), 0, s, t.recs.as<Record>(), t.rec_cap,
+                       t.slots.as<Slot>(), t.cap, t.list.as<uint32_t>(), cnt, pos, (int64_t)h->cube_size,
+                       h->hash_mask, h->st.h.as<uint64_t>(), h->st.w.as<uint32_t>(), h->st.kx.as<int64_t>(),
+                       h->st.ky.as<int64_t>(), h->st.kz.as<int64_t>(), h->st.p.as<uint32_t>());
+    WQ_HIP(h, hipGetLastError());
+    h->st_stale = false;
+    return WQ_OK;
+}
+
+}  // namespace wq

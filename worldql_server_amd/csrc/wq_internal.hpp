@@ -52,11 +52,24 @@ struct Table {
     int rec_shift = 64;
     DevBuf slots;     // Slot[cap]: cubes without a packed key
     DevBuf claim;     // u32[cap] (build scratch)
-    DevBuf list;      // u32[n_entries + n_cubes]: per cube [count, peers...]
+    DevBuf list;      // u32 words: per cube [count, peers...] (+ room for relocated lists)
     DevBuf any;       // u64[n_any] sorted (world << 32 | peer)
     uint64_t cap = 0;
     int shift = 64;
     uint64_t n_cubes = 0, n_any = 0;
+    // incremental updates (wq_delta.hip): list words in use (lists are bump-allocated past the
+    // build's dense region when they outgrow their capacity) and record slots in use (including
+    // records whose cube emptied: they keep their key, count 0)
+    uint64_t list_used = 0, list_cap = 0, n_recs = 0;
+};
+
+// Scratch of the incremental update (wq_delta.hip).
+struct DeltaWs {
+    DevBuf pk, peer, kind;  // per op (u64, u32, u8)
+    DevBuf sp, skd;         // per op in (pk, peer, op) order: peer, kind
+    DevBuf plan;            // uint4 per delta cube {record slot, new count, changed, -}
+    DevBuf reloc, reloc_off;  // u32 per delta cube: words of a relocated list, their exclusive scan
+    DevBuf part, summ;      // per-block partial sums, the summary read back
 };
 
 // Route workspace, persistent across calls so a tick needs no memset: two counter slots (each
@@ -93,6 +106,11 @@ struct wq_router {
 
     wq::State st, st_next;
     wq::Table tab;
+    // After incremental updates the sorted state `st` and the any-keys are stale; they are
+    // regenerated from the records on demand (table_materialize / table_ensure_any).
+    bool st_stale = false, any_stale = false;
+    wq::DeltaWs dws;
+    uint64_t n_delta_applies = 0, n_delta_fallbacks = 0;
 
     // build scratch
     wq::DevBuf ev_h, ev_w, ev_kx, ev_ky, ev_kz, ev_p, ev_kind, d_ops;
@@ -139,6 +157,13 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n);
 // keys: sorted unique (world << 32 | peer); world == WQ_WORLD_INVALID removes the peer everywhere.
 int table_remove_peers(wq_router* h, const uint64_t* keys_sorted_unique, size_t n);
 int table_rebuild_derived(wq_router* h);
+// wq_delta.hip. Applies n subscribe / unsubscribe ops (already in h->d_ops) to the records and lists
+// in place; *applied = false (and nothing changed) when the batch needs the full rebuild.
+int table_apply_delta(wq_router* h, size_t n, bool* applied);
+// Regenerates `st` (grouped by cube, peers ascending) from the records, slots and lists.
+int table_materialize(wq_router* h);
+// Rebuilds the any-keys if incremental updates left them stale.
+int table_ensure_any(wq_router* h);
 int set_error(wq_router* h, int code, const char* what, hipError_t e = hipSuccess);
 }  // namespace wq
 

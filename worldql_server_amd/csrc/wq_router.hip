@@ -126,7 +126,9 @@ int wq_router_destroy(wq_router* h) {
                       &h->key64_b, &h->flags, &h->scan, &h->sort_tmp, &h->small, &h->cube_id,
                       &h->cube_start, &h->rws.buf, &h->rws.info, &h->rws.e, &h->rws.tiles,
                       &h->h_in, &h->h_out, &h->tab.recs, &h->tab.rclaim, &h->shard_hist,
-                      &h->rec_keys, &h->rec_w, &h->rec_s, &h->rec_r};
+                      &h->rec_keys, &h->rec_w, &h->rec_s, &h->rec_r, &h->ppos, &h->rws.agg,
+                      &h->dws.pk, &h->dws.peer, &h->dws.kind, &h->dws.sp, &h->dws.skd, &h->dws.plan,
+                      &h->dws.reloc, &h->dws.reloc_off, &h->dws.part, &h->dws.summ};
     for (DevBuf* b : bufs) b->release();
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -143,6 +145,9 @@ int wq_set_stream(wq_router* h, void* stream) {
 
 int wq_get_stats(wq_router* h, wq_stats* out) {
     if (!h || !out) return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    int rc = table_ensure_any(h);
+    if (rc) return rc;
     out->n_entries = h->st.n;
     out->n_cubes = h->tab.n_cubes;
     out->n_any = h->tab.n_any;
@@ -182,6 +187,13 @@ int wq_set_radius(wq_router* h, double radius) {
 int wq_debug_set_route_config(wq_router* h, int cfg) {
     if (!h || cfg < 0 || cfg >= route_config_count()) return WQ_E_INVALID;
     h->route_cfg = cfg;
+    return WQ_OK;
+}
+
+int wq_debug_update_counts(wq_router* h, uint64_t* incremental, uint64_t* rebuild_fallbacks) {
+    if (!h || !incremental || !rebuild_fallbacks) return WQ_E_INVALID;
+    *incremental = h->n_delta_applies;
+    *rebuild_fallbacks = h->n_delta_fallbacks;
     return WQ_OK;
 }
 
@@ -297,7 +309,9 @@ int wq_route_global_device(wq_router* h, const uint32_t* d_world, const uint32_t
     if (n_msgs >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
     if (capacity > 0xFFFFFFFFull) capacity = 0xFFFFFFFFull;
     WQ_HIP(h, hipSetDevice(h->device));
-    int rc = launch_route_global(h, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs, capacity);
+    int rc = table_ensure_any(h);
+    if (rc) return rc;
+    rc = launch_route_global(h, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs, capacity);
     if (rc) return rc;
     if (d_counters)
         WQ_HIP(h, hipMemcpyAsync(d_counters, h->rws.last, sizeof(wq_route_counters), hipMemcpyDeviceToDevice,
@@ -311,6 +325,8 @@ int wq_route_global(wq_router* h, const uint32_t* world, const uint32_t* sender,
         return WQ_E_INVALID;
     if (M >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
     WQ_HIP(h, hipSetDevice(h->device));
+    int rc0 = table_ensure_any(h);
+    if (rc0) return rc0;
     const size_t o_w = 0, o_s = align256(M * 4), o_r = align256(o_s + M * 4), n_in = align256(o_r + M + 1);
     WQ_ALLOC(h, h->h_in, n_in);
     char* din = h->h_in.as<char>();
@@ -401,6 +417,8 @@ int wq_is_subscribed_any(wq_router* h, size_t n, const uint32_t* world, const ui
     if (n == 0) return WQ_OK;
     if (n >= 0xFFFFFFFFull) return WQ_E_INVALID;
     WQ_HIP(h, hipSetDevice(h->device));
+    int rc0 = table_ensure_any(h);
+    if (rc0) return rc0;
     const size_t o_w = 0, o_p = align256(n * 4), o_o = align256(o_p + n * 4);
     WQ_ALLOC(h, h->h_in, o_o + n);
     char* d = h->h_in.as<char>();
@@ -418,6 +436,8 @@ int wq_is_subscribed_any(wq_router* h, size_t n, const uint32_t* world, const ui
 int wq_world_peers(wq_router* h, uint32_t world, uint32_t* out, size_t capacity, size_t* n_out) {
     if (!h || !n_out || (capacity && !out)) return WQ_E_INVALID;
     WQ_HIP(h, hipSetDevice(h->device));
+    int rc0 = table_ensure_any(h);
+    if (rc0) return rc0;
     WQ_ALLOC(h, h->small, 64);
     hipStream_t s = h->stream;
     int rc = launch_world_range(h, world, h->small.as<uint64_t>());

@@ -20,17 +20,11 @@
 // kernel in this file.
 #include <cstring>
 
-#include <rocprim/rocprim.hpp>
-
-#include "wq_internal.hpp"
+#include "table_prims.hpp"
 
 namespace wq {
 
 namespace {
-
-constexpr int kBlock = 256;
-
-inline unsigned grid_for(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 __global__ void k_ops_to_events(const wq_op* __restrict__ ops, uint32_t n, uint64_t base,
                                 double sf, int64_t si, uint64_t hmask, uint64_t* ev_h,
@@ -62,18 +56,6 @@ __global__ void k_ops_to_events(const wq_op* __restrict__ ops, uint32_t n, uint6
 __global__ void k_fill_u8(uint8_t* a, uint64_t n, uint8_t v) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i < n) a[i] = v;
-}
-
-__global__ void k_iota(uint32_t* a, uint64_t n) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) a[i] = (uint32_t)i;
-}
-
-template <typename T>
-__global__ void k_gather(const T* __restrict__ src, const uint32_t* __restrict__ idx, T* dst,
-                         uint64_t n) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) dst[i] = src[idx[i]];
 }
 
 struct EvView {
@@ -175,7 +157,8 @@ __global__ void k_insert_cubes(EvView st, const uint32_t* __restrict__ cube_star
         uint64_t sig = 0;
         for (uint32_t i = 0; i < cnt; ++i) sig |= peer_sig(st.p[j + i]);
         r.sig = sig;
-        r.unused[0] = r.unused[1] = 0xFFFFFFFFu;
+        r.unused[0] = cnt;  // list capacity: the build packs lists densely
+        r.unused[1] = 0xFFFFFFFFu;
 #pragma unroll 2
         for (int i = 0; i < kInline; ++i) r.peers[i] = (uint32_t)i < cnt ? st.p[j + i] : 0xFFFFFFFFu;
         return;
@@ -222,53 +205,6 @@ __global__ void k_keep_not_removed(const uint32_t* __restrict__ st_w, const uint
     keep[i] = gone ? 0u : 1u;
 }
 
-// ---- rocPRIM wrappers (temp storage in h->sort_tmp) ----
-
-template <typename K>
-int sort_pairs(wq_router* h, const K* kin, K* kout, const uint32_t* vin, uint32_t* vout, uint64_t n,
-               int end_bit) {
-    size_t bytes = 0;
-    WQ_HIP(h, rocprim::radix_sort_pairs(nullptr, bytes, kin, kout, vin, vout, (size_t)n, 0, end_bit,
-                                        h->stream));
-    WQ_ALLOC(h, h->sort_tmp, bytes);
-    WQ_HIP(h, rocprim::radix_sort_pairs(h->sort_tmp.p, bytes, kin, kout, vin, vout, (size_t)n, 0,
-                                        end_bit, h->stream));
-    return WQ_OK;
-}
-
-int sort_keys_u64(wq_router* h, const uint64_t* kin, uint64_t* kout, uint64_t n) {
-    size_t bytes = 0;
-    WQ_HIP(h, rocprim::radix_sort_keys(nullptr, bytes, kin, kout, (size_t)n, 0, 64, h->stream));
-    WQ_ALLOC(h, h->sort_tmp, bytes);
-    WQ_HIP(h, rocprim::radix_sort_keys(h->sort_tmp.p, bytes, kin, kout, (size_t)n, 0, 64, h->stream));
-    return WQ_OK;
-}
-
-int scan_u32(wq_router* h, const uint32_t* in, uint32_t* out, uint64_t n, bool inclusive) {
-    size_t bytes = 0;
-    if (inclusive) {
-        WQ_HIP(h, rocprim::inclusive_scan(nullptr, bytes, in, out, (size_t)n, rocprim::plus<uint32_t>(),
-                                          h->stream));
-        WQ_ALLOC(h, h->sort_tmp, bytes);
-        WQ_HIP(h, rocprim::inclusive_scan(h->sort_tmp.p, bytes, in, out, (size_t)n,
-                                          rocprim::plus<uint32_t>(), h->stream));
-    } else {
-        WQ_HIP(h, rocprim::exclusive_scan(nullptr, bytes, in, out, 0u, (size_t)n,
-                                          rocprim::plus<uint32_t>(), h->stream));
-        WQ_ALLOC(h, h->sort_tmp, bytes);
-        WQ_HIP(h, rocprim::exclusive_scan(h->sort_tmp.p, bytes, in, out, 0u, (size_t)n,
-                                          rocprim::plus<uint32_t>(), h->stream));
-    }
-    return WQ_OK;
-}
-
-// n-th element of a device u32 array (synchronous read; build path only).
-int read_u32(wq_router* h, const uint32_t* a, uint64_t i, uint32_t* out) {
-    WQ_HIP(h, hipMemcpyAsync(out, a + i, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
-    WQ_HIP(h, hipStreamSynchronize(h->stream));
-    return WQ_OK;
-}
-
 EvView ev_view(wq_router* h) {
     return EvView{h->ev_h.as<uint64_t>(), h->ev_w.as<uint32_t>(), h->ev_kx.as<int64_t>(),
                   h->ev_ky.as<int64_t>(), h->ev_kz.as<int64_t>(), h->ev_p.as<uint32_t>()};
@@ -278,16 +214,6 @@ EvView st_view(const State& s) {
                   s.kz.as<int64_t>(), s.p.as<uint32_t>()};
 }
 
-int ensure_state(wq_router* h, State& s, uint64_t n) {
-    const uint64_t m = n ? n : 1;
-    WQ_ALLOC(h, s.h, m * 8);
-    WQ_ALLOC(h, s.w, m * 4);
-    WQ_ALLOC(h, s.kx, m * 8);
-    WQ_ALLOC(h, s.ky, m * 8);
-    WQ_ALLOC(h, s.kz, m * 8);
-    WQ_ALLOC(h, s.p, m * 4);
-    return WQ_OK;
-}
 
 // Stable LSD sort of `order` by one key column (gathered through the current order).
 template <typename K>
@@ -304,6 +230,8 @@ int refine_by(wq_router* h, const K* column, uint64_t n, int bits) {
 }
 
 }  // namespace
+
+int build_any(wq_router* h);
 
 int set_error(wq_router* h, int code, const char* what, hipError_t e) {
     if (h) {
@@ -342,6 +270,14 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops) {
 
     hipStream_t s = h->stream;
     WQ_HIP(h, hipMemcpyAsync(h->d_ops.p, ops, n_ops * sizeof(wq_op), hipMemcpyHostToDevice, s));
+    int rc;
+    // small batches against a built table: update the touched cubes in place (wq_delta.hip)
+    if (S && h->tab.n_cubes && 4 * n_ops <= S) {
+        bool applied = false;
+        if ((rc = table_apply_delta(h, n_ops, &applied))) return rc;
+        if (applied) return WQ_OK;
+    }
+    if (h->st_stale && (rc = table_materialize(h))) return rc;
     // live entries first: they are the earliest "present" events
     if (S) {
         WQ_HIP(h, hipMemcpyAsync(h->ev_h.p, h->st.h.p, S * 8, hipMemcpyDeviceToDevice, s));
@@ -364,7 +300,7 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops) {
     uint32_t* idx_a = h->idx_a.as<uint32_t>();
     uint32_t* idx_b = h->idx_b.as<uint32_t>();
     hipLaunchKernelGGL(k_iota, dim3(grid_for(N)), dim3(kBlock), 0, s, idx_a, N);
-    int rc = sort_pairs<uint32_t>(h, h->ev_p.as<uint32_t>(), h->key32_a.as<uint32_t>(), idx_a, idx_b, N, 32);
+    rc = sort_pairs<uint32_t>(h, h->ev_p.as<uint32_t>(), h->key32_a.as<uint32_t>(), idx_a, idx_b, N, 32);
     if (rc) return rc;
     hipLaunchKernelGGL(k_gather<uint64_t>, dim3(grid_for(N)), dim3(kBlock), 0, s, h->ev_h.as<uint64_t>(),
                        idx_b, h->key64_a.as<uint64_t>(), N);
@@ -417,6 +353,10 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops) {
 int table_remove_peers(wq_router* h, const uint64_t* keys, size_t n_rm) {
     const uint64_t S = h->st.n;
     if (S == 0 || n_rm == 0) return WQ_OK;
+    if (h->st_stale) {
+        int rc0 = table_materialize(h);
+        if (rc0) return rc0;
+    }
     hipStream_t s = h->stream;
     WQ_ALLOC(h, h->key32_b, n_rm * 8);
     WQ_ALLOC(h, h->flags, S * 4);
@@ -463,7 +403,8 @@ int table_rebuild_derived(wq_router* h) {
         WQ_ALLOC(h, h->cube_start, ((uint64_t)n_cubes + 1) * 4);
         hipLaunchKernelGGL(k_cube_start, dim3(grid_for(S)), dim3(kBlock), 0, s, head, cid, S, n_cubes,
                            h->cube_start.as<uint32_t>());
-        WQ_ALLOC(h, t.list, (S + n_cubes) * 4);
+        // dense lists, plus room for lists that incremental updates relocate (wq_delta.hip)
+        WQ_ALLOC(h, t.list, ((S + n_cubes) * 3 / 2 + 65536) * 4);
         hipLaunchKernelGGL(k_fill_lists, dim3(grid_for(S)), dim3(kBlock), 0, s, h->st.p.as<uint32_t>(), head,
                            cid, h->cube_start.as<uint32_t>(), S, t.list.as<uint32_t>());
     } else {
@@ -502,8 +443,22 @@ int table_rebuild_derived(wq_router* h) {
                            rcap - 1, t.rec_shift, t.claim.as<uint32_t>(), t.slots.as<Slot>(), cap - 1, t.shift,
                            h->hash_mask, (double)h->cube_size);
     t.n_cubes = n_cubes;
+    t.n_recs = n_cubes;
+    t.list_used = S ? S + n_cubes : 0;
+    t.list_cap = t.list.bytes / 4;
+    h->st_stale = false;
+    if ((rc = build_any(h))) return rc;
+    WQ_HIP(h, hipGetLastError());
+    WQ_HIP(h, hipStreamSynchronize(s));
+    return WQ_OK;
+}
 
-    // sorted unique (world << 32 | peer)
+// Sorted unique (world << 32 | peer) keys from the (fresh) state.
+int build_any(wq_router* h) {
+    hipStream_t s = h->stream;
+    const uint64_t S = h->st.n;
+    Table& t = h->tab;
+    int rc;
     t.n_any = 0;
     if (S) {
         WQ_ALLOC(h, h->key64_a, S * 8);
@@ -526,8 +481,17 @@ int table_rebuild_derived(wq_router* h) {
     } else {
         WQ_ALLOC(h, t.any, 8);
     }
+    h->any_stale = false;
+    return WQ_OK;
+}
+
+int table_ensure_any(wq_router* h) {
+    if (!h->any_stale) return WQ_OK;
+    int rc;
+    if (h->st_stale && (rc = table_materialize(h))) return rc;
+    if ((rc = build_any(h))) return rc;
     WQ_HIP(h, hipGetLastError());
-    WQ_HIP(h, hipStreamSynchronize(s));
+    WQ_HIP(h, hipStreamSynchronize(h->stream));
     return WQ_OK;
 }
 
