@@ -40,15 +40,22 @@ METRIC = "routed msg→peer pairs/sec per tick at 1/2/4/8 GPUs; % HBM roofline"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
+                    help="c2 = the headline (BASELINE.json configs[1]); c3/c4/c5 = SURVEY.md §8(d)")
+    ap.add_argument("--steps", type=int, default=None, help="timed ticks (default 50; c4 20, c3/c5 10)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed ticks (default 10; c3/c4/c5 2)")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink C2 (tests only; 1.0 = the headline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline's routing work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shard", choices=["world", "cube"], default="world",
                     help="multi-GPU partitioning (see module docstring)")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "r01_pmc_route.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.steps is None:
+        a.steps = {"c2": 50, "c3": 10, "c4": 20, "c5": 10}[a.config]
+    if a.warmup is None:
+        a.warmup = 10 if a.config == "c2" else 2
+    return a
 
 
 def algorithmic_bytes(M: int, F: int, P: int) -> int:
@@ -127,6 +134,9 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
+    if a.config != "c2":
+        import bench_configs
+        return bench_configs.run(a, rank, world_size, local_rank, dev)
     if a.shard == "cube":
         return run_cube(a, rank, world_size, local_rank, dev)
 
@@ -230,7 +240,7 @@ def main():
         },
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "route tick (count + tile_scan + emit)", "kernel_avg_us": k_avg_s * 1e6,
+                     "kernel": "route tick (single launch: tick_kernel)", "kernel_avg_us": k_avg_s * 1e6,
                      "algorithmic_bytes": B},
     }
     if rank == 0 and world_size == 1 and not a.no_cpu_baseline:

@@ -1,0 +1,392 @@
+"""bench.py --config c3 | c4 | c5: the SURVEY.md §8(d) configurations past the headline.
+
+Every mode prints one JSON line in bench.py's format (metric = routed pairs/s; value = all ranks'
+pairs over the max-over-ranks time of the timed ticks). Inputs are generated and uploaded before
+the timed region; a tick's timed work is everything the tick does on the GPU.
+
+  c3  1M peers x 3x3x3 (S = 27M), 10M messages/tick, 90% from 256 Zipf-weighted Gaussian hotspots.
+      N = 1: the whole configuration on one GPU. N > 1: strong scaling through the cube-hash sharded
+      path (worldql_server_amd/sharded.py; every rank ingests M/N messages, RCCL all-to-all).
+  c4  8 worlds x 50k peers per GPU (weak scaling; 8 GPUs = the 64 worlds of C4, world-sharded, no
+      message exchange). A tick = that tick's AreaUnsubscribe/AreaSubscribe churn (5% of peers move
+      by N(0,16)^3) applied incrementally on the device (wq_apply_ops_device), then one message per
+      peer at its new position (ExceptSelf).
+  c5  1M entities moving U[-4,4)^3 per tick in U[-1024,1024)^3, 3x3x3 subscriptions, one message
+      each; a tick = the subscription diff of the move (incremental), the new peer positions, and the
+      route with the exact radius filter r = 16. One GPU (N > 1 is not implemented for c5 yet).
+"""
+from __future__ import annotations
+
+import json
+import time
+
+import numpy as np
+
+import bench
+from bench import HBM_PEAK_GBS, METRIC, algorithmic_bytes, reduce_over_ranks
+
+
+def run(a, rank, world_size, local_rank, dev):
+    return {"c3": run_c3, "c4": run_c4, "c5": run_c5}[a.config](a, rank, world_size, local_rank, dev)
+
+
+def _emit(out, rank):
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def _line(a, world_size, value, ms_per_step, scaling, workload, config, roofline, data):
+    return {"metric": METRIC, "value": value, "unit": "pairs/s", "n_gpus": world_size, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": scaling,
+            "vs_baseline": None, "dtype": "f64", "data": data,
+            "config": {"workload": workload, **config}, "roofline": roofline}
+
+
+def _counters(cnt):
+    from worldql_server_amd import abi
+    return cnt.cpu().numpy().view(abi.COUNTERS_DTYPE)
+
+
+# ---- C3 ---------------------------------------------------------------------------------------
+
+def run_c3(a, rank, world_size, local_rank, dev):
+    import torch
+    from worldql_server_amd import synth_ext
+    from worldql_server_amd.router import Router
+
+    t0 = time.perf_counter()
+    w = synth_ext.config_c3(scale=a.scale)
+    gen_s = time.perf_counter() - t0
+    if world_size > 1:
+        return _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s)
+    M = len(w.world)
+    r = Router(w.cube_size, local_rank)
+    stream = torch.cuda.Stream(device=dev)
+    r.set_stream(stream.cuda_stream)
+    t0 = time.perf_counter()
+    r.apply_ops(w.ops)
+    build_s = time.perf_counter() - t0
+    st = r.stats()
+    pos = torch.from_numpy(w.pos).to(dev)
+    world = torch.from_numpy(w.world.view(np.int32)).to(dev)
+    sender = torch.from_numpy(w.sender.view(np.int32)).to(dev)
+    repl = torch.from_numpy(w.repl).to(dev)
+    offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    r.route_device(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
+                   0, 0, 0, cnt.data_ptr())
+    torch.cuda.synchronize(dev)
+    P = int(_counters(cnt)["n_pairs"][0])
+    cap = P + 1024
+    peers = torch.empty(cap, dtype=torch.int32, device=dev)
+    msgs = torch.empty(cap, dtype=torch.int32, device=dev)
+    args = (pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
+            peers.data_ptr(), msgs.data_ptr(), cap)
+    for _ in range(a.warmup):
+        r.route_device(*args, 0)
+    r.route_device(*args, cnt.data_ptr())
+    torch.cuda.synchronize(dev)
+    c = _counters(cnt)[0]
+    P, F = int(c["n_pairs"]), int(c["n_candidates"])
+    assert c["overflow"] == 0 and c["error"] == 0, c
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(a.steps):
+        r.route_device(*args, 0)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    t_ms = ev0.elapsed_time(ev1)
+    r.profile_enable(True)
+    for _ in range(a.steps):
+        r.route_device(*args, 0)
+    k_ms, launches = r.profile_read()
+    r.profile_enable(False)
+    k_avg_s = k_ms / launches / 1e3
+    B = algorithmic_bytes(M, F, P)
+    out = _line(a, 1, P * a.steps / (t_ms / 1e3), t_ms / a.steps, "strong",
+                "C3: 1M peers x 3x3x3, 10M LocalMessages/tick, 256 Zipf(1) Gaussian hotspots (sigma 128) + 10% "
+                "uniform in U[-4096,4096)^3, cube_size 16, ExceptSelf, whole configuration on one GPU"
+                + ("" if a.scale == 1.0 else f" (scaled {a.scale})"),
+                {"messages_per_tick": M, "peers": w.n_peers, "subscriptions": int(st["n_entries"]),
+                 "cubes": int(st["n_cubes"]), "pairs_per_tick": P, "candidates_per_tick": F,
+                 "parallelism": "1 GPU", "table_build_s": round(build_s, 3), "generate_s": round(gen_s, 1)},
+                {"bound": "hbm", "achieved": B / k_avg_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": B / k_avg_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                 "kernel": "route tick (single launch: tick_kernel)", "kernel_avg_us": k_avg_s * 1e6,
+                 "algorithmic_bytes": B},
+                "synthetic (splitmix64, SURVEY.md §8(d) C3 generator)")
+    if not a.no_cpu_baseline:
+        out["cpu_baseline"] = _cpu_route_sample(w, a.cpu_seconds, "C3")
+    _emit(out, rank)
+    r.close()
+
+
+def _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s):
+    import torch
+    import torch.distributed as dist
+    from worldql_server_amd.router import Router
+    from worldql_server_amd.sharded import DeviceShard, DistExchange, ShardedRouter
+
+    M_all = len(w.world)
+    lo, hi = rank * M_all // world_size, (rank + 1) * M_all // world_size
+    stream = torch.cuda.Stream(device=dev)
+    r = Router(w.cube_size, local_rank)
+    be = DeviceShard(r, stream)
+    sr = ShardedRouter(be, DistExchange())
+    t0 = time.perf_counter()
+    sr.apply_ops(w.ops)
+    build_s = time.perf_counter() - t0
+    st = r.stats()
+    with torch.cuda.stream(stream):
+        pos = torch.from_numpy(w.pos[lo:hi]).to(dev)
+        world = torch.from_numpy(w.world[lo:hi].view(np.int32)).to(dev)
+        sender = torch.from_numpy(w.sender[lo:hi].view(np.int32)).to(dev)
+        repl = torch.from_numpy(w.repl[lo:hi]).to(dev)
+        for _ in range(max(a.warmup, 1)):
+            res = sr.tick(world, sender, repl, pos=pos)
+        stream.synchronize()
+        P_in = int(res.peers.shape[0])
+        P_own, F_own = be.read_counters()
+        R = sr.last_recv
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t_wall = time.perf_counter()
+        for _ in range(a.steps):
+            res = sr.tick(world, sender, repl, pos=pos)
+        torch.cuda.synchronize(dev)
+        t_ms = (time.perf_counter() - t_wall) * 1e3
+        dist.barrier()
+        t_max_ms, pairs_all = reduce_over_ranks(t_ms, P_in, dev, world_size)
+        r.profile_enable(True)
+        for _ in range(a.steps):
+            sr.tick(world, sender, repl, pos=pos)
+        k_ms, launches = r.profile_read()
+        r.profile_enable(False)
+    k_avg_s = k_ms / launches / 1e3
+    B = algorithmic_bytes(R, F_own, P_own)
+    out = _line(a, world_size, pairs_all * a.steps / (t_max_ms / 1e3), t_max_ms / a.steps, "strong",
+                f"C3 over {world_size} GPUs by cube hash: 1M peers x 3x3x3, 10M LocalMessages/tick in total, "
+                "256 Zipf(1) Gaussian hotspots + 10% uniform, cube_size 16, ExceptSelf"
+                + ("" if a.scale == 1.0 else f" (scaled {a.scale})"),
+                {"messages_per_tick": M_all, "messages_per_gpu": hi - lo, "peers": w.n_peers,
+                 "subscriptions_this_shard": int(st["n_entries"]), "pairs_per_tick": int(pairs_all),
+                 "parallelism": f"cube-hash x{world_size} (RCCL all-to-all)", "table_build_s": round(build_s, 3),
+                 "generate_s": round(gen_s, 1)},
+                {"bound": "hbm", "achieved": B / k_avg_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": B / k_avg_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                 "kernel": "route tick on rank 0's shard", "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
+                "synthetic (splitmix64, SURVEY.md §8(d) C3 generator)")
+    _emit(out, rank)
+    r.close()
+    dist.destroy_process_group()
+
+
+def _cpu_route_sample(w, seconds, name):
+    """The C restatement on 1 host thread, routing a bounded prefix of the tick's messages."""
+    from oracle import oracle as orc
+    o = orc.COracle(w.cube_size)
+    t0 = time.perf_counter()
+    o.apply_ops(w.ops)
+    build_s = time.perf_counter() - t0
+    M = len(w.world)
+    chunk = min(M, 50_000)
+    pairs = msgs = 0
+    t_route = 0.0
+    start = 0
+    while t_route < seconds and start < M:
+        sl = slice(start, start + chunk)
+        t0 = time.perf_counter()
+        _, peers, _ = o.route(w.pos[sl], w.world[sl], w.sender[sl], w.repl[sl])
+        t_route += time.perf_counter() - t0
+        pairs += len(peers)
+        msgs += len(w.world[sl])
+        start += chunk
+    return {"value": pairs / t_route, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"{name}: {msgs} of the tick's {M} messages ({pairs} pairs) routed in {t_route:.2f} s by "
+                      f"oracle/wq_oracle.c on 1 host thread; table of {len(w.ops)} subscriptions built in "
+                      f"{build_s:.1f} s (not timed)"}
+
+
+# ---- C4 / C5: churn ticks ----------------------------------------------------------------------
+
+def _ops_tensor(ops, dev):
+    import torch
+    raw = np.ascontiguousarray(ops).view(np.uint8)
+    return torch.from_numpy(raw.copy()).to(dev)
+
+
+def _churn_ticks(a, r, dev, stream, ticks, M, world_t, sender_t, repl_t, positions=False):
+    """Runs the pregenerated ticks (ops, pos) through update + route; returns per-phase timings."""
+    import torch
+    ops_d = [_ops_tensor(t[0], dev) for t in ticks]
+    n_ops = [len(t[0]) for t in ticks]
+    pos_d = [torch.from_numpy(t[1]).to(dev) for t in ticks]
+    offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    cap = 80 * M + 1024
+    peers = torch.empty(cap, dtype=torch.int32, device=dev)
+    msgs = torch.empty(cap, dtype=torch.int32, device=dev)
+    cnt = torch.zeros((len(ticks), 24), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+
+    def one(i, c):
+        r.apply_ops_device(ops_d[i].data_ptr(), n_ops[i])
+        if positions:
+            r.set_peer_positions_device(pos_d[i].data_ptr(), M)
+        r.route_device(pos_d[i].data_ptr(), world_t.data_ptr(), sender_t.data_ptr(), repl_t.data_ptr(), M,
+                       offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap, c)
+
+    for i in range(a.warmup):
+        one(i, cnt[i].data_ptr())
+    torch.cuda.synchronize(dev)
+    upd0, _ = r.update_counts()
+    r.profile_enable(True)
+    t0 = time.perf_counter()
+    for i in range(a.warmup, a.warmup + a.steps):
+        one(i, cnt[i].data_ptr())
+    torch.cuda.synchronize(dev)
+    t_ms = (time.perf_counter() - t0) * 1e3
+    k_ms, launches = r.profile_read()
+    r.profile_enable(False)
+    upd1, fb = r.update_counts()
+    c = _counters(cnt)[a.warmup:]
+    assert (c["overflow"] == 0).all() and (c["error"] == 0).all()
+    return {"t_ms": t_ms, "route_ms": k_ms, "launches": launches, "P": int(c["n_pairs"].sum()),
+            "F": int(c["n_candidates"].sum()), "ops": int(sum(n_ops[a.warmup:])),
+            "incremental": upd1 - upd0, "fallbacks": fb}
+
+
+def run_c4(a, rank, world_size, local_rank, dev):
+    import torch
+    import torch.distributed as dist
+    from worldql_server_amd import synth_ext
+    from worldql_server_amd.router import Router
+
+    worlds = range(8 * rank, 8 * rank + 8)
+    c4 = synth_ext.config_c4(scale=a.scale, worlds=worlds)
+    t0 = time.perf_counter()
+    init = c4.initial_ops()
+    ticks = [c4.step()[:2] for _ in range(a.warmup + a.steps)]
+    gen_s = time.perf_counter() - t0
+    M = c4.n_peers
+    stream = torch.cuda.Stream(device=dev)
+    r = Router(16, local_rank)
+    r.set_stream(stream.cuda_stream)
+    t0 = time.perf_counter()
+    r.apply_ops(init)
+    build_s = time.perf_counter() - t0
+    S0 = r.stats()["n_entries"]
+    world_t = torch.from_numpy(c4.world.view(np.int32)).to(dev)
+    sender_t = torch.from_numpy(np.arange(M, dtype=np.int32)).to(dev)
+    repl_t = torch.zeros(M, dtype=torch.uint8, device=dev)
+    if world_size > 1:
+        dist.barrier()
+    res = _churn_ticks(a, r, dev, stream, ticks, M, world_t, sender_t, repl_t)
+    t_max_ms, pairs_all = reduce_over_ranks(res["t_ms"], res["P"], dev, world_size)
+    steps = a.steps
+    k_avg_s = res["route_ms"] / res["launches"] / 1e3
+    B = algorithmic_bytes(M, res["F"] // steps, res["P"] // steps) + 40 * (res["ops"] // steps)
+    update_ms = (res["t_ms"] - res["route_ms"]) / steps
+    out = _line(a, world_size, pairs_all / (t_max_ms / 1e3), t_max_ms / steps, "weak",
+                f"C4 world-sharded: 8 worlds x 50k peers per GPU ({8 * world_size} worlds in all), 3x3x3 each, "
+                "U[-256,256)^3 per world; per tick 5% of peers move N(0,16)^3 (incremental unsub/sub churn), then "
+                "one LocalMessage per peer (ExceptSelf)" + ("" if a.scale == 1.0 else f" (scaled {a.scale})"),
+                {"messages_per_tick": M * world_size, "peers_per_gpu": M, "subscriptions_per_gpu": int(S0),
+                 "churn_ops_per_tick_per_gpu": res["ops"] // steps, "pairs_per_tick": int(pairs_all) // steps,
+                 "update_ms_per_tick": round(update_ms, 3), "route_ms_per_tick": round(res["route_ms"] / steps, 3),
+                 "incremental_updates": res["incremental"], "rebuild_fallbacks": res["fallbacks"],
+                 "parallelism": f"world-sharded x{world_size}", "table_build_s": round(build_s, 3),
+                 "generate_s": round(gen_s, 1)},
+                {"bound": "hbm", "achieved": B / (t_max_ms / steps / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                 "unit": "GB/s", "frac": B / (t_max_ms / steps / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                 "kernel": "whole tick (incremental update + route); route launch alone below",
+                 "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
+                "synthetic (splitmix64, SURVEY.md §8(d) C4 generator)")
+    if rank == 0 and world_size == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = _cpu_churn_sample(init, ticks, c4.world, a.cpu_seconds)
+    _emit(out, rank)
+    r.close()
+    if world_size > 1:
+        dist.destroy_process_group()
+
+
+def _cpu_churn_sample(init, ticks, world, seconds):
+    """The C restatement on 1 host thread, on ONE world of the GPU's eight (a bounded sample):
+    its initial subscriptions (not timed), then whole ticks — that world's churn ops applied one
+    by one, then its messages routed — until `seconds` of ticks have run."""
+    from oracle import oracle as orc
+    w0 = world.min()
+    o = orc.COracle(16)
+    o.apply_ops(init[init["world"] == w0])
+    sel = world == w0
+    M = int(sel.sum())
+    wz = np.full(M, w0, np.uint32)
+    sender = np.flatnonzero(sel).astype(np.uint32)
+    repl = np.zeros(M, np.uint8)
+    pairs = n = 0
+    t = 0.0
+    for ops, pos in ticks:
+        t0 = time.perf_counter()
+        o.apply_ops(ops[ops["world"] == w0])
+        _, peers, _ = o.route(pos[sel], wz, sender, repl)
+        t += time.perf_counter() - t0
+        pairs += len(peers)
+        n += 1
+        if t >= seconds:
+            break
+    return {"value": pairs / t, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"C4, world {int(w0)} only (1 of 8 per GPU): {n} whole ticks (churn ops applied in order, "
+                      f"then {M} messages routed; {pairs} pairs) in {t:.2f} s by oracle/wq_oracle.c on 1 host thread"}
+
+
+def run_c5(a, rank, world_size, local_rank, dev):
+    import torch
+    from worldql_server_amd import synth_ext
+    from worldql_server_amd.router import Router
+
+    if world_size > 1:
+        raise SystemExit("bench.py --config c5 runs on one GPU (the sharded radius path is not built yet)")
+    c5 = synth_ext.config_c5(scale=a.scale)
+    t0 = time.perf_counter()
+    init = c5.initial_ops()
+    init_pos = c5.pos.copy()
+    ticks = []
+    for _ in range(a.warmup + a.steps):
+        ops = c5.step()
+        ticks.append((ops, c5.pos.copy()))
+    gen_s = time.perf_counter() - t0
+    M = c5.n
+    stream = torch.cuda.Stream(device=dev)
+    r = Router(16, local_rank)
+    r.set_stream(stream.cuda_stream)
+    t0 = time.perf_counter()
+    r.apply_ops(init)
+    build_s = time.perf_counter() - t0
+    S0 = r.stats()["n_entries"]
+    r.set_peer_positions(init_pos)
+    r.set_radius(c5.radius)
+    world_t = torch.zeros(M, dtype=torch.int32, device=dev)
+    sender_t = torch.from_numpy(np.arange(M, dtype=np.int32)).to(dev)
+    repl_t = torch.zeros(M, dtype=torch.uint8, device=dev)
+    res = _churn_ticks(a, r, dev, stream, ticks, M, world_t, sender_t, repl_t, positions=True)
+    steps = a.steps
+    k_avg_s = res["route_ms"] / res["launches"] / 1e3
+    P, F = res["P"] // steps, res["F"] // steps
+    B = algorithmic_bytes(M, F, P) + 40 * (res["ops"] // steps) + 24 * M + 24 * F
+    out = _line(a, 1, res["P"] / (res["t_ms"] / 1e3), res["t_ms"] / steps, "strong",
+                "C5: 1M entities in U[-1024,1024)^3 moving U[-4,4)^3 per tick, 3x3x3 subscriptions kept current "
+                "by incremental churn, one LocalMessage each, exact radius filter r=16 (f64, no FMA) after the "
+                "cube broadphase; one GPU" + ("" if a.scale == 1.0 else f" (scaled {a.scale})"),
+                {"messages_per_tick": M, "entities": M, "subscriptions": int(S0),
+                 "churn_ops_per_tick": res["ops"] // steps, "pairs_per_tick": P, "broadphase_candidates_per_tick": F,
+                 "update_ms_per_tick": round((res["t_ms"] - res["route_ms"]) / steps, 3),
+                 "route_ms_per_tick": round(res["route_ms"] / steps, 3),
+                 "incremental_updates": res["incremental"], "rebuild_fallbacks": res["fallbacks"],
+                 "parallelism": "1 GPU", "table_build_s": round(build_s, 3), "generate_s": round(gen_s, 1)},
+                {"bound": "hbm", "achieved": B / (res["t_ms"] / steps / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                 "unit": "GB/s", "frac": B / (res["t_ms"] / steps / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                 "kernel": "whole tick (incremental update + positions + radius route); route launches alone below",
+                 "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
+                "synthetic (splitmix64, SURVEY.md §8(d) C5 generator)")
+    _emit(out, rank)
+    r.close()

@@ -103,6 +103,12 @@ int wq_get_stats(wq_router* h, wq_stats* out);
  * Replaces area_subscribe.rs:137-138 / area_unsubscribe.rs:189-190 -> AreaMap::{add,remove}_subscription
  * and thread.rs:124-125 -> WorldMap::remove_peer. */
 int wq_apply_ops(wq_router* h, const wq_op* ops, size_t n);
+/* The same for a batch already in device memory (e.g. assembled by the caller's own kernels):
+ * subscribe / unsubscribe ops only — a REMOVE_PEER op or the reserved world id fails the whole
+ * batch with WQ_E_INVALID before anything changes (use wq_remove_peers for disconnects).
+ * The call blocks on one small read-back (the update plan's sizes); the update itself is ordered
+ * on the handle's stream, before any later tick. */
+int wq_apply_ops_device(wq_router* h, const wq_op* d_ops, size_t n);
 /* WorldMap::remove_peer for n peers (every world), world_map.rs:41-61. */
 int wq_remove_peers(wq_router* h, const uint32_t* peers, size_t n);
 

@@ -34,7 +34,7 @@ struct DeltaSummary {
     uint64_t d_live;       // two's complement: cubes that became non-empty - cubes that emptied
     uint64_t new_recs;     // records claimed
     uint64_t reloc_words;  // list words to bump-allocate
-    uint32_t irregular;    // an op without a packed key
+    uint32_t irregular;    // 1: an op without a packed key; 2: an invalid op (device batches)
     uint32_t n_dc;         // touched cubes
 };
 
@@ -67,6 +67,7 @@ __global__ void k_delta_events(const wq_op* __restrict__ ops, uint32_t n, double
     int64_t k[3];
     op_key(o, sf, si, k);
     uint64_t p = 0;
+    if (o.kind > WQ_OP_UNSUBSCRIBE || o.world == WQ_WORLD_INVALID) atomicOr(&sum->irregular, 2u);  // bad op
     if (!pack_key(o.world, k[0], k[1], k[2], sf, &p)) atomicOr(&sum->irregular, 1u);
     pk[i] = p;
     peer[i] = o.peer;
@@ -355,7 +356,7 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     WQ_ALLOC(h, h->cube_start, ((uint64_t)n + 1) * 4);
     DeltaSummary* sum = d.summ.as<DeltaSummary>();
     WQ_HIP(h, hipMemsetAsync(sum, 0, sizeof(DeltaSummary), s));
-    hipLaunchKernelGGL(k_delta_events, dim3(nb), dim3(kBlock), 0, s, h->d_ops.as<wq_op>(), n,
+    hipLaunchKernelGGL(k_delta_events, dim3(nb), dim3(kBlock), 0, s, h->cur_ops, n,
                        (double)h->cube_size, (int64_t)h->cube_size, d.pk.as<uint64_t>(), d.peer.as<uint32_t>(),
                        d.kind.as<uint8_t>(), sum);
     // order = stable sort by (pk, peer): by peer, then stably by pk
@@ -387,6 +388,7 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     DeltaSummary hs;
     WQ_HIP(h, hipMemcpyAsync(&hs, sum, sizeof(hs), hipMemcpyDeviceToHost, s));
     WQ_HIP(h, hipStreamSynchronize(s));
+    if (hs.irregular & 2u) return set_error(h, WQ_E_INVALID, "bad op (kind or reserved world id)");
     const uint64_t list_limit = std::min<uint64_t>(t.list_cap, 0xFFFFFFFFull);
     if (hs.irregular || t.list_used + hs.reloc_words > list_limit || 4 * (t.n_recs + hs.new_recs) > t.rec_cap) {
         h->n_delta_fallbacks++;

@@ -115,6 +115,9 @@ __host__ __device__ __forceinline__ uint64_t peer_sig(uint32_t peer) {
     return (1ull << (h >> 26)) | (1ull << ((h >> 20) & 63u));
 }
 static_assert(sizeof(Record) == 128, "Record must be one 128-byte line");
+// Capacity (peers) a list gets when the table is built: 25% headroom plus 2, so the incremental
+// update (wq_delta.hip) edits most churned lists in place.
+__host__ __device__ __forceinline__ uint32_t list_capacity(uint32_t count) { return count + count / 4 + 2; }
 
 __host__ __device__ __forceinline__ bool pack_key(uint32_t w, int64_t x, int64_t y, int64_t z, double sf,
                                                   uint64_t* pk) {

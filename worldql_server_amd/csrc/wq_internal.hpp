@@ -114,6 +114,7 @@ struct wq_router {
 
     // build scratch
     wq::DevBuf ev_h, ev_w, ev_kx, ev_ky, ev_kz, ev_p, ev_kind, d_ops;
+    const wq_op* cur_ops = nullptr;  // the batch being applied (h->d_ops, or the caller's device array)
     wq::DevBuf idx_a, idx_b, key32_a, key32_b, key64_a, key64_b, flags, scan, sort_tmp, small;
     wq::DevBuf cube_id, cube_start;
 
@@ -153,12 +154,14 @@ int route_config_count();
 // and both slots zeroed, nothing left to launch).
 int route_counters(wq_router* h, size_t M, uint32_t* d_offsets, wq_route_counters** cur, wq_route_counters** nxt);
 // wq_table.hip
-int table_apply_segment(wq_router* h, const wq_op* ops, size_t n);
+// ops on the host (copied to h->d_ops) or, with on_device, a device array the batch is read from
+// (validated on the device: no REMOVE_PEER, no reserved world id).
+int table_apply_segment(wq_router* h, const wq_op* ops, size_t n, bool on_device = false);
 // keys: sorted unique (world << 32 | peer); world == WQ_WORLD_INVALID removes the peer everywhere.
 int table_remove_peers(wq_router* h, const uint64_t* keys_sorted_unique, size_t n);
 int table_rebuild_derived(wq_router* h);
-// wq_delta.hip. Applies n subscribe / unsubscribe ops (already in h->d_ops) to the records and lists
-// in place; *applied = false (and nothing changed) when the batch needs the full rebuild.
+// wq_delta.hip. Applies n subscribe / unsubscribe ops (h->cur_ops) to the records and lists in
+// place; *applied = false (and nothing changed) when the batch needs the full rebuild.
 int table_apply_delta(wq_router* h, size_t n, bool* applied);
 // Regenerates `st` (grouped by cube, peers ascending) from the records, slots and lists.
 int table_materialize(wq_router* h);

@@ -240,6 +240,12 @@ int wq_apply_ops(wq_router* h, const wq_op* ops, size_t n) {
     return WQ_OK;
 }
 
+int wq_apply_ops_device(wq_router* h, const wq_op* d_ops, size_t n) {
+    if (!h || (n && !d_ops)) return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    return table_apply_segment(h, d_ops, n, true);
+}
+
 int wq_remove_peers(wq_router* h, const uint32_t* peers, size_t n) {
     if (!h || (n && !peers)) return WQ_E_INVALID;
     WQ_HIP(h, hipSetDevice(h->device));

@@ -29,10 +29,11 @@ namespace {
 __global__ void k_ops_to_events(const wq_op* __restrict__ ops, uint32_t n, uint64_t base,
                                 double sf, int64_t si, uint64_t hmask, uint64_t* ev_h,
                                 uint32_t* ev_w, int64_t* ev_kx, int64_t* ev_ky, int64_t* ev_kz,
-                                uint32_t* ev_p, uint8_t* ev_kind) {
+                                uint32_t* ev_p, uint8_t* ev_kind, uint32_t* flag) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const wq_op o = ops[i];
+    if (o.kind > WQ_OP_UNSUBSCRIBE || o.world == WQ_WORLD_INVALID) atomicOr(flag, 2u);  // bad op
     int64_t k0, k1, k2;
     if (o.key_is_raw) {  // impl ToCubeArea for CubeArea: identity (cube_area.rs:65-70)
         k0 = o.u.key[0];
@@ -127,20 +128,27 @@ __global__ void k_cube_start(const uint32_t* __restrict__ head, const uint32_t* 
     if (i == 0) cube_start[n_cubes] = (uint32_t)n;
 }
 
-// Cube c's entries [s_c, s_{c+1}) land at list[s_c + c + 1 ...], its count at list[s_c + c].
+// Words of cube c's list block: [count, peers..., headroom] (list_capacity, wq_device.hpp).
+__global__ void k_list_words(const uint32_t* __restrict__ cube_start, uint32_t n_cubes, uint32_t* words) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c < n_cubes) words[c] = 1u + list_capacity(cube_start[c + 1] - cube_start[c]);
+}
+
+// Cube c's entries [s_c, s_{c+1}) land at list[loff_c + 1 ...], its count at list[loff_c].
 __global__ void k_fill_lists(const uint32_t* __restrict__ st_p, const uint32_t* __restrict__ head,
                              const uint32_t* __restrict__ cid, const uint32_t* __restrict__ cube_start,
-                             uint64_t n, uint32_t* list) {
+                             const uint32_t* __restrict__ loff, uint64_t n, uint32_t* list) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const uint32_t c = cid[i] - 1;
-    list[i + c + 1] = st_p[i];
-    if (head[i]) list[i + c] = cube_start[c + 1] - (uint32_t)i;
+    const uint32_t j = (uint32_t)i - cube_start[c];
+    list[loff[c] + 1 + j] = st_p[i];
+    if (head[i]) list[loff[c]] = cube_start[c + 1] - (uint32_t)i;
 }
 
 // Regular cubes -> 128-byte records (one line per lookup); the rest -> 32-byte full-key slots.
-__global__ void k_insert_cubes(EvView st, const uint32_t* __restrict__ cube_start, uint32_t n_cubes,
-                               uint32_t* rclaim, Record* recs, uint64_t rmask, int rshift, uint32_t* claim,
+__global__ void k_insert_cubes(EvView st, const uint32_t* __restrict__ cube_start,
+                               const uint32_t* __restrict__ loff, uint32_t n_cubes, uint32_t* rclaim, Record* recs, uint64_t rmask, int rshift, uint32_t* claim,
                                Slot* slots, uint64_t mask, int shift, uint64_t hmask, double sf) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     if (c >= n_cubes) return;
@@ -153,11 +161,11 @@ __global__ void k_insert_cubes(EvView st, const uint32_t* __restrict__ cube_star
         Record& r = recs[s];
         r.pk = pk;
         r.count = cnt;
-        r.list_off = j + c;
+        r.list_off = loff[c];
         uint64_t sig = 0;
         for (uint32_t i = 0; i < cnt; ++i) sig |= peer_sig(st.p[j + i]);
         r.sig = sig;
-        r.unused[0] = cnt;  // list capacity: the build packs lists densely
+        r.unused[0] = list_capacity(cnt);
         r.unused[1] = 0xFFFFFFFFu;
 #pragma unroll 2
         for (int i = 0; i < kInline; ++i) r.peers[i] = (uint32_t)i < cnt ? st.p[j + i] : 0xFFFFFFFFu;
@@ -170,7 +178,7 @@ __global__ void k_insert_cubes(EvView st, const uint32_t* __restrict__ cube_star
     r.k[1] = st.ky[j];
     r.k[2] = st.kz[j];
     r.world = st.w[j];
-    r.off = j + c;
+    r.off = loff[c];
     slots[s] = r;
 }
 
@@ -245,13 +253,13 @@ int set_error(wq_router* h, int code, const char* what, hipError_t e) {
 }
 
 // Apply one batch of subscribe / unsubscribe ops (no REMOVE_PEER inside).
-int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops) {
+int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops, bool on_device) {
     if (n_ops == 0) return WQ_OK;
     const uint64_t S = h->st.n;
     const uint64_t N = S + n_ops;
     if (N >= 0xFFFFFFFFull) return set_error(h, WQ_E_INVALID, "more than 2^32-1 subscription events");
 
-    WQ_ALLOC(h, h->d_ops, n_ops * sizeof(wq_op));
+    if (!on_device) WQ_ALLOC(h, h->d_ops, n_ops * sizeof(wq_op));
     WQ_ALLOC(h, h->ev_h, N * 8);
     WQ_ALLOC(h, h->ev_w, N * 4);
     WQ_ALLOC(h, h->ev_kx, N * 8);
@@ -269,7 +277,12 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops) {
     WQ_ALLOC(h, h->small, 64);
 
     hipStream_t s = h->stream;
-    WQ_HIP(h, hipMemcpyAsync(h->d_ops.p, ops, n_ops * sizeof(wq_op), hipMemcpyHostToDevice, s));
+    if (on_device) {
+        h->cur_ops = ops;
+    } else {
+        WQ_HIP(h, hipMemcpyAsync(h->d_ops.p, ops, n_ops * sizeof(wq_op), hipMemcpyHostToDevice, s));
+        h->cur_ops = h->d_ops.as<wq_op>();
+    }
     int rc;
     // small batches against a built table: update the touched cubes in place (wq_delta.hip)
     if (S && h->tab.n_cubes && 4 * n_ops <= S) {
@@ -289,11 +302,13 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops) {
         hipLaunchKernelGGL(k_fill_u8, dim3(grid_for(S)), dim3(kBlock), 0, s, h->ev_kind.as<uint8_t>(), S,
                            (uint8_t)1);
     }
-    hipLaunchKernelGGL(k_ops_to_events, dim3(grid_for(n_ops)), dim3(kBlock), 0, s, h->d_ops.as<wq_op>(),
+    uint32_t* dflag = h->small.as<uint32_t>();
+    WQ_HIP(h, hipMemsetAsync(dflag, 0, 4, s));
+    hipLaunchKernelGGL(k_ops_to_events, dim3(grid_for(n_ops)), dim3(kBlock), 0, s, h->cur_ops,
                        (uint32_t)n_ops, S, (double)h->cube_size, (int64_t)h->cube_size, h->hash_mask,
                        h->ev_h.as<uint64_t>(), h->ev_w.as<uint32_t>(), h->ev_kx.as<int64_t>(),
                        h->ev_ky.as<int64_t>(), h->ev_kz.as<int64_t>(), h->ev_p.as<uint32_t>(),
-                       h->ev_kind.as<uint8_t>());
+                       h->ev_kind.as<uint8_t>(), dflag);
     WQ_HIP(h, hipGetLastError());
 
     // order = stable sort by (hash, peer): sort by peer, then stably by hash
@@ -309,13 +324,12 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops) {
     uint32_t* order = idx_a;
 
     EvView ev = ev_view(h);
-    uint32_t* dflag = h->small.as<uint32_t>();
-    WQ_HIP(h, hipMemsetAsync(dflag, 0, 4, s));
     hipLaunchKernelGGL(k_detect_collision, dim3(grid_for(N)), dim3(kBlock), 0, s, ev, order, N, dflag);
     uint32_t collided = 0;
     rc = read_u32(h, dflag, 0, &collided);
     if (rc) return rc;
-    if (collided) {
+    if (collided & 2u) return set_error(h, WQ_E_INVALID, "bad op (kind or reserved world id)");
+    if (collided & 1u) {
         // exact path: LSD passes peer, kz, ky, kx, world, hash over the original event order
         h->hash_fallbacks++;
         hipLaunchKernelGGL(k_iota, dim3(grid_for(N)), dim3(kBlock), 0, s, idx_b, N);
@@ -391,6 +405,7 @@ int table_rebuild_derived(wq_router* h) {
     Table& t = h->tab;
     int rc;
     uint32_t n_cubes = 0;
+    uint64_t list_words = 0;
     EvView st = st_view(h->st);
     if (S) {
         WQ_ALLOC(h, h->flags, S * 4);
@@ -403,10 +418,23 @@ int table_rebuild_derived(wq_router* h) {
         WQ_ALLOC(h, h->cube_start, ((uint64_t)n_cubes + 1) * 4);
         hipLaunchKernelGGL(k_cube_start, dim3(grid_for(S)), dim3(kBlock), 0, s, head, cid, S, n_cubes,
                            h->cube_start.as<uint32_t>());
-        // dense lists, plus room for lists that incremental updates relocate (wq_delta.hip)
-        WQ_ALLOC(h, t.list, ((S + n_cubes) * 3 / 2 + 65536) * 4);
+        // list blocks with headroom (list_capacity), then room for lists that incremental updates
+        // relocate (wq_delta.hip)
+        WQ_ALLOC(h, h->cube_id, (uint64_t)n_cubes * 8);
+        uint32_t* words = h->cube_id.as<uint32_t>();
+        uint32_t* loff = words + n_cubes;
+        hipLaunchKernelGGL(k_list_words, dim3(grid_for(n_cubes)), dim3(kBlock), 0, s, h->cube_start.as<uint32_t>(),
+                           n_cubes, words);
+        if ((rc = scan_u32(h, words, loff, n_cubes, false))) return rc;
+        uint32_t lw = 0, lo = 0;
+        if ((rc = read_u32(h, words, n_cubes - 1, &lw))) return rc;
+        if ((rc = read_u32(h, loff, n_cubes - 1, &lo))) return rc;
+        list_words = (uint64_t)lo + lw;
+        if (list_words + list_words / 2 + 65536 >= 0xFFFFFFFFull)
+            return set_error(h, WQ_E_INVALID, "subscription lists exceed 2^32 words");
+        WQ_ALLOC(h, t.list, (list_words + list_words / 2 + 65536) * 4);
         hipLaunchKernelGGL(k_fill_lists, dim3(grid_for(S)), dim3(kBlock), 0, s, h->st.p.as<uint32_t>(), head,
-                           cid, h->cube_start.as<uint32_t>(), S, t.list.as<uint32_t>());
+                           cid, h->cube_start.as<uint32_t>(), loff, S, t.list.as<uint32_t>());
     } else {
         WQ_ALLOC(h, t.list, 4);
     }
@@ -439,12 +467,13 @@ int table_rebuild_derived(wq_router* h) {
     t.rec_shift = 64 - log2r;
     if (n_cubes)
         hipLaunchKernelGGL(k_insert_cubes, dim3(grid_for(n_cubes)), dim3(kBlock), 0, s, st,
-                           h->cube_start.as<uint32_t>(), n_cubes, t.rclaim.as<uint32_t>(), t.recs.as<Record>(),
+                           h->cube_start.as<uint32_t>(), h->cube_id.as<uint32_t>() + n_cubes, n_cubes,
+                           t.rclaim.as<uint32_t>(), t.recs.as<Record>(),
                            rcap - 1, t.rec_shift, t.claim.as<uint32_t>(), t.slots.as<Slot>(), cap - 1, t.shift,
                            h->hash_mask, (double)h->cube_size);
     t.n_cubes = n_cubes;
     t.n_recs = n_cubes;
-    t.list_used = S ? S + n_cubes : 0;
+    t.list_used = list_words;
     t.list_cap = t.list.bytes / 4;
     h->st_stale = false;
     if ((rc = build_any(h))) return rc;

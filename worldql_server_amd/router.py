@@ -51,6 +51,7 @@ def load_library(build_if_missing: bool = True):
         "wq_set_stream": ([vp, vp], i32),
         "wq_get_stats": ([vp, vp], i32),
         "wq_apply_ops": ([vp, vp, sz], i32),
+        "wq_apply_ops_device": ([vp, vp, sz], i32),
         "wq_remove_peers": ([vp, vp, sz], i32),
         "wq_route_tick": ([vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, ctypes.POINTER(sz)], i32),
         "wq_route_tick_device": ([vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, vp], i32),
@@ -138,6 +139,10 @@ class Router:
     def apply_ops(self, ops: np.ndarray) -> None:
         ops = np.ascontiguousarray(ops, dtype=abi.OP_DTYPE)
         self._check(self.lib.wq_apply_ops(self.h, _p(ops), len(ops)))
+
+    def apply_ops_device(self, ops_ptr: int, n: int) -> None:
+        """A subscribe / unsubscribe batch already on the device (40-byte wq_op records)."""
+        self._check(self.lib.wq_apply_ops_device(self.h, ops_ptr or None, n))
 
     def remove_peers(self, peers) -> None:
         a = np.ascontiguousarray(peers, dtype=np.uint32)

@@ -72,30 +72,34 @@ def config_c3(scale: float = 1.0, sigma: float = 128.0) -> Workload:
 def _moves_to_ops(world, peers, old, new, s: int) -> np.ndarray:
     """AreaUnsubscribe for the cells of old + s*d that new + s*d no longer covers, then
     AreaSubscribe for the cells newly covered (positions, quantised by the table like the reference
-    handlers do)."""
+    handlers do). Quantisation is per axis, so a peer's 27 cells are the product of three per-axis
+    triples {cell(v - s), cell(v), cell(v + s)}: a cell is left iff one of its axis values is not in
+    the new triple of that axis."""
     peers = np.asarray(peers, np.uint32)
     world = np.asarray(world, np.uint32)
     # only peers whose own cell changed can change their 27 cells
     ch = (cell_keys(old, s) != cell_keys(new, s)).any(1)
     if not ch.all():
         world, peers, old, new = world[ch], peers[ch], old[ch], new[ch]
-    if len(peers) == 0:
-        return np.zeros(0, abi.OP_DTYPE)
-    if len(peers) > 20_000:  # bound the (n, 27, 27, 3) comparison's memory
-        parts = [_moves_to_ops(world[i:i + 20_000], peers[i:i + 20_000], old[i:i + 20_000], new[i:i + 20_000], s)
-                 for i in range(0, len(peers), 20_000)]
-        un = abi.concat_ops([p_[p_["kind"] == abi.OP_UNSUBSCRIBE] for p_ in parts])
-        su = abi.concat_ops([p_[p_["kind"] == abi.OP_SUBSCRIBE] for p_ in parts])
-        return abi.concat_ops([un, su])
-    po = old[:, None, :] + s * NEIGHBOURHOOD[None, :, :]          # (n, 27, 3)
-    pn = new[:, None, :] + s * NEIGHBOURHOOD[None, :, :]
-    ko, kn = cell_keys(po, s), cell_keys(pn, s)
-    same = (ko[:, :, None, :] == kn[:, None, :, :]).all(-1)          # (n, 27 old, 27 new)
-    left = ~same.any(2)
-    entered = ~same.any(1)
     n = len(peers)
-    rw = np.repeat(np.asarray(world, np.uint32), 27).reshape(n, 27)
-    rp = np.repeat(np.asarray(peers, np.uint32), 27).reshape(n, 27)
+    if n == 0:
+        return np.zeros(0, abi.OP_DTYPE)
+    step = s * np.array([-1.0, 0.0, 1.0])
+    d = (NEIGHBOURHOOD + 1).astype(np.int64)                          # (27, 3) axis indices
+    keep_old = np.ones((n, 27), bool)
+    keep_new = np.ones((n, 27), bool)
+    for ax in range(3):
+        to = cell_keys(old[:, ax, None] + step, s)                    # (n, 3)
+        tn = cell_keys(new[:, ax, None] + step, s)
+        in_new = (to[:, :, None] == tn[:, None, :]).any(2)            # old axis value still covered
+        in_old = (tn[:, :, None] == to[:, None, :]).any(2)
+        keep_old &= in_new[:, d[:, ax]]
+        keep_new &= in_old[:, d[:, ax]]
+    left, entered = ~keep_old, ~keep_new
+    po = old[:, None, :] + s * NEIGHBOURHOOD[None, :, :]               # (n, 27, 3)
+    pn = new[:, None, :] + s * NEIGHBOURHOOD[None, :, :]
+    rw = np.repeat(world, 27).reshape(n, 27)
+    rp = np.repeat(peers, 27).reshape(n, 27)
     un = abi.ops_array(rw[left], rp[left], np.full(int(left.sum()), abi.OP_UNSUBSCRIBE, np.uint8), pos=po[left])
     su = abi.ops_array(rw[entered], rp[entered], np.full(int(entered.sum()), abi.OP_SUBSCRIBE, np.uint8),
                        pos=pn[entered])
