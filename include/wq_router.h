@@ -217,9 +217,11 @@ int wq_profile_read(wq_router* h, double* kernel_ms, uint64_t* launches);
 /* ---- test hook: keep only the low `bits` bits of the 64-bit cube hash (64 = normal).
  * Forces bucket collisions so the exact-compare fallback paths are exercised. */
 int wq_debug_set_hash_bits(wq_router* h, int bits);
-/* ---- test hook: how many op batches took the incremental update (wq_delta.hip) and how many
- * of those fell back to the full rebuild (irregular keys, list space, record load). */
-int wq_debug_update_counts(wq_router* h, uint64_t* incremental, uint64_t* rebuild_fallbacks);
+/* ---- test hook: how many op batches took the incremental update (wq_delta.hip), how many
+ * tried it but fell back to the full rebuild (irregular keys, list space, record load), and how
+ * many incremental batches needed the per-lane path (a cube with > 256 peers or > 64 changes). */
+int wq_debug_update_counts(wq_router* h, uint64_t* incremental, uint64_t* rebuild_fallbacks,
+                           uint64_t* lane_batches);
 /* ---- tuning hook: select a compiled route-kernel shape (messages per thread, expansion chunk);
  * 0 is the default. Results are identical for every shape. */
 int wq_debug_set_route_config(wq_router* h, int cfg);

@@ -32,8 +32,9 @@ namespace {
 struct DeltaSummary {
     uint64_t d_entries;    // two's complement: adds - removes
     uint64_t d_live;       // two's complement: cubes that became non-empty - cubes that emptied
-    uint64_t new_recs;     // records claimed
+    uint64_t n_big;        // touched cubes too large for the wave path (lists > kWaveOld, > kWaveCh changes)
     uint64_t reloc_words;  // list words to bump-allocate
+    uint64_t new_recs;     // records claimed by this batch's new cubes
     uint32_t irregular;    // 1: an op without a packed key; 2: an invalid op (device batches)
     uint32_t n_dc;         // touched cubes
 };
@@ -59,7 +60,11 @@ __device__ __forceinline__ void op_key(const wq_op& o, double sf, int64_t si, in
     }
 }
 
-__global__ void k_delta_events(const wq_op* __restrict__ ops, uint32_t n, double sf, int64_t si, uint64_t* pk,
+// Per op: packed key, and the record slot of its cube — a cube the table does not hold yet gets
+// its record here (key claimed by compare-and-swap on the probe path, count 0), so the batch can
+// be grouped by slot with a short radix sort. The caller guarantees free slots (load <= 1/2).
+__global__ void k_delta_events(const wq_op* __restrict__ ops, uint32_t n, double sf, int64_t si, Record* recs,
+                               uint64_t rmask, int rshift, uint64_t hmask, uint64_t* pk, uint32_t* slot,
                                uint32_t* peer, uint8_t* kind, DeltaSummary* sum) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
@@ -67,9 +72,27 @@ __global__ void k_delta_events(const wq_op* __restrict__ ops, uint32_t n, double
     int64_t k[3];
     op_key(o, sf, si, k);
     uint64_t p = 0;
-    if (o.kind > WQ_OP_UNSUBSCRIBE || o.world == WQ_WORLD_INVALID) atomicOr(&sum->irregular, 2u);  // bad op
-    if (!pack_key(o.world, k[0], k[1], k[2], sf, &p)) atomicOr(&sum->irregular, 1u);
+    uint32_t sl = 0;  // ops without a record (the batch then falls back): slot 0, an in-bounds dummy
+    if (o.kind > WQ_OP_UNSUBSCRIBE || o.world == WQ_WORLD_INVALID) {
+        atomicOr(&sum->irregular, 2u);  // bad op
+    } else if (!pack_key(o.world, k[0], k[1], k[2], sf, &p)) {
+        atomicOr(&sum->irregular, 1u);
+    } else {
+        uint64_t j = slot_of(rec_hash(p) & hmask, rshift);
+        for (;;) {
+            unsigned long long* kp = reinterpret_cast<unsigned long long*>(&recs[j].pk);
+            unsigned long long cur = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur == 0) {
+                cur = atomicCAS(kp, 0ull, (unsigned long long)p);
+                if (cur == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&sum->new_recs), 1ull);
+            }
+            if (cur == 0 || cur == p) break;
+            j = (j + 1) & rmask;
+        }
+        sl = (uint32_t)j;
+    }
     pk[i] = p;
+    slot[i] = sl;
     peer[i] = o.peer;
     kind[i] = o.kind == WQ_OP_SUBSCRIBE ? 1 : 0;
 }
@@ -158,7 +181,6 @@ __global__ __launch_bounds__(kBlock) void k_delta_plan(DeltaTable tb, const uint
         const int64_t dl = (int64_t)(oc == 0 && nc > 0) - (int64_t)(oc > 0 && nc == 0);
         if (de) atomicAdd(&acc[0], (unsigned long long)de);
         if (dl) atomicAdd(&acc[1], (unsigned long long)dl);
-        if (slot == kNone && nc > 0) atomicAdd(&acc[2], 1ull);
         if (rw) atomicAdd(&acc[3], (unsigned long long)rw);
     }
     if (c < n) reloc[c] = rw;
@@ -182,7 +204,7 @@ __global__ __launch_bounds__(kBlock) void k_delta_reduce(const uint64_t* __restr
     if (threadIdx.x == 0) {
         sum->d_entries = acc[0];
         sum->d_live = acc[1];
-        sum->new_recs = acc[2];
+        sum->n_big = acc[2];
         sum->reloc_words = acc[3];
     }
 }
@@ -203,13 +225,9 @@ __global__ __launch_bounds__(kBlock) void k_delta_apply(DeltaTable tb, const uin
     const uint32_t nc = pl.y, oc = pl.w;
     uint64_t slot = pl.x;
     uint32_t off = 0, cap = 0;
-    if (pl.x == kNone) {  // a new cube: the first unclaimed slot of its probe sequence
-        slot = slot_of(rec_hash(pk) & tb.hmask, tb.rshift);
-        while (atomicCAS(&tb.rclaim[slot], 0u, 1u) != 0u) slot = (slot + 1) & tb.rmask;
-    } else {
-        off = tb.recs[slot].list_off;
-        cap = tb.recs[slot].unused[0];
-    }
+    if (pl.x == kNone) return;  // unreachable: k_delta_events gave every cube of the batch a record
+    off = tb.recs[slot].list_off;
+    cap = tb.recs[slot].unused[0];
     uint32_t* L = tb.list;
     if (reloc[c]) {  // forward merge of the old list and the changes into new space
         const uint32_t dst = (uint32_t)(list_base + reloc_off[c]);
@@ -266,6 +284,225 @@ __global__ __launch_bounds__(kBlock) void k_delta_apply(DeltaTable tb, const uin
     r.unused[1] = kNone;
 #pragma unroll 4
     for (int j = 0; j < kInline; ++j) r.peers[j] = (uint32_t)j < nc ? a[j] : kNone;
+}
+
+// ---- the group path: 16 lanes per touched cube ------------------------------------------------
+// The batch is grouped by record slot (one radix sort over log2(capacity) bits). A light plan reads
+// only each touched cube's record header and reserves relocation space for an upper bound (old
+// count + changes). Then a group of 16 lanes per cube stages the list in LDS (old count + changes
+// <= kGroupList), takes the cube's changes in op order 16 at a time, sorts each chunk by (peer, op)
+// with a bitonic network in registers (the last op of a peer wins within the chunk, chunks apply in
+// order), merges adds and removes into the other LDS buffer by rank, and finally writes the list
+// and the record line with coalesced stores. A batch holding a cube beyond the bound takes the
+// per-lane path above.
+constexpr int kG = 16;
+constexpr int kGroups = kBlock / kG;
+constexpr uint32_t kGroupList = 128;
+constexpr uint32_t kGroupGrid = 2048;
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t lds_lower_bound(const uint32_t* a, uint32_t n, uint32_t v) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < v)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+__global__ void k_delta_mark_slot(const uint32_t* __restrict__ order, const uint32_t* __restrict__ sslot,
+                                  const uint32_t* __restrict__ peer, const uint8_t* __restrict__ kind, uint32_t n,
+                                  uint32_t* sp, uint8_t* skd, uint32_t* head) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t a = order[i];
+    sp[i] = peer[a];
+    skd[i] = kind[a];
+    head[i] = (i == 0 || sslot[i] != sslot[i - 1]) ? 1u : 0u;
+}
+
+// One lane per touched cube: {slot, first op, ops, old count} and the relocation reserve.
+__global__ __launch_bounds__(kBlock) void k_delta_plan_light(const Record* __restrict__ recs,
+                                                             const uint32_t* __restrict__ cube_start,
+                                                             const uint32_t* __restrict__ sslot,
+                                                             const uint8_t* __restrict__ skd,
+                                                             const DeltaSummary* sum, uint32_t n, uint4* cinfo,
+                                                             uint32_t* reloc, uint64_t* part) {
+    __shared__ unsigned long long acc[4];
+    if (threadIdx.x < 4) acc[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    uint32_t rw = 0;
+    if (c < sum->n_dc) {
+        const uint32_t s0 = cube_start[c], nch = cube_start[c + 1] - s0;
+        const uint32_t slot = sslot[s0];
+        const uint4* line = reinterpret_cast<const uint4*>(recs + slot);
+        const uint32_t oc = line[0].z, cap = line[1].z;
+        uint32_t subs = 0;  // only subscribes can grow the list
+        for (uint32_t t = s0; t < s0 + nch; ++t) subs += skd[t];
+        if ((uint64_t)oc + nch > kGroupList) atomicAdd(&acc[2], 1ull);
+        const uint64_t ub = (uint64_t)oc + subs;
+        if (ub > cap) rw = 1 + grown((uint32_t)std::min<uint64_t>(ub, 0x7FFFFFFFull));
+        cinfo[c] = make_uint4(slot, s0, nch, oc);
+        if (rw) atomicAdd(&acc[3], (unsigned long long)rw);
+    }
+    if (c < n) reloc[c] = rw;
+    __syncthreads();
+    if (threadIdx.x < 4) part[4ull * blockIdx.x + threadIdx.x] = acc[threadIdx.x];
+}
+
+struct GroupLds {
+    uint32_t buf[kGroups][2][kGroupList];
+    uint32_t add[kGroups][kG];
+    uint32_t rem[kGroups][kG];
+};
+
+__global__ __launch_bounds__(kBlock) void k_delta_apply_group(DeltaTable tb, const uint4* __restrict__ cinfo,
+                                                              const uint32_t* __restrict__ sp,
+                                                              const uint8_t* __restrict__ skd,
+                                                              const DeltaSummary* sum,
+                                                              const uint32_t* __restrict__ reloc,
+                                                              const uint32_t* __restrict__ reloc_off,
+                                                              uint64_t list_base, uint64_t* part) {
+    __shared__ GroupLds sm;
+    __shared__ unsigned long long acc[2];
+    if (threadIdx.x < 2) acc[threadIdx.x] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, gl = threadIdx.x & (kG - 1), grp = threadIdx.x / kG;
+    const int gshift = lane & ~(kG - 1);
+    const uint32_t lt = (1u << gl) - 1u;
+    const uint32_t n_dc = sum->n_dc;
+    int64_t de = 0, dl = 0;
+    uint32_t* add = sm.add[grp];
+    uint32_t* rem = sm.rem[grp];
+    for (uint32_t c = blockIdx.x * kGroups + grp; c < n_dc; c += gridDim.x * kGroups) {
+        const uint4 ci = cinfo[c];
+        const uint32_t slot = ci.x, s0 = ci.y, nch = ci.z, oc = ci.w;
+        Record* rec = tb.recs + slot;
+        const uint4 h0 = reinterpret_cast<const uint4*>(rec)[0];
+        const uint32_t off = h0.w, cap0 = reinterpret_cast<const uint4*>(rec)[1].z;
+        uint32_t* cur = sm.buf[grp][0];
+        uint32_t* nxt = sm.buf[grp][1];
+        wave_lds_sync();  // the previous cube's LDS reads are done
+        for (uint32_t k = gl; k < oc; k += kG) cur[k] = tb.list[off + 1 + k];
+        wave_lds_sync();
+        uint32_t n = oc;
+        bool changed = false;
+        for (uint32_t t0 = 0; t0 < nch; t0 += kG) {
+            const uint32_t m = std::min<uint32_t>(kG, nch - t0);
+            const bool has = (uint32_t)gl < m;
+            uint64_t key = has ? (((uint64_t)sp[s0 + t0 + gl] << 32) | (uint32_t)gl) : ~0ull;
+            const uint32_t kd = has ? skd[s0 + t0 + gl] : 0u;
+#pragma unroll
+            for (int k = 2; k <= kG; k <<= 1) {
+#pragma unroll
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    const uint64_t o = __shfl_xor(key, j, kG);
+                    const bool keep_min = ((gl & j) == 0) == ((gl & k) == 0);
+                    key = keep_min ? (o < key ? o : key) : (o > key ? o : key);
+                }
+            }
+            const uint32_t q = (uint32_t)(key >> 32);
+            const bool sub = __shfl(kd, (int)((uint32_t)key & (kG - 1)), kG) != 0;
+            const uint32_t qn = __shfl(q, (gl + 1) & (kG - 1), kG);
+            const bool last = has && ((uint32_t)gl == m - 1 || qn != q);
+            const uint32_t at = last ? lds_lower_bound(cur, n, q) : 0u;
+            const bool present = last && at < n && cur[at] == q;
+            const bool is_add = last && sub && !present, is_rm = last && !sub && present;
+            const uint32_t ga = (uint32_t)(__ballot(is_add) >> gshift) & 0xFFFFu;
+            const uint32_t gr = (uint32_t)(__ballot(is_rm) >> gshift) & 0xFFFFu;
+            const uint32_t nadd = (uint32_t)__popc(ga), nrm = (uint32_t)__popc(gr);
+            if (!(nadd | nrm)) continue;
+            changed = true;
+            const uint32_t add_rank = (uint32_t)__popc(ga & lt);
+            if (is_add) add[add_rank] = q;
+            if (is_rm) rem[__popc(gr & lt)] = q;
+            wave_lds_sync();
+            for (uint32_t k = gl; k < n; k += kG) {  // kept peers shift by the removals / adds below them
+                const uint32_t x = cur[k];
+                const uint32_t r = lds_lower_bound(rem, nrm, x);
+                if (r < nrm && rem[r] == x) continue;
+                nxt[k - r + lds_lower_bound(add, nadd, x)] = x;
+            }
+            if (is_add) nxt[add_rank + at - lds_lower_bound(rem, nrm, q)] = q;
+            wave_lds_sync();
+            uint32_t* t = cur;
+            cur = nxt;
+            nxt = t;
+            n = n + nadd - nrm;
+        }
+        if (!changed) continue;
+        uint32_t dst = off, cap = cap0;
+        const uint32_t rl = reloc[c];
+        if (rl) {
+            dst = (uint32_t)(list_base + reloc_off[c]);
+            cap = rl - 1;
+        }
+        uint32_t* L = tb.list + dst;
+        uint64_t sig = 0;
+        for (uint32_t k = gl; k < n; k += kG) {
+            const uint32_t v = cur[k];
+            L[1 + k] = v;
+            sig |= peer_sig(v);
+        }
+#pragma unroll
+        for (int d = kG / 2; d >= 1; d >>= 1) sig |= __shfl_xor(sig, d, kG);
+        if (gl == 0) L[0] = n;
+        uint32_t* rw = reinterpret_cast<uint32_t*>(rec);  // the record line: 32 words, two per lane
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int w = gl + h * kG;
+            uint32_t v;
+            switch (w) {
+                case 0: v = h0.x; break;
+                case 1: v = h0.y; break;
+                case 2: v = n; break;
+                case 3: v = dst; break;
+                case 4: v = (uint32_t)sig; break;
+                case 5: v = (uint32_t)(sig >> 32); break;
+                case 6: v = cap; break;
+                case 7: v = kNone; break;
+                default: v = (uint32_t)(w - kInlineWord0) < n ? cur[w - kInlineWord0] : kNone; break;
+            }
+            rw[w] = v;
+        }
+        if (gl == 0) {
+            de += (int64_t)n - (int64_t)oc;
+            dl += (int64_t)(oc == 0 && n > 0) - (int64_t)(oc > 0 && n == 0);
+        }
+    }
+    if (de) atomicAdd(&acc[0], (unsigned long long)de);
+    if (dl) atomicAdd(&acc[1], (unsigned long long)dl);
+    __syncthreads();
+    if (threadIdx.x < 2) part[2ull * blockIdx.x + threadIdx.x] = acc[threadIdx.x];
+}
+
+// Adds the group path's per-block entry / live-cube deltas into the running totals.
+__global__ __launch_bounds__(kBlock) void k_delta_stats(const uint64_t* __restrict__ part, uint32_t nb,
+                                                        uint64_t* dstat) {
+    __shared__ unsigned long long acc[2];
+    if (threadIdx.x < 2) acc[threadIdx.x] = 0;
+    __syncthreads();
+    unsigned long long v0 = 0, v1 = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += kBlock) {
+        v0 += part[2ull * b];
+        v1 += part[2ull * b + 1];
+    }
+    if (v0) atomicAdd(&acc[0], v0);
+    if (v1) atomicAdd(&acc[1], v1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        dstat[0] += acc[0];
+        dstat[1] += acc[1];
+    }
 }
 
 // ---- materialize: the sorted-state arrays from the records and slots ---------------------------
@@ -325,41 +562,28 @@ __global__ void k_mat_write(const Record* __restrict__ recs, uint64_t rcap, cons
 
 }  // namespace
 
-int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
-    *applied = false;
-    if (n_ops == 0) {
-        *applied = true;
+int table_sync_delta_stats(wq_router* h) {
+    if (!h->dstat_pending) {
+        WQ_HIP(h, hipStreamSynchronize(h->stream));
         return WQ_OK;
     }
-    const uint32_t n = (uint32_t)n_ops;
+    uint64_t v[2];
+    WQ_HIP(h, hipMemcpyAsync(v, h->dws.dstat.p, 16, hipMemcpyDeviceToHost, h->stream));
+    WQ_HIP(h, hipMemsetAsync(h->dws.dstat.p, 0, 16, h->stream));
+    WQ_HIP(h, hipStreamSynchronize(h->stream));
+    h->st.n = (uint64_t)((int64_t)h->st.n + (int64_t)v[0]);
+    h->tab.n_cubes = (uint64_t)((int64_t)h->tab.n_cubes + (int64_t)v[1]);
+    h->dstat_pending = false;
+    return WQ_OK;
+}
+
+namespace {
+
+// The per-lane path (any cube size): sort by (pk, peer), one lane per touched cube.
+int delta_plan_lanes(wq_router* h, uint32_t n, DeltaTable tb, DeltaSummary* sum) {
     DeltaWs& d = h->dws;
-    Table& t = h->tab;
     hipStream_t s = h->stream;
     const uint32_t nb = grid_for(n);
-    WQ_ALLOC(h, d.pk, (uint64_t)n * 8);
-    WQ_ALLOC(h, d.peer, (uint64_t)n * 4);
-    WQ_ALLOC(h, d.kind, n);
-    WQ_ALLOC(h, d.sp, (uint64_t)n * 4);
-    WQ_ALLOC(h, d.skd, n);
-    WQ_ALLOC(h, d.plan, (uint64_t)n * 16);
-    WQ_ALLOC(h, d.reloc, (uint64_t)n * 4);
-    WQ_ALLOC(h, d.reloc_off, (uint64_t)n * 4);
-    WQ_ALLOC(h, d.part, (uint64_t)nb * 32);
-    WQ_ALLOC(h, d.summ, sizeof(DeltaSummary));
-    WQ_ALLOC(h, h->idx_a, (uint64_t)n * 4);
-    WQ_ALLOC(h, h->idx_b, (uint64_t)n * 4);
-    WQ_ALLOC(h, h->key32_a, (uint64_t)n * 4);
-    WQ_ALLOC(h, h->key64_a, (uint64_t)n * 8);
-    WQ_ALLOC(h, h->key64_b, (uint64_t)n * 8);
-    WQ_ALLOC(h, h->flags, (uint64_t)n * 4);
-    WQ_ALLOC(h, h->scan, (uint64_t)n * 4);
-    WQ_ALLOC(h, h->cube_start, ((uint64_t)n + 1) * 4);
-    DeltaSummary* sum = d.summ.as<DeltaSummary>();
-    WQ_HIP(h, hipMemsetAsync(sum, 0, sizeof(DeltaSummary), s));
-    hipLaunchKernelGGL(k_delta_events, dim3(nb), dim3(kBlock), 0, s, h->cur_ops, n,
-                       (double)h->cube_size, (int64_t)h->cube_size, d.pk.as<uint64_t>(), d.peer.as<uint32_t>(),
-                       d.kind.as<uint8_t>(), sum);
-    // order = stable sort by (pk, peer): by peer, then stably by pk
     uint32_t* idx_a = h->idx_a.as<uint32_t>();
     uint32_t* idx_b = h->idx_b.as<uint32_t>();
     hipLaunchKernelGGL(k_iota, dim3(nb), dim3(kBlock), 0, s, idx_a, (uint64_t)n);
@@ -377,40 +601,142 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     if ((rc = scan_u32(h, head, cid, n, true))) return rc;
     uint32_t* cube_start = h->cube_start.as<uint32_t>();
     hipLaunchKernelGGL(k_delta_cubes, dim3(nb), dim3(kBlock), 0, s, head, cid, n, cube_start, sum);
-    DeltaTable tb{t.recs.as<Record>(), t.rclaim.as<uint32_t>(), t.rec_cap - 1, t.rec_shift, h->hash_mask,
-                  t.list.as<uint32_t>()};
     hipLaunchKernelGGL(k_delta_plan, dim3(nb), dim3(kBlock), 0, s, tb, cube_start, spk, d.sp.as<uint32_t>(),
                        d.skd.as<uint8_t>(), sum, n, d.plan.as<uint4>(), d.reloc.as<uint32_t>(),
                        d.part.as<uint64_t>());
     hipLaunchKernelGGL(k_delta_reduce, dim3(1), dim3(kBlock), 0, s, d.part.as<uint64_t>(), nb, sum);
-    if ((rc = scan_u32(h, d.reloc.as<uint32_t>(), d.reloc_off.as<uint32_t>(), n, false))) return rc;
+    return scan_u32(h, d.reloc.as<uint32_t>(), d.reloc_off.as<uint32_t>(), n, false);
+}
+
+// The group path's plan: sort by record slot, light plan per touched cube.
+int delta_plan_groups(wq_router* h, uint32_t n, DeltaSummary* sum) {
+    DeltaWs& d = h->dws;
+    Table& t = h->tab;
+    hipStream_t s = h->stream;
+    const uint32_t nb = grid_for(n);
+    int bits = 1;
+    while ((1ull << bits) < t.rec_cap) bits++;
+    uint32_t* idx_a = h->idx_a.as<uint32_t>();
+    uint32_t* idx_b = h->idx_b.as<uint32_t>();
+    hipLaunchKernelGGL(k_iota, dim3(nb), dim3(kBlock), 0, s, idx_a, (uint64_t)n);
+    int rc = sort_pairs<uint32_t>(h, d.slot.as<uint32_t>(), h->key32_a.as<uint32_t>(), idx_a, idx_b, n, bits);
+    if (rc) return rc;
+    const uint32_t* sslot = h->key32_a.as<uint32_t>();
+    uint32_t* head = h->flags.as<uint32_t>();
+    uint32_t* cid = h->scan.as<uint32_t>();
+    hipLaunchKernelGGL(k_delta_mark_slot, dim3(nb), dim3(kBlock), 0, s, idx_b, sslot, d.peer.as<uint32_t>(),
+                       d.kind.as<uint8_t>(), n, d.sp.as<uint32_t>(), d.skd.as<uint8_t>(), head);
+    if ((rc = scan_u32(h, head, cid, n, true))) return rc;
+    uint32_t* cube_start = h->cube_start.as<uint32_t>();
+    hipLaunchKernelGGL(k_delta_cubes, dim3(nb), dim3(kBlock), 0, s, head, cid, n, cube_start, sum);
+    hipLaunchKernelGGL(k_delta_plan_light, dim3(nb), dim3(kBlock), 0, s, t.recs.as<Record>(), cube_start, sslot,
+                       d.skd.as<uint8_t>(), sum, n, d.plan.as<uint4>(), d.reloc.as<uint32_t>(), d.part.as<uint64_t>());
+    hipLaunchKernelGGL(k_delta_reduce, dim3(1), dim3(kBlock), 0, s, d.part.as<uint64_t>(), nb, sum);
+    return scan_u32(h, d.reloc.as<uint32_t>(), d.reloc_off.as<uint32_t>(), n, false);
+}
+
+int read_summary(wq_router* h, const DeltaSummary* sum, DeltaSummary* hs) {
     WQ_HIP(h, hipGetLastError());
-    DeltaSummary hs;
-    WQ_HIP(h, hipMemcpyAsync(&hs, sum, sizeof(hs), hipMemcpyDeviceToHost, s));
-    WQ_HIP(h, hipStreamSynchronize(s));
-    if (hs.irregular & 2u) return set_error(h, WQ_E_INVALID, "bad op (kind or reserved world id)");
-    const uint64_t list_limit = std::min<uint64_t>(t.list_cap, 0xFFFFFFFFull);
-    if (hs.irregular || t.list_used + hs.reloc_words > list_limit || 4 * (t.n_recs + hs.new_recs) > t.rec_cap) {
-        h->n_delta_fallbacks++;
-        return WQ_OK;  // nothing was modified: the caller rebuilds
+    WQ_HIP(h, hipMemcpyAsync(hs, sum, sizeof(*hs), hipMemcpyDeviceToHost, h->stream));
+    return table_sync_delta_stats(h);  // synchronises the stream
+}
+
+}  // namespace
+
+int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
+    *applied = false;
+    if (n_ops == 0) {
+        *applied = true;
+        return WQ_OK;
     }
-    hipLaunchKernelGGL(k_delta_apply, dim3(nb), dim3(kBlock), 0, s, tb, cube_start, spk, d.sp.as<uint32_t>(),
-                       d.skd.as<uint8_t>(), sum, d.plan.as<uint4>(), d.reloc.as<uint32_t>(),
-                       d.reloc_off.as<uint32_t>(), t.list_used);
+    const uint32_t n = (uint32_t)n_ops;
+    DeltaWs& d = h->dws;
+    Table& t = h->tab;
+    hipStream_t s = h->stream;
+    // every op may bring a new cube: keep the record table at load <= 1/2 through the claims
+    if (2 * (t.n_recs + n) > t.rec_cap) {
+        h->n_delta_fallbacks++;
+        return WQ_OK;
+    }
+    const uint32_t nb = grid_for(n);
+    WQ_ALLOC(h, d.pk, (uint64_t)n * 8);
+    WQ_ALLOC(h, d.slot, (uint64_t)n * 4);
+    WQ_ALLOC(h, d.peer, (uint64_t)n * 4);
+    WQ_ALLOC(h, d.kind, n);
+    WQ_ALLOC(h, d.sp, (uint64_t)n * 4);
+    WQ_ALLOC(h, d.skd, n);
+    WQ_ALLOC(h, d.plan, (uint64_t)n * 16);
+    WQ_ALLOC(h, d.reloc, (uint64_t)n * 4);
+    WQ_ALLOC(h, d.reloc_off, (uint64_t)n * 4);
+    WQ_ALLOC(h, d.part, ((uint64_t)nb + kGroupGrid) * 32);
+    WQ_ALLOC(h, d.summ, sizeof(DeltaSummary));
+    if (!d.dstat.p) {
+        WQ_ALLOC(h, d.dstat, 16);
+        WQ_HIP(h, hipMemsetAsync(d.dstat.p, 0, 16, s));
+    }
+    WQ_ALLOC(h, h->idx_a, (uint64_t)n * 4);
+    WQ_ALLOC(h, h->idx_b, (uint64_t)n * 4);
+    WQ_ALLOC(h, h->key32_a, (uint64_t)n * 4);
+    WQ_ALLOC(h, h->key64_a, (uint64_t)n * 8);
+    WQ_ALLOC(h, h->key64_b, (uint64_t)n * 8);
+    WQ_ALLOC(h, h->flags, (uint64_t)n * 4);
+    WQ_ALLOC(h, h->scan, (uint64_t)n * 4);
+    WQ_ALLOC(h, h->cube_start, ((uint64_t)n + 1) * 4);
+    DeltaSummary* sum = d.summ.as<DeltaSummary>();
+    WQ_HIP(h, hipMemsetAsync(sum, 0, sizeof(DeltaSummary), s));
+    hipLaunchKernelGGL(k_delta_events, dim3(nb), dim3(kBlock), 0, s, h->cur_ops, n, (double)h->cube_size,
+                       (int64_t)h->cube_size, t.recs.as<Record>(), t.rec_cap - 1, t.rec_shift, h->hash_mask,
+                       d.pk.as<uint64_t>(), d.slot.as<uint32_t>(), d.peer.as<uint32_t>(), d.kind.as<uint8_t>(), sum);
+    DeltaTable tb{t.recs.as<Record>(), t.rclaim.as<uint32_t>(), t.rec_cap - 1, t.rec_shift, h->hash_mask,
+                  t.list.as<uint32_t>()};
+    int rc = delta_plan_groups(h, n, sum);
+    if (rc) return rc;
+    DeltaSummary hs;
+    if ((rc = read_summary(h, sum, &hs))) return rc;
+    // the claims of a batch that falls back stay as empty records (count 0): invisible to every
+    // query, dropped by the rebuild
+    t.n_recs += hs.new_recs;
+    if (hs.irregular & 2u) return set_error(h, WQ_E_INVALID, "bad op (kind or reserved world id)");
+    const bool groups = hs.n_big == 0 && !hs.irregular;
+    if (!groups && !hs.irregular) {  // a cube past the wave path's bounds: plan the batch per lane
+        if ((rc = delta_plan_lanes(h, n, tb, sum))) return rc;
+        if ((rc = read_summary(h, sum, &hs))) return rc;
+    }
+    const uint64_t list_limit = std::min<uint64_t>(t.list_cap, 0xFFFFFFFFull);
+    if (hs.irregular || t.list_used + hs.reloc_words > list_limit || 4 * t.n_recs > t.rec_cap) {
+        h->n_delta_fallbacks++;
+        return WQ_OK;  // no list or count changed: the caller rebuilds
+    }
+    if (groups) {
+        const uint32_t ng = std::min<uint32_t>((n + kGroups - 1) / kGroups, kGroupGrid);
+        hipLaunchKernelGGL(k_delta_apply_group, dim3(ng), dim3(kBlock), 0, s, tb, d.plan.as<uint4>(),
+                           d.sp.as<uint32_t>(), d.skd.as<uint8_t>(), sum, d.reloc.as<uint32_t>(),
+                           d.reloc_off.as<uint32_t>(), t.list_used, d.part.as<uint64_t>());
+        // entry / live-cube deltas stay on the device until the next read-back (table_sync_delta_stats)
+        hipLaunchKernelGGL(k_delta_stats, dim3(1), dim3(kBlock), 0, s, d.part.as<uint64_t>(), ng,
+                           d.dstat.as<uint64_t>());
+        h->dstat_pending = true;
+    } else {
+        hipLaunchKernelGGL(k_delta_apply, dim3(nb), dim3(kBlock), 0, s, tb, h->cube_start.as<uint32_t>(),
+                           h->key64_b.as<uint64_t>(), d.sp.as<uint32_t>(), d.skd.as<uint8_t>(), sum,
+                           d.plan.as<uint4>(), d.reloc.as<uint32_t>(), d.reloc_off.as<uint32_t>(), t.list_used);
+        h->st.n = (uint64_t)((int64_t)h->st.n + (int64_t)hs.d_entries);
+        t.n_cubes = (uint64_t)((int64_t)t.n_cubes + (int64_t)hs.d_live);
+    }
     WQ_HIP(h, hipGetLastError());
     t.list_used += hs.reloc_words;
-    h->st.n = (uint64_t)((int64_t)h->st.n + (int64_t)hs.d_entries);
-    t.n_cubes = (uint64_t)((int64_t)t.n_cubes + (int64_t)hs.d_live);
-    t.n_recs += hs.new_recs;
     h->st_stale = true;
     h->any_stale = true;
     h->n_delta_applies++;
+    if (!groups) h->n_delta_lane_batches++;
     *applied = true;
     return WQ_OK;
 }
 
 int table_materialize(wq_router* h) {
     if (!h->st_stale) return WQ_OK;
+    int rc0 = table_sync_delta_stats(h);
+    if (rc0) return rc0;
     Table& t = h->tab;
     hipStream_t s = h->stream;
     const uint64_t D = t.rec_cap + t.cap;

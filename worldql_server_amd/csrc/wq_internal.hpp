@@ -65,11 +65,12 @@ struct Table {
 
 // Scratch of the incremental update (wq_delta.hip).
 struct DeltaWs {
-    DevBuf pk, peer, kind;  // per op (u64, u32, u8)
+    DevBuf pk, slot, peer, kind;  // per op (u64, u32, u32, u8)
     DevBuf sp, skd;         // per op in (pk, peer, op) order: peer, kind
     DevBuf plan;            // uint4 per delta cube {record slot, new count, changed, -}
     DevBuf reloc, reloc_off;  // u32 per delta cube: words of a relocated list, their exclusive scan
     DevBuf part, summ;      // per-block partial sums, the summary read back
+    DevBuf dstat;           // i64 x2: entry / live-cube deltas of group-path batches not yet read back
 };
 
 // Route workspace, persistent across calls so a tick needs no memset: two counter slots (each
@@ -110,7 +111,8 @@ struct wq_router {
     // regenerated from the records on demand (table_materialize / table_ensure_any).
     bool st_stale = false, any_stale = false;
     wq::DeltaWs dws;
-    uint64_t n_delta_applies = 0, n_delta_fallbacks = 0;
+    uint64_t n_delta_applies = 0, n_delta_fallbacks = 0, n_delta_lane_batches = 0;
+    bool dstat_pending = false;
 
     // build scratch
     wq::DevBuf ev_h, ev_w, ev_kx, ev_ky, ev_kz, ev_p, ev_kind, d_ops;
@@ -163,6 +165,9 @@ int table_rebuild_derived(wq_router* h);
 // wq_delta.hip. Applies n subscribe / unsubscribe ops (h->cur_ops) to the records and lists in
 // place; *applied = false (and nothing changed) when the batch needs the full rebuild.
 int table_apply_delta(wq_router* h, size_t n, bool* applied);
+// Folds the device-side entry / live-cube deltas of incremental batches into st.n / tab.n_cubes
+// (synchronises the stream).
+int table_sync_delta_stats(wq_router* h);
 // Regenerates `st` (grouped by cube, peers ascending) from the records, slots and lists.
 int table_materialize(wq_router* h);
 // Rebuilds the any-keys if incremental updates left them stale.

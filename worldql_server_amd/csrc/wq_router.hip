@@ -127,8 +127,8 @@ int wq_router_destroy(wq_router* h) {
                       &h->cube_start, &h->rws.buf, &h->rws.info, &h->rws.e, &h->rws.tiles,
                       &h->h_in, &h->h_out, &h->tab.recs, &h->tab.rclaim, &h->shard_hist,
                       &h->rec_keys, &h->rec_w, &h->rec_s, &h->rec_r, &h->ppos, &h->rws.agg,
-                      &h->dws.pk, &h->dws.peer, &h->dws.kind, &h->dws.sp, &h->dws.skd, &h->dws.plan,
-                      &h->dws.reloc, &h->dws.reloc_off, &h->dws.part, &h->dws.summ};
+                      &h->dws.pk, &h->dws.slot, &h->dws.peer, &h->dws.kind, &h->dws.sp, &h->dws.skd, &h->dws.plan,
+                      &h->dws.reloc, &h->dws.reloc_off, &h->dws.part, &h->dws.summ, &h->dws.dstat};
     for (DevBuf* b : bufs) b->release();
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -148,6 +148,7 @@ int wq_get_stats(wq_router* h, wq_stats* out) {
     WQ_HIP(h, hipSetDevice(h->device));
     int rc = table_ensure_any(h);
     if (rc) return rc;
+    if ((rc = table_sync_delta_stats(h))) return rc;
     out->n_entries = h->st.n;
     out->n_cubes = h->tab.n_cubes;
     out->n_any = h->tab.n_any;
@@ -190,10 +191,12 @@ int wq_debug_set_route_config(wq_router* h, int cfg) {
     return WQ_OK;
 }
 
-int wq_debug_update_counts(wq_router* h, uint64_t* incremental, uint64_t* rebuild_fallbacks) {
-    if (!h || !incremental || !rebuild_fallbacks) return WQ_E_INVALID;
+int wq_debug_update_counts(wq_router* h, uint64_t* incremental, uint64_t* rebuild_fallbacks,
+                           uint64_t* lane_batches) {
+    if (!h || !incremental || !rebuild_fallbacks || !lane_batches) return WQ_E_INVALID;
     *incremental = h->n_delta_applies;
     *rebuild_fallbacks = h->n_delta_fallbacks;
+    *lane_batches = h->n_delta_lane_batches;
     return WQ_OK;
 }
 

@@ -255,11 +255,26 @@ int set_error(wq_router* h, int code, const char* what, hipError_t e) {
 // Apply one batch of subscribe / unsubscribe ops (no REMOVE_PEER inside).
 int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops, bool on_device) {
     if (n_ops == 0) return WQ_OK;
+    hipStream_t s = h->stream;
+    if (on_device) {
+        h->cur_ops = ops;
+    } else {
+        WQ_ALLOC(h, h->d_ops, n_ops * sizeof(wq_op));
+        WQ_HIP(h, hipMemcpyAsync(h->d_ops.p, ops, n_ops * sizeof(wq_op), hipMemcpyHostToDevice, s));
+        h->cur_ops = h->d_ops.as<wq_op>();
+    }
+    int rc;
+    // small batches against a built table: update the touched cubes in place (wq_delta.hip). The
+    // entry count may lag by the device-side deltas of earlier batches: it only picks the path.
+    if (h->st.n && h->tab.n_cubes && 4 * n_ops <= h->st.n) {
+        bool applied = false;
+        if ((rc = table_apply_delta(h, n_ops, &applied))) return rc;
+        if (applied) return WQ_OK;
+    }
+    if ((rc = table_sync_delta_stats(h))) return rc;
     const uint64_t S = h->st.n;
     const uint64_t N = S + n_ops;
     if (N >= 0xFFFFFFFFull) return set_error(h, WQ_E_INVALID, "more than 2^32-1 subscription events");
-
-    if (!on_device) WQ_ALLOC(h, h->d_ops, n_ops * sizeof(wq_op));
     WQ_ALLOC(h, h->ev_h, N * 8);
     WQ_ALLOC(h, h->ev_w, N * 4);
     WQ_ALLOC(h, h->ev_kx, N * 8);
@@ -275,21 +290,6 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops, bool on_de
     WQ_ALLOC(h, h->flags, N * 4);
     WQ_ALLOC(h, h->scan, N * 4);
     WQ_ALLOC(h, h->small, 64);
-
-    hipStream_t s = h->stream;
-    if (on_device) {
-        h->cur_ops = ops;
-    } else {
-        WQ_HIP(h, hipMemcpyAsync(h->d_ops.p, ops, n_ops * sizeof(wq_op), hipMemcpyHostToDevice, s));
-        h->cur_ops = h->d_ops.as<wq_op>();
-    }
-    int rc;
-    // small batches against a built table: update the touched cubes in place (wq_delta.hip)
-    if (S && h->tab.n_cubes && 4 * n_ops <= S) {
-        bool applied = false;
-        if ((rc = table_apply_delta(h, n_ops, &applied))) return rc;
-        if (applied) return WQ_OK;
-    }
     if (h->st_stale && (rc = table_materialize(h))) return rc;
     // live entries first: they are the earliest "present" events
     if (S) {
@@ -365,6 +365,10 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops, bool on_de
 // WorldMap::remove_peer / AreaMap::remove_peer for sorted unique (world << 32 | peer) keys
 // (world_map.rs:41-61, area_map.rs:124-135).
 int table_remove_peers(wq_router* h, const uint64_t* keys, size_t n_rm) {
+    if (h->dstat_pending) {
+        int rc0 = table_sync_delta_stats(h);
+        if (rc0) return rc0;
+    }
     const uint64_t S = h->st.n;
     if (S == 0 || n_rm == 0) return WQ_OK;
     if (h->st_stale) {
@@ -492,6 +496,8 @@ int build_any(wq_router* h) {
     if (S) {
         WQ_ALLOC(h, h->key64_a, S * 8);
         WQ_ALLOC(h, h->key64_b, S * 8);
+        WQ_ALLOC(h, h->flags, S * 4);
+        WQ_ALLOC(h, h->scan, S * 4);
         hipLaunchKernelGGL(k_any_keys, dim3(grid_for(S)), dim3(kBlock), 0, s, h->st.w.as<uint32_t>(),
                            h->st.p.as<uint32_t>(), S, h->key64_a.as<uint64_t>());
         if ((rc = sort_keys_u64(h, h->key64_a.as<uint64_t>(), h->key64_b.as<uint64_t>(), S))) return rc;

@@ -68,7 +68,7 @@ def load_library(build_if_missing: bool = True):
         "wq_debug_set_route_config": ([vp, i32], i32),
         "wq_debug_route_config_count": ([], i32),
         "wq_debug_set_timeline": ([vp, vp], i32),
-        "wq_debug_update_counts": ([vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], i32),
+        "wq_debug_update_counts": ([vp] + [ctypes.POINTER(ctypes.c_uint64)] * 3, i32),
         "wq_set_peer_positions": ([vp, vp, sz], i32),
         "wq_set_peer_positions_device": ([vp, vp, sz], i32),
         "wq_set_radius": ([vp, ctypes.c_double], i32),
@@ -276,11 +276,12 @@ class Router:
         self._check(self.lib.wq_world_peers(self.h, world, _p(out), n.value, ctypes.byref(n)))
         return out[: n.value]
 
-    def update_counts(self):
-        """(batches applied incrementally, batches that fell back to the full rebuild)."""
-        a, b = ctypes.c_uint64(), ctypes.c_uint64()
-        self._check(self.lib.wq_debug_update_counts(self.h, ctypes.byref(a), ctypes.byref(b)))
-        return a.value, b.value
+    def update_counts(self, lanes: bool = False):
+        """(batches applied incrementally, batches that fell back to the full rebuild)
+        [+ incremental batches that took the per-lane path, with lanes=True]."""
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self.lib.wq_debug_update_counts(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return (a.value, b.value, c.value) if lanes else (a.value, b.value)
 
     def route_config_count(self) -> int:
         return int(self.lib.wq_debug_route_config_count())
