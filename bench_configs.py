@@ -13,7 +13,8 @@ the timed region; a tick's timed work is everything the tick does on the GPU.
       peer at its new position (ExceptSelf).
   c5  1M entities moving U[-4,4)^3 per tick in U[-1024,1024)^3, 3x3x3 subscriptions, one message
       each; a tick = the subscription diff of the move (incremental), the new peer positions, and the
-      route with the exact radius filter r = 16. One GPU (N > 1 is not implemented for c5 yet).
+      route with the exact radius filter r = 16. N = 1: one GPU. N > 1: strong scaling by cube hash
+      (message positions travel in the records to the owners; every rank holds all positions).
 """
 from __future__ import annotations
 
@@ -345,7 +346,7 @@ def run_c5(a, rank, world_size, local_rank, dev):
     from worldql_server_amd.router import Router
 
     if world_size > 1:
-        raise SystemExit("bench.py --config c5 runs on one GPU (the sharded radius path is not built yet)")
+        return _run_c5_sharded(a, rank, world_size, local_rank, dev)
     c5 = synth_ext.config_c5(scale=a.scale)
     t0 = time.perf_counter()
     init = c5.initial_ops()
@@ -390,3 +391,74 @@ def run_c5(a, rank, world_size, local_rank, dev):
                 "synthetic (splitmix64, SURVEY.md §8(d) C5 generator)")
     _emit(out, rank)
     r.close()
+
+
+def _run_c5_sharded(a, rank, world_size, local_rank, dev):
+    """C5 over G GPUs by cube hash (strong scaling): every rank applies the churn ops it owns and
+    holds every entity's position; it ingests 1/G of the messages, whose records carry their
+    positions to the owners (RCCL all-to-all), which route them with the radius filter."""
+    import torch
+    import torch.distributed as dist
+    from worldql_server_amd import synth_ext
+    from worldql_server_amd.router import Router
+    from worldql_server_amd.sharded import DeviceShard, DistExchange, ShardedRouter
+
+    c5 = synth_ext.config_c5(scale=a.scale)
+    t0 = time.perf_counter()
+    init = c5.initial_ops()
+    init_pos = c5.pos.copy()
+    ticks = []
+    for _ in range(a.warmup + a.steps):
+        ops = c5.step()
+        ticks.append((ops, c5.pos.copy()))
+    gen_s = time.perf_counter() - t0
+    N = c5.n
+    lo, hi = rank * N // world_size, (rank + 1) * N // world_size
+    stream = torch.cuda.Stream(device=dev)
+    r = Router(16, local_rank)
+    be = DeviceShard(r, stream)
+    sr = ShardedRouter(be, DistExchange())
+    sr.apply_ops(init)
+    be.set_radius(c5.radius, init_pos)
+    own_ops = []
+    for ops, _ in ticks:  # host-partitioned churn: the ops of the cubes this rank owns
+        owner = r.shard_ops(ops, world_size)
+        own_ops.append(_ops_tensor(ops[owner == rank], dev))
+    pos_d = [torch.from_numpy(p_).to(dev) for _, p_ in ticks]
+    world = torch.zeros(hi - lo, dtype=torch.int32, device=dev)
+    sender = torch.arange(lo, hi, dtype=torch.int32, device=dev)
+    repl = torch.zeros(hi - lo, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+
+    def one(i):
+        r.apply_ops_device(own_ops[i].data_ptr(), int(own_ops[i].shape[0]) // 40)
+        r.set_peer_positions_device(pos_d[i].data_ptr(), N)
+        return sr.tick(world, sender, repl, pos=pos_d[i][lo:hi])
+
+    with torch.cuda.stream(stream):
+        for i in range(a.warmup):
+            one(i)
+        stream.synchronize()
+        dist.barrier()
+        P_in = 0
+        t_wall = time.perf_counter()
+        for i in range(a.warmup, a.warmup + a.steps):
+            res = one(i)
+            P_in += int(res.peers.shape[0])
+        torch.cuda.synchronize(dev)
+        t_ms = (time.perf_counter() - t_wall) * 1e3
+        dist.barrier()
+    t_max_ms, pairs_all = reduce_over_ranks(t_ms, P_in, dev, world_size)
+    out = _line(a, world_size, pairs_all / (t_max_ms / 1e3), t_max_ms / a.steps, "strong",
+                f"C5 over {world_size} GPUs by cube hash: 1M entities, incremental churn on the owners, "
+                "message positions to the owners by RCCL all-to-all, exact radius filter r=16"
+                + ("" if a.scale == 1.0 else f" (scaled {a.scale})"),
+                {"messages_per_tick": N, "messages_per_gpu": hi - lo, "entities": N,
+                 "pairs_per_tick": int(pairs_all) // a.steps,
+                 "parallelism": f"cube-hash x{world_size} (RCCL all-to-all)", "generate_s": round(gen_s, 1)},
+                {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                 "traffic": None, "kernel": "whole sharded tick (update + exchange + radius route)"},
+                "synthetic (splitmix64, SURVEY.md §8(d) C5 generator)")
+    _emit(out, rank)
+    r.close()
+    dist.destroy_process_group()

@@ -183,27 +183,33 @@ int wq_quantize_device(wq_router* h, const double* d_coords, size_t n, int64_t* 
 #define WQ_MAX_SHARDS 64
 #define WQ_SHARD_ALL 0xFFFFFFFFu /* owner of a REMOVE_PEER op: every shard */
 
-/* One message on the wire between GPUs (40 bytes): its quantised CubeArea, world, sender,
- * index in the ingesting GPU's batch, and replication code. */
+/* One message on the wire between GPUs (40 bytes): its quantised CubeArea (or, with flags &
+ * WQ_REC_POS, the bits of its f64 position — what the owner's radius filter needs), world,
+ * sender, index in the ingesting GPU's batch, and replication code. */
 typedef struct wq_msg_rec {
     int64_t key[3];
     uint32_t world;
     uint32_t sender;
     uint32_t msg;
     uint8_t repl;
-    uint8_t pad_[3];
+    uint8_t flags;
+    uint8_t pad_[2];
 } wq_msg_rec;
+#define WQ_REC_POS 1u /* key[] holds the message position (double[3] bits); the owner quantises */
 
 /* Owner shard of each op (host arrays); REMOVE_PEER ops get WQ_SHARD_ALL. Each shard applies,
  * in array order, the ops it owns plus every REMOVE_PEER (area_subscribe.rs / area_unsubscribe.rs
  * / thread.rs:124-125 on the owner). */
 int wq_shard_ops(wq_router* h, const wq_op* ops, size_t n, uint32_t n_shards, uint32_t* owner);
 /* Quantise (or take raw keys), compute owners and write the records grouped by owner, stable in
- * message order: d_out[M] and d_counts[n_shards] (device). Asynchronous on the handle's stream. */
+ * message order: d_out[M] and d_counts[n_shards] (device). Asynchronous on the handle's stream.
+ * With the radius filter on (wq_set_radius) and positions given, the records carry the positions
+ * (WQ_REC_POS) so the owner can filter; every shard then needs the peer positions. */
 int wq_shard_messages_device(wq_router* h, const double* d_pos, const int64_t* d_keys,
                              const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
                              size_t n_msgs, uint32_t n_shards, wq_msg_rec* d_out, uint32_t* d_counts);
-/* wq_route_tick_device on received records (the owner side of a sharded tick). */
+/* wq_route_tick_device on received records (the owner side of a sharded tick). With the radius
+ * filter on, records without WQ_REC_POS have no position and route to nobody. */
 int wq_route_records_device(wq_router* h, const wq_msg_rec* d_recs, size_t n_msgs, uint32_t* d_offsets,
                             uint32_t* d_peers, uint32_t* d_msgs, size_t capacity,
                             wq_route_counters* d_counters);

@@ -183,3 +183,54 @@ def test_c4_scaled_churn_is_incremental():
     assert r.update_counts(lanes=True) == (5, 0, 0)  # C4 churn: the wave path throughout
     for wid in (0, 8, 56):
         assert (r.world_peers(wid) == o.world_peers(wid)).all()
+
+
+@pytest.mark.parametrize("hash_bits", [64, 6])
+def test_remove_peers_in_place_vs_oracle(hash_bits):
+    """WorldMap::remove_peer / AreaMap::remove_peer batches applied in place on every list
+    (every-world and one-world removals, long lists, full-key slot cubes), interleaved with
+    incremental churn; the table then keeps routing and answering queries exactly."""
+    rng = np.random.default_rng(21 + hash_bits)
+    f = 1.0 if hash_bits == 64 else 0.05
+    r, o = mk_router(hash_bits=hash_bits), orc.COracle(16)
+    half = 96.0 * f ** (1 / 3)
+    n_peers = 3000
+    base = _random_ops(rng, int(40000 * f), 3, n_peers, half, 1.0)
+    hot = abi.ops_array(np.zeros(400, np.uint32), np.arange(400, dtype=np.uint32), np.zeros(400, np.uint8),
+                        pos=np.tile([[8.0, 8.0, 8.0]], (400, 1)))  # a 400-peer list
+    raw = abi.ops_array(np.ones(60, np.uint32), rng.integers(0, n_peers, 60).astype(np.uint32),
+                        np.zeros(60, np.uint8), key=rng.integers(-4, 4, (60, 3)) * 3)  # off-grid: slot table
+    ops = abi.concat_ops([base, hot, raw])
+    r.apply_ops(ops)
+    o.apply_ops(ops)
+    M = 3000
+
+    def check():
+        pos = rng.uniform(-half - 8, half + 8, (M, 3))
+        pos[:100] = [8.0, 8.0, 8.0]
+        world = rng.integers(0, 3, M).astype(np.uint32)
+        sender = rng.integers(0, n_peers, M).astype(np.uint32)
+        repl = rng.integers(0, 3, M).astype(np.uint8)
+        _check(r, o, pos, world, sender, repl)
+        keys = rng.integers(-4, 4, (200, 3)) * 3
+        kw = np.ones(200, np.uint32)
+        kp = rng.integers(0, n_peers, 200).astype(np.uint32)
+        got = r.is_subscribed(kw, kp, True, keys)
+        assert (got == np.array([o.is_subscribed(1, int(p), True, k) for p, k in zip(kp, keys)])).all()
+        for w in range(3):
+            assert (r.world_peers(w) == o.world_peers(w)).all()
+
+    for t in range(3):
+        gone = rng.choice(n_peers, 150, replace=False).astype(np.uint32)
+        r.remove_peers(gone)          # every world
+        o.apply_ops(abi.ops_array(np.full(150, abi.WORLD_INVALID, np.uint32), gone,
+                                  np.full(150, abi.OP_REMOVE_PEER, np.uint8), pos=np.zeros((150, 3))))
+        one = abi.ops_array(np.full(80, t % 3, np.uint32), rng.choice(n_peers, 80, replace=False).astype(np.uint32),
+                            np.full(80, abi.OP_REMOVE_PEER, np.uint8), pos=np.zeros((80, 3)))  # one world
+        churn = _random_ops(rng, int(2000 * f), 3, n_peers, half, 0.6)
+        b = abi.concat_ops([one, churn])
+        r.apply_ops(b)
+        o.apply_ops(b)
+        check()
+    inc, fb = r.update_counts()
+    assert inc == 3 and fb == 0  # the churn after each removal stays incremental

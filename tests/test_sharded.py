@@ -54,6 +54,10 @@ class OracleShard:
         self.o = orc.COracle(cube_size)
         self.cube_size = cube_size
         self.cap = 1 << 40
+        self.radius, self.peer_pos = 0.0, None
+
+    def set_radius(self, radius, peer_pos):
+        self.radius, self.peer_pos = radius, np.asarray(peer_pos, np.float64)
 
     def shard_ops(self, ops, G):
         k = np.where(ops["key_is_raw"][:, None] == 1, ops["key"],
@@ -73,11 +77,19 @@ class OracleShard:
         recs = np.zeros(len(world), abi.MSG_REC_DTYPE)
         recs["key"], recs["world"], recs["sender"] = k[order], world[order], sender[order]
         recs["msg"], recs["repl"] = order, repl[order]
+        if self.radius > 0 and pos is not None:  # the owner's radius filter needs the positions
+            recs["key"] = np.ascontiguousarray(pos.numpy()[order]).view(np.int64)
+            recs["flags"] = abi.REC_POS
         counts = np.bincount(own, minlength=G).astype(np.int32)
         return torch.from_numpy(recs.view(np.uint8).reshape(-1, 40).copy()), torch.from_numpy(counts)
 
     def route_records(self, recs, n, P_hint=None):
         r = recs.numpy().reshape(-1).view(abi.MSG_REC_DTYPE)
+        if self.radius > 0:
+            pos = np.where((r["flags"] & abi.REC_POS)[:, None] != 0, np.ascontiguousarray(r["key"]).view(np.float64),
+                           np.nan)
+            offs, peers = self.o.route_radius(pos, r["world"], r["sender"], r["repl"], self.peer_pos, self.radius)[:2]
+            return torch.from_numpy(offs.astype(np.int32)), torch.from_numpy(peers.astype(np.int32))
         offs, peers, _ = self.o.route(None, r["world"], r["sender"], r["repl"], keys=r["key"])
         return torch.from_numpy(offs.astype(np.int32)), torch.from_numpy(peers.astype(np.int32))
 
@@ -173,6 +185,61 @@ def test_cube_sharded_tick_threads_cpu():
     _thread_cluster(4, lambda r: OracleShard(16), "cpu")
 
 
+def _radius_cluster(G, make_backend, device):
+    """C5-shaped (scaled) moving entities with the radius filter, sharded by cube over G threads:
+    every shard holds all peer positions; the records carry message positions to the owners."""
+    from worldql_server_amd import synth_ext
+    c5 = synth_ext.config_c5(scale=0.003)
+    init = c5.initial_ops()
+    c5.step()
+    ops = abi.concat_ops([init, c5.step()])
+    pos, world, sender, repl = c5.messages()
+    repl = synth.stream(5, 77).below(3, len(world)).astype(np.uint8)
+    o = orc.COracle(16)
+    o.apply_ops(ops)
+    offs, peers = o.route_radius(pos, world, sender, repl, c5.pos, c5.radius)[:2]
+    want = [peers[offs[i]:offs[i + 1]] for i in range(len(world))]
+    hub = ThreadHub(G)
+    res, errs = {}, []
+
+    def body(rank):
+        try:
+            be = make_backend(rank)
+            be.set_radius(c5.radius, c5.pos)
+            sr = ShardedRouter(be, ThreadExchange(hub, rank))
+            sr.apply_ops(ops)
+            lo, hi = rank * len(world) // G, (rank + 1) * len(world) // G
+            t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+            if device != "cpu":
+                with torch.cuda.stream(be.stream):
+                    tick = sr.tick(t(world[lo:hi]), t(sender[lo:hi]), t(repl[lo:hi]), pos=t(pos[lo:hi]))
+            else:
+                tick = sr.tick(t(world[lo:hi]), t(sender[lo:hi]), t(repl[lo:hi]), pos=t(pos[lo:hi]))
+            res[rank] = (lo, hi, tick.per_message(hi - lo))
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            hub.barrier.abort()
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(G)]
+    for t_ in th:
+        t_.start()
+    for t_ in th:
+        t_.join()
+    if errs:
+        raise errs[0]
+    total = 0
+    for r in range(G):
+        lo, hi, got = res[r]
+        for m in range(hi - lo):
+            assert np.array_equal(got[m], want[lo + m]), (lo + m, got[m], want[lo + m])
+            total += len(got[m])
+    assert total > 0
+
+
+def test_radius_sharded_tick_threads_cpu():
+    _radius_cluster(3, lambda r: OracleShard(16), "cpu")
+
+
 def test_shard_owner_split_is_balanced():
     w, ops = make_tick(n_peers=2000, n_msgs=20000)
     be = OracleShard(16)
@@ -213,3 +280,15 @@ def test_shard_kernels_match_restatement_gpu():
         want_recs, want_counts = fake.shard(args[0], None, *args[1:], G)
         assert np.array_equal(counts.cpu().numpy(), want_counts.numpy())
         assert np.array_equal(recs.cpu().numpy(), want_recs.numpy())  # stable grouping, bit-exact
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [1, 2, 3])
+def test_radius_sharded_tick_gpu_threads(G):
+    from worldql_server_amd.router import Router
+    from worldql_server_amd.sharded import DeviceShard
+
+    def make(rank):
+        return DeviceShard(Router(16, 0), torch.cuda.Stream(device=0))
+
+    _radius_cluster(G, make, "cuda:0")

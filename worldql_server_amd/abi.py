@@ -79,9 +79,10 @@ MAX_SHARDS = 64
 SHARD_ALL = 0xFFFFFFFF  # owner of a REMOVE_PEER op
 
 # struct wq_msg_rec: 40 bytes on the wire between GPUs
+REC_POS = 1  # wq_msg_rec.flags: key holds the f64 position bits (radius filter on)
 MSG_REC_DTYPE = np.dtype({
-    "names": ["key", "world", "sender", "msg", "repl"],
-    "formats": [(np.int64, 3), np.uint32, np.uint32, np.uint32, np.uint8],
-    "offsets": [0, 24, 28, 32, 36],
+    "names": ["key", "world", "sender", "msg", "repl", "flags"],
+    "formats": [(np.int64, 3), np.uint32, np.uint32, np.uint32, np.uint8, np.uint8],
+    "offsets": [0, 24, 28, 32, 36, 37],
     "itemsize": 40,
 })

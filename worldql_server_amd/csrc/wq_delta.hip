@@ -505,6 +505,104 @@ __global__ __launch_bounds__(kBlock) void k_delta_stats(const uint64_t* __restri
     }
 }
 
+// ---- REMOVE_PEER in place (§8(f) F3) -------------------------------------------------------------
+// WorldMap::remove_peer / AreaMap::remove_peer (world_map.rs:41-61, area_map.rs:124-135) for a
+// batch of peers: one pass over every cube of both tables, 16 lanes per cube, removing the peers
+// from each list in place (a chunk's kept peers move only to lower positions, so a forward
+// compaction by group ballots is safe) and rewriting the record's count, signature and inline
+// peers where something moved. Peers removed from every world are a bitmap test; removals from
+// one world a binary search in the sorted (world << 32 | peer) keys. Empty cubes keep their record.
+struct RemoveSet {
+    const uint32_t* all_bits;  // peers removed from every world (bitmap), nullptr if none
+    uint32_t all_n;            // bitmap length in peers
+    const uint64_t* keys;      // sorted (world << 32 | peer) removed from one world
+    uint32_t n_keys;
+};
+
+__device__ __forceinline__ bool removed(const RemoveSet& rs, uint32_t w, uint32_t p) {
+    if (rs.all_bits && p < rs.all_n && ((rs.all_bits[p >> 5] >> (p & 31)) & 1u)) return true;
+    if (!rs.n_keys) return false;
+    const uint64_t v = ((uint64_t)w << 32) | p;
+    uint32_t lo = 0, hi = rs.n_keys;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (rs.keys[mid] < v)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo < rs.n_keys && rs.keys[lo] == v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_remove_peers(DeltaTable tb, const Slot* __restrict__ slots,
+                                                         uint64_t scap, RemoveSet rs, uint64_t* part) {
+    __shared__ unsigned long long acc[2];
+    if (threadIdx.x < 2) acc[threadIdx.x] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, gl = threadIdx.x & (kG - 1), grp = threadIdx.x / kG;
+    const int gshift = lane & ~(kG - 1);
+    const uint32_t lt = (1u << gl) - 1u;
+    const uint64_t rcap = tb.rmask + 1, D = rcap + scap;
+    int64_t de = 0, dl = 0;
+    for (uint64_t e = (uint64_t)blockIdx.x * kGroups + grp; e < D; e += (uint64_t)gridDim.x * kGroups) {
+        const bool is_rec = e < rcap;
+        uint32_t w, off, n;
+        if (is_rec) {
+            const uint4 h0 = reinterpret_cast<const uint4*>(tb.recs + e)[0];
+            const uint64_t pk = ((uint64_t)h0.y << 32) | h0.x;
+            if (!pk || !h0.z) continue;
+            w = (uint32_t)(pk >> 54) - 1u;
+            n = h0.z;
+            off = h0.w;
+        } else {
+            const SlotView v = load_slot(slots, e - rcap);
+            if (v.world == kWorldEmpty) continue;
+            w = v.world;
+            off = v.off;
+            n = tb.list[off];
+        }
+        uint32_t* L = tb.list + off + 1;
+        uint32_t* rw = reinterpret_cast<uint32_t*>(tb.recs + e);
+        uint32_t kept = 0;
+        uint64_t sig = 0;
+        for (uint32_t c0 = 0; c0 < n; c0 += kG) {
+            const uint32_t k = c0 + gl;
+            const uint32_t x = k < n ? L[k] : 0u;
+            const bool keep = k < n && !removed(rs, w, x);
+            const uint32_t mk = (uint32_t)(__ballot(keep) >> gshift) & 0xFFFFu;
+            if (keep) {
+                const uint32_t pos = kept + (uint32_t)__popc(mk & lt);
+                sig |= peer_sig(x);
+                if (pos != k) {  // shifted by an earlier removal
+                    L[pos] = x;
+                    if (is_rec && pos < (uint32_t)kInline) rw[kInlineWord0 + pos] = x;
+                }
+            }
+            kept += (uint32_t)__popc(mk);
+        }
+        if (kept == n) continue;  // group-uniform: nothing removed here
+#pragma unroll
+        for (int d = kG / 2; d >= 1; d >>= 1) sig |= __shfl_xor(sig, d, kG);
+        if (gl == 0) L[-1] = kept;
+        if (is_rec) {
+            for (uint32_t k = kept + gl; k < n && k < (uint32_t)kInline; k += kG) rw[kInlineWord0 + k] = kNone;
+            if (gl == 0) {
+                rw[2] = kept;
+                rw[4] = (uint32_t)sig;
+                rw[5] = (uint32_t)(sig >> 32);
+            }
+        }
+        if (gl == 0) {
+            de -= (int64_t)(n - kept);
+            dl -= kept == 0 ? 1 : 0;
+        }
+    }
+    if (de) atomicAdd(&acc[0], (unsigned long long)de);
+    if (dl) atomicAdd(&acc[1], (unsigned long long)dl);
+    __syncthreads();
+    if (threadIdx.x < 2) part[2ull * blockIdx.x + threadIdx.x] = acc[threadIdx.x];
+}
+
 // ---- materialize: the sorted-state arrays from the records and slots ---------------------------
 
 __device__ __forceinline__ void unpack_key(uint64_t pk, int64_t s, uint32_t* w, int64_t* k) {
@@ -730,6 +828,57 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     h->n_delta_applies++;
     if (!groups) h->n_delta_lane_batches++;
     *applied = true;
+    return WQ_OK;
+}
+
+int table_remove_peers_inplace(wq_router* h, const uint64_t* keys, size_t n_rm) {
+    DeltaWs& d = h->dws;
+    Table& t = h->tab;
+    hipStream_t s = h->stream;
+    // split: (WQ_WORLD_INVALID, peer) = every world -> bitmap; the rest stay sorted keys
+    size_t n_all = 0;
+    uint32_t max_all = 0;
+    while (n_all < n_rm && (keys[n_rm - 1 - n_all] >> 32) == WQ_WORLD_INVALID) {
+        max_all = std::max<uint32_t>(max_all, (uint32_t)keys[n_rm - 1 - n_all]);
+        ++n_all;
+    }
+    const size_t n_one = n_rm - n_all;  // keys sort by world first: the every-world ones are last
+    RemoveSet rs{nullptr, 0, nullptr, (uint32_t)n_one};
+    if (n_all) {
+        const uint32_t words = max_all / 32 + 1;
+        std::vector<uint32_t> bits(words, 0u);
+        for (size_t i = n_one; i < n_rm; ++i) {
+            const uint32_t p = (uint32_t)keys[i];
+            bits[p >> 5] |= 1u << (p & 31);
+        }
+        WQ_ALLOC(h, d.rm_bits, (uint64_t)words * 4);
+        WQ_HIP(h, hipMemcpyAsync(d.rm_bits.p, bits.data(), (size_t)words * 4, hipMemcpyHostToDevice, s));
+        rs.all_bits = d.rm_bits.as<uint32_t>();
+        rs.all_n = words * 32;
+    }
+    if (n_one) {
+        WQ_ALLOC(h, h->key32_b, n_one * 8);
+        WQ_HIP(h, hipMemcpyAsync(h->key32_b.p, keys, n_one * 8, hipMemcpyHostToDevice, s));
+        rs.keys = h->key32_b.as<uint64_t>();
+    }
+    WQ_ALLOC(h, d.part, (uint64_t)kGroupGrid * 32);
+    if (!d.dstat.p) {
+        WQ_ALLOC(h, d.dstat, 16);
+        WQ_HIP(h, hipMemsetAsync(d.dstat.p, 0, 16, s));
+    }
+    DeltaTable tb{t.recs.as<Record>(), t.rclaim.as<uint32_t>(), t.rec_cap - 1, t.rec_shift, h->hash_mask,
+                  t.list.as<uint32_t>()};
+    const uint64_t D = t.rec_cap + t.cap;
+    const uint32_t ng = (uint32_t)std::min<uint64_t>((D + kGroups - 1) / kGroups, kGroupGrid);
+    hipLaunchKernelGGL(k_remove_peers, dim3(ng), dim3(kBlock), 0, s, tb, t.slots.as<Slot>(), t.cap, rs,
+                       d.part.as<uint64_t>());
+    hipLaunchKernelGGL(k_delta_stats, dim3(1), dim3(kBlock), 0, s, d.part.as<uint64_t>(), ng, d.dstat.as<uint64_t>());
+    WQ_HIP(h, hipGetLastError());
+    h->dstat_pending = true;
+    h->st_stale = true;
+    h->any_stale = true;
+    // the host arrays above are read by copies still in flight
+    WQ_HIP(h, hipStreamSynchronize(s));
     return WQ_OK;
 }
 

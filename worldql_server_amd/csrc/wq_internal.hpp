@@ -71,6 +71,7 @@ struct DeltaWs {
     DevBuf reloc, reloc_off;  // u32 per delta cube: words of a relocated list, their exclusive scan
     DevBuf part, summ;      // per-block partial sums, the summary read back
     DevBuf dstat;           // i64 x2: entry / live-cube deltas of group-path batches not yet read back
+    DevBuf rm_bits;         // REMOVE_PEER from every world: bitmap over peer ids
 };
 
 // Route workspace, persistent across calls so a tick needs no memset: two counter slots (each
@@ -165,6 +166,9 @@ int table_rebuild_derived(wq_router* h);
 // wq_delta.hip. Applies n subscribe / unsubscribe ops (h->cur_ops) to the records and lists in
 // place; *applied = false (and nothing changed) when the batch needs the full rebuild.
 int table_apply_delta(wq_router* h, size_t n, bool* applied);
+// REMOVE_PEER in place: keys sorted unique (world << 32 | peer), world WQ_WORLD_INVALID = every
+// world; one pass over every cube's list (wq_delta.hip).
+int table_remove_peers_inplace(wq_router* h, const uint64_t* keys, size_t n);
 // Folds the device-side entry / live-cube deltas of incremental batches into st.n / tab.n_cubes
 // (synchronises the stream).
 int table_sync_delta_stats(wq_router* h);

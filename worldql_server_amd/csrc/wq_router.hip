@@ -128,7 +128,8 @@ int wq_router_destroy(wq_router* h) {
                       &h->h_in, &h->h_out, &h->tab.recs, &h->tab.rclaim, &h->shard_hist,
                       &h->rec_keys, &h->rec_w, &h->rec_s, &h->rec_r, &h->ppos, &h->rws.agg,
                       &h->dws.pk, &h->dws.slot, &h->dws.peer, &h->dws.kind, &h->dws.sp, &h->dws.skd, &h->dws.plan,
-                      &h->dws.reloc, &h->dws.reloc_off, &h->dws.part, &h->dws.summ, &h->dws.dstat};
+                      &h->dws.reloc, &h->dws.reloc_off, &h->dws.part, &h->dws.summ, &h->dws.dstat,
+                      &h->dws.rm_bits};
     for (DevBuf* b : bufs) b->release();
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;

@@ -32,6 +32,7 @@ struct ShardIn {
     uint32_t nblk;
     double sf;
     int64_t si;
+    bool pos_rec;  // records carry the positions (radius filter on)
 };
 
 template <bool RAW>
@@ -156,14 +157,22 @@ __global__ void __launch_bounds__(kBlock)
         const uint32_t m = m0 + i * kBlock;
         if (m < in.M) {
             wq_msg_rec r;
-            r.key[0] = kx[i];
-            r.key[1] = ky[i];
-            r.key[2] = kz[i];
+            if (!RAW && in.pos_rec) {  // the owner's radius filter needs the position itself
+                r.key[0] = __double_as_longlong(in.pos[3ull * m]);
+                r.key[1] = __double_as_longlong(in.pos[3ull * m + 1]);
+                r.key[2] = __double_as_longlong(in.pos[3ull * m + 2]);
+                r.flags = WQ_REC_POS;
+            } else {
+                r.key[0] = kx[i];
+                r.key[1] = ky[i];
+                r.key[2] = kz[i];
+                r.flags = 0;
+            }
             r.world = in.world[m];
             r.sender = in.sender[m];
             r.msg = m;
             r.repl = in.repl[m];
-            r.pad_[0] = r.pad_[1] = r.pad_[2] = 0;
+            r.pad_[0] = r.pad_[1] = 0;
             out[wc[i * kWaves + wave][own[i]] + rank[i]] = r;
         }
     }
@@ -191,16 +200,23 @@ __global__ void op_owner_kernel(const wq_op* __restrict__ ops, uint32_t n, doubl
     owner[i] = shard_of(op.world, x, y, z, G);
 }
 
-// Records -> the SoA inputs of the route passes (keys are already quantised).
+// Records -> the SoA inputs of the route passes: quantised keys, or (pos != nullptr, radius
+// filter on) positions — a record without one gets NaN, which no radius test passes.
 __global__ void unpack_records_kernel(const wq_msg_rec* __restrict__ r, uint32_t M, int64_t* __restrict__ keys,
-                                      uint32_t* __restrict__ world, uint32_t* __restrict__ sender,
-                                      uint8_t* __restrict__ repl) {
+                                      double* __restrict__ pos, uint32_t* __restrict__ world,
+                                      uint32_t* __restrict__ sender, uint8_t* __restrict__ repl) {
     const uint32_t m = blockIdx.x * kBlock + threadIdx.x;
     if (m >= M) return;
     const wq_msg_rec x = r[m];
-    keys[3ull * m] = x.key[0];
-    keys[3ull * m + 1] = x.key[1];
-    keys[3ull * m + 2] = x.key[2];
+    if (pos) {
+        const bool has = (x.flags & WQ_REC_POS) != 0;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) pos[3ull * m + d] = has ? __longlong_as_double(x.key[d]) : __builtin_nan("");
+    } else {
+        keys[3ull * m] = x.key[0];
+        keys[3ull * m + 1] = x.key[1];
+        keys[3ull * m + 2] = x.key[2];
+    }
     world[m] = x.world;
     sender[m] = x.sender;
     repl[m] = x.repl;
@@ -229,6 +245,7 @@ int launch_shard_messages(wq_router* h, const double* d_pos, const int64_t* d_ke
     in.nblk = (uint32_t)((M + kShardTile - 1) / kShardTile);
     in.sf = (double)h->cube_size;
     in.si = (int64_t)h->cube_size;
+    in.pos_rec = h->radius > 0.0 && d_pos != nullptr;
     WQ_ALLOC(h, h->shard_hist, (uint64_t)in.nblk * G * 4);
     uint32_t* hist = h->shard_hist.as<uint32_t>();
     if (d_keys)
@@ -256,18 +273,21 @@ int launch_op_owner(wq_router* h, const wq_op* d_ops, size_t n, uint32_t G, uint
 
 int launch_route_records(wq_router* h, const wq_msg_rec* d_recs, size_t M, uint32_t* d_offsets, uint32_t* d_peers,
                          uint32_t* d_msgs, size_t capacity) {
-    WQ_ALLOC(h, h->rec_keys, M * 24 + 256);
+    WQ_ALLOC(h, h->rec_keys, M * 24 + 256);  // keys, or positions with the radius filter on
     WQ_ALLOC(h, h->rec_w, M * 4 + 256);
     WQ_ALLOC(h, h->rec_s, M * 4 + 256);
     WQ_ALLOC(h, h->rec_r, M + 256);
+    const bool radius = h->radius > 0.0;
     if (M) {
         hipLaunchKernelGGL(unpack_records_kernel, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                           h->stream, d_recs, (uint32_t)M, h->rec_keys.as<int64_t>(), h->rec_w.as<uint32_t>(),
+                           h->stream, d_recs, (uint32_t)M, h->rec_keys.as<int64_t>(),
+                           radius ? h->rec_keys.as<double>() : nullptr, h->rec_w.as<uint32_t>(),
                            h->rec_s.as<uint32_t>(), h->rec_r.as<uint8_t>());
         WQ_HIP(h, hipGetLastError());
     }
-    return launch_route(h, nullptr, h->rec_keys.as<int64_t>(), h->rec_w.as<uint32_t>(), h->rec_s.as<uint32_t>(),
-                        h->rec_r.as<uint8_t>(), M, d_offsets, d_peers, d_msgs, capacity);
+    return launch_route(h, radius ? h->rec_keys.as<double>() : nullptr, radius ? nullptr : h->rec_keys.as<int64_t>(),
+                        h->rec_w.as<uint32_t>(), h->rec_s.as<uint32_t>(), h->rec_r.as<uint8_t>(), M, d_offsets, d_peers,
+                        d_msgs, capacity);
 }
 
 }  // namespace wq

@@ -199,20 +199,6 @@ __global__ void k_scatter_flagged_u64(const uint64_t* __restrict__ a, const uint
     if (i < n && flags[i]) out[pos[i]] = a[i];
 }
 
-// removed: sorted (world << 32 | peer); world 0xFFFFFFFF matches every world.
-__global__ void k_keep_not_removed(const uint32_t* __restrict__ st_w, const uint32_t* __restrict__ st_p,
-                                   uint64_t n, const uint64_t* __restrict__ removed, uint32_t n_removed,
-                                   uint32_t* keep) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t k1 = ((uint64_t)st_w[i] << 32) | st_p[i];
-    const uint64_t k2 = ((uint64_t)kWorldEmpty << 32) | st_p[i];
-    const uint32_t a = lower_bound_dev(removed, n_removed, k1);
-    const uint32_t b = lower_bound_dev(removed, n_removed, k2);
-    const bool gone = (a < n_removed && removed[a] == k1) || (b < n_removed && removed[b] == k2);
-    keep[i] = gone ? 0u : 1u;
-}
-
 EvView ev_view(wq_router* h) {
     return EvView{h->ev_h.as<uint64_t>(), h->ev_w.as<uint32_t>(), h->ev_kx.as<int64_t>(),
                   h->ev_ky.as<int64_t>(), h->ev_kz.as<int64_t>(), h->ev_p.as<uint32_t>()};
@@ -365,41 +351,9 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops, bool on_de
 // WorldMap::remove_peer / AreaMap::remove_peer for sorted unique (world << 32 | peer) keys
 // (world_map.rs:41-61, area_map.rs:124-135).
 int table_remove_peers(wq_router* h, const uint64_t* keys, size_t n_rm) {
-    if (h->dstat_pending) {
-        int rc0 = table_sync_delta_stats(h);
-        if (rc0) return rc0;
-    }
-    const uint64_t S = h->st.n;
-    if (S == 0 || n_rm == 0) return WQ_OK;
-    if (h->st_stale) {
-        int rc0 = table_materialize(h);
-        if (rc0) return rc0;
-    }
-    hipStream_t s = h->stream;
-    WQ_ALLOC(h, h->key32_b, n_rm * 8);
-    WQ_ALLOC(h, h->flags, S * 4);
-    WQ_ALLOC(h, h->scan, S * 4);
-    WQ_HIP(h, hipMemcpyAsync(h->key32_b.p, keys, n_rm * 8, hipMemcpyHostToDevice, s));
-    uint32_t* keep = h->flags.as<uint32_t>();
-    uint32_t* pos = h->scan.as<uint32_t>();
-    hipLaunchKernelGGL(k_keep_not_removed, dim3(grid_for(S)), dim3(kBlock), 0, s, h->st.w.as<uint32_t>(),
-                       h->st.p.as<uint32_t>(), S, h->key32_b.as<uint64_t>(), (uint32_t)n_rm, keep);
-    int rc = scan_u32(h, keep, pos, S, false);
-    if (rc) return rc;
-    uint32_t last_pos = 0, last_keep = 0;
-    if ((rc = read_u32(h, pos, S - 1, &last_pos))) return rc;
-    if ((rc = read_u32(h, keep, S - 1, &last_keep))) return rc;
-    const uint64_t S_new = (uint64_t)last_pos + last_keep;
-    if (S_new == S) return WQ_OK;
-    if ((rc = ensure_state(h, h->st_next, S_new))) return rc;
-    StOut out{h->st_next.h.as<uint64_t>(), h->st_next.w.as<uint32_t>(), h->st_next.kx.as<int64_t>(),
-              h->st_next.ky.as<int64_t>(), h->st_next.kz.as<int64_t>(), h->st_next.p.as<uint32_t>()};
-    hipLaunchKernelGGL(k_scatter_state, dim3(grid_for(S)), dim3(kBlock), 0, s, st_view(h->st), nullptr, keep,
-                       pos, S, out);
-    WQ_HIP(h, hipGetLastError());
-    std::swap(h->st, h->st_next);
-    h->st.n = S_new;
-    return table_rebuild_derived(h);
+    // one in-place pass over every cube's list (wq_delta.hip); the state and any-keys go stale
+    if (n_rm == 0 || (h->st.n == 0 && !h->dstat_pending)) return WQ_OK;
+    return table_remove_peers_inplace(h, keys, n_rm);
 }
 
 // Per-cube lists, slot table and the (world, peer) "any" keys from the sorted state.

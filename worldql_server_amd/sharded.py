@@ -105,6 +105,11 @@ class DeviceShard:
     def apply_ops(self, ops: np.ndarray) -> None:
         self.router.apply_ops(ops)
 
+    def set_radius(self, radius: float, peer_pos) -> None:
+        """C5: every shard holds every peer's position; records then carry message positions."""
+        self.router.set_peer_positions(peer_pos)
+        self.router.set_radius(radius)
+
     def shard(self, pos, keys, world, sender, repl, n_shards: int):
         M = int(world.shape[0])
         recs = torch.empty((M, abi.MSG_REC_DTYPE.itemsize), dtype=torch.uint8, device=self.device)
