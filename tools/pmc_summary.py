@@ -46,7 +46,7 @@ def main():
         out = {"messages_per_tick": a.M, "pairs_per_tick": a.P,
                "hbm_bytes_per_launch": fetch + write, "fetch_bytes_corrected": fetch, "write_bytes": write,
                "kernels": route,
-               "note": "sum over the tick's count + tile_scan + emit launches; FETCH_SIZE (KB) x 1024 x 2 "
+               "note": "sum over the tick's launches (default: the single tick_kernel); FETCH_SIZE (KB) x 1024 x 2 "
                        "(gfx950 128-B requests tallied at 64 B), WRITE_SIZE (KB) x 1024"}
         with open(a.json, "w") as f:
             json.dump(out, f, indent=1)

@@ -87,7 +87,7 @@ __device__ __forceinline__ uint32_t row_scan(uint32_t e, uint32_t* wave_tot, uin
 template <int STAGE, int U = 8, bool RADIUS = false>
 __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView& tv, const EmitOut& o, uint32_t m0,
                                          uint32_t e, uint2 inf, uint32_t st, uint64_t g0, uint32_t T) {
-    static_assert(STAGE % 1024 == 0, "STAGE: whole quads for every lane");
+    static_assert(STAGE % 4 == 0, "STAGE: whole 16-byte quads");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid == 0) sm.n_gq = 0;
     lds_barrier();

@@ -92,7 +92,7 @@ typedef uint32_t u32_a1 __attribute__((aligned(1)));
 template <bool RAW_KEYS, int STAGE, int U>
 __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
     // U: record lines in flight per lane in the fallback emit_row
-    static_assert(STAGE % 1024 == 0, "STAGE: whole quads for every lane");
+    static_assert(STAGE % 4 == 0, "STAGE: whole 16-byte quads");
     __shared__ TickSmem<STAGE> sm;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const TableView& tv = p.t;

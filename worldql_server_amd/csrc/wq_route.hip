@@ -1,26 +1,16 @@
-// wq_route.hip — the LocalMessage hot path on gfx950: one tick of messages in three launches.
+// wq_route.hip — the LocalMessage hot path on gfx950: launch selection for one tick.
 //
 // Replaces, per message, worldql_server/src/processing/local_message.rs:52-86:
 //   world_map.get(world) -> Vector3::to_cube_area (cube_area.rs:72-77 -> coord_clamp :23-44)
 //   -> AreaMap::get_subscribed_peers (area_map.rs:52-60) -> replication filter (:60-86).
 //
-// 1. count_kernel   quantise (kernel 1) + exact packed key per message (one lane per message,
-//                   coalesced inputs), then the table probe (kernel 2) with EIGHT lanes per
-//                   message: one coalesced 128-byte load of the bucket record line (key, count,
-//                   28 inline peers) per 8 lanes, the sender compared against the inline peers
-//                   in parallel and reduced with lane shuffles. Writes the filtered count e_m,
-//                   an 8-byte locator (record slot + count / list offset / "the sender itself",
-//                   skipped index) and the block's total. No inter-block waits.
-// 2. tile_scan      one block scans the block totals (C2: 1,954 values) -> tile_prefix[], P.
-// 3. emit_kernel    CSR offsets = tile_prefix + a block-local scan of e_m, then the
-//                   load-balanced expand + compaction (kernel 3): a tile stages its messages'
-//                   inline peer lists in LDS (8 lanes per record line again; the table is
-//                   Infinity-Cache resident since pass 1), marks each message's first output in
-//                   an LDS owner array, max-scans it, and writes output j with thread j % 256 —
-//                   one coalesced stream per tile whatever the fan-out skew.
-// A single fused launch was measured first: its decoupled look-back made
-// every tile wait for the slowest earlier tile's probes (p50 13 us, max 47 us per tile), capping
-// it at 115-135 us per C2 tick. The split re-reads the record lines once and removes every wait.
+// Default: ONE launch (route_tick.hpp: count from the whole record line held in registers, block
+// scan, LDS image of the block's outputs, decoupled look-back, aligned 16-byte copy-out). Other
+// compiled shapes, selectable with wq_debug_set_route_config and identical in output: the same
+// single launch with other image sizes, and three launches (route_count.hpp count_kernel,
+// route_scan.hpp tile_scan_kernel, route_emit.hpp emit_kernel) which re-read the record lines
+// once but never wait on another block. The radius filter (route_radius.hpp) always takes three
+// launches. DESIGN.md §4-5 has the measurements behind each choice.
 // Output: CSR offsets[M+1] (message-major), peers[P], optional msgs[P].
 #include <algorithm>
 
@@ -67,11 +57,13 @@ void launch_tick(const TickParams& p, hipStream_t s, unsigned grid) {
 // Three launches: count (messages per lane, min waves per SIMD) / tile_scan / emit. One launch:
 // messages per block; its three-launch fallback (too many blocks to be resident) is count 4/2.
 const Cfg kCfgs[] = {
-    WQ_CFG1(3072, 2),         // 0: default, single launch (63 us on C2)
+    WQ_CFG1(2816, 2),         // 0: default, single launch; 20.3 KB LDS -> 8 blocks per CU (63.3 us on C2)
     WQ_CFG3(1, 8, 4096 + 2),  // 1: three launches (73 us on C2)
     WQ_CFG1(4096, 2),         // 2
     WQ_CFG3(1, 8, 4096 + 8),  // 3
     WQ_CFG3(4, 2, 4096 + 2),  // 4
+    WQ_CFG1(3072, 2),         // 5: 21.6 KB LDS -> 7 blocks per CU (65.6 us)
+    WQ_CFG1(2560, 2),         // 6: C2 blocks overflow the image (78 us)
 };
 #undef WQ_CFG1
 #undef WQ_CFG3
