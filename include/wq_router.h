@@ -214,6 +214,16 @@ int wq_route_records_device(wq_router* h, const wq_msg_rec* d_recs, size_t n_msg
                             uint32_t* d_peers, uint32_t* d_msgs, size_t capacity,
                             wq_route_counters* d_counters);
 
+/* ---- F2: per-peer send lists (PeerMap::broadcast_to, worldql_server/src/transport/peer_map.rs:151-163)
+ * The transpose of a tick's message-major CSR for a transport that batches per peer: for every
+ * peer p < n_peers whose bit is set in d_connected (bit p % 32 of word p / 32; NULL = every peer
+ * connected) the messages it must receive, ascending — the reference's "recipients intersected
+ * with the connected peers". d_peer_offsets[n_peers + 1]; d_msgs_out[n_pairs] (the kept ones
+ * first: d_peer_offsets[n_peers] of them). n_pairs = d_offsets[n_msgs]. Asynchronous. */
+int wq_peer_major_device(wq_router* h, const uint32_t* d_offsets, const uint32_t* d_peers, size_t n_msgs,
+                         size_t n_pairs, const uint32_t* d_connected, uint32_t n_peers,
+                         uint32_t* d_peer_offsets, uint32_t* d_msgs_out);
+
 /* ---- instrumentation ----
  * When enabled, every route launch is bracketed by HIP events on the launch stream;
  * wq_profile_read returns the summed kernel-only milliseconds and launch count (and resets). */

@@ -24,6 +24,8 @@ int launch_shard_messages(wq_router* h, const double* d_pos, const int64_t* d_ke
 int launch_op_owner(wq_router* h, const wq_op* d_ops, size_t n, uint32_t G, uint32_t* d_owner);
 int launch_route_records(wq_router* h, const wq_msg_rec* d_recs, size_t M, uint32_t* d_offsets, uint32_t* d_peers,
                          uint32_t* d_msgs, size_t capacity);
+int launch_peer_major(wq_router* h, const uint32_t* d_offsets, const uint32_t* d_peers, size_t M, size_t P,
+                      const uint32_t* d_connected, uint32_t n_peers, uint32_t* d_peer_offsets, uint32_t* d_msgs_out);
 int launch_route_global(wq_router* h, const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
                         size_t M, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity);
 }  // namespace wq
@@ -399,6 +401,17 @@ int wq_route_records_device(wq_router* h, const wq_msg_rec* d_recs, size_t n_msg
         WQ_HIP(h, hipMemcpyAsync(d_counters, h->rws.last, sizeof(wq_route_counters), hipMemcpyDeviceToDevice,
                                  h->stream));
     return WQ_OK;
+}
+
+int wq_peer_major_device(wq_router* h, const uint32_t* d_offsets, const uint32_t* d_peers, size_t n_msgs,
+                         size_t n_pairs, const uint32_t* d_connected, uint32_t n_peers, uint32_t* d_peer_offsets,
+                         uint32_t* d_msgs_out) {
+    if (!h || !d_peer_offsets || (n_msgs && !d_offsets) || (n_pairs && (!d_peers || !d_msgs_out)) ||
+        n_peers == 0xFFFFFFFFu || n_pairs > 0xFFFFFFFFull || n_msgs >= 0xFFFFFFFFull)
+        return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    return launch_peer_major(h, d_offsets, d_peers, n_msgs, n_pairs, d_connected, n_peers, d_peer_offsets,
+                             d_msgs_out);
 }
 
 int wq_is_subscribed(wq_router* h, size_t n, const uint32_t* world, const uint32_t* peer, int key_is_raw,

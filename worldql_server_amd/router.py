@@ -57,6 +57,7 @@ def load_library(build_if_missing: bool = True):
         "wq_route_tick_device": ([vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, vp], i32),
         "wq_route_global": ([vp, vp, vp, vp, sz, vp, vp, vp, sz, ctypes.POINTER(sz)], i32),
         "wq_route_global_device": ([vp, vp, vp, vp, sz, vp, vp, vp, sz, vp], i32),
+        "wq_peer_major_device": ([vp, vp, vp, sz, sz, vp, u32, vp, vp], i32),
         "wq_is_subscribed": ([vp, sz, vp, vp, i32, vp, vp], i32),
         "wq_is_subscribed_any": ([vp, sz, vp, vp, vp], i32),
         "wq_world_peers": ([vp, u32, vp, sz, ctypes.POINTER(sz)], i32),
@@ -213,6 +214,13 @@ class Router:
         self._check(self.lib.wq_route_global_device(self.h, world_ptr, sender_ptr, repl_ptr, n_msgs, offsets_ptr,
                                                     peers_ptr or None, msgs_ptr or None, capacity,
                                                     counters_ptr or None))
+
+    def peer_major_device(self, offsets_ptr: int, peers_ptr: int | None, n_msgs: int, n_pairs: int,
+                          connected_ptr: int | None, n_peers: int, peer_offsets_ptr: int, msgs_out_ptr: int | None):
+        """Per-peer send lists of a tick's CSR, disconnected peers dropped (peer_map.rs:151-163)."""
+        self._check(self.lib.wq_peer_major_device(self.h, offsets_ptr or None, peers_ptr or None, n_msgs, n_pairs,
+                                                  connected_ptr or None, n_peers, peer_offsets_ptr,
+                                                  msgs_out_ptr or None))
 
     # ---- multi-GPU (cube-hash ownership; driven by sharded.py) ----
     def shard_ops(self, ops: np.ndarray, n_shards: int) -> np.ndarray:
