@@ -11,16 +11,19 @@
 //   count   one lane per message: two binary searches give the world's range and the sender's
 //           rank inside it; e and a locator {range start, skipped rank};
 //   scan    tile_scan_kernel over the 256-message tiles (route_scan.hpp);
-//   emit    one block per tile: CSR offsets, then the tile's outputs as one flat block-strided
-//           range (owner by a forward walk over the tile's starts), copied from the any-keys with
-//           coalesced loads and stores — a world's range is contiguous, so a 50k-peer world is a
-//           streaming copy.
+//   offsets one block per tile: the tile prefix + an in-tile scan;
+//   copy    the whole tick's outputs as one flat range over a persistent grid (owner by binary
+//           search over the offsets), copied from the any-keys with coalesced loads and stores —
+//           a world's range is contiguous, so even one message to a 50k-peer world is a streaming
+//           copy spread over every CU.
 #include "route_scan.hpp"
 #include "wq_internal.hpp"
 
 namespace wq {
 
 namespace {
+
+constexpr unsigned kCopyGrid = 2048;  // persistent copy grid: 8 blocks per CU
 
 __device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t* a, uint64_t n, uint64_t v) {
     uint64_t lo = 0, hi = n;
@@ -106,57 +109,41 @@ __global__ __launch_bounds__(kBlock) void global_count_kernel(GlobalParams p) {
     }
 }
 
-__global__ __launch_bounds__(kBlock) void global_emit_kernel(GlobalParams p) {
-    __shared__ uint32_t s_st[kBlock + 1];
-    __shared__ uint2 s_inf[kBlock];
+// CSR offsets: the tile's prefix (tile_scan) + an in-tile exclusive scan of e.
+__global__ __launch_bounds__(kBlock) void global_offsets_kernel(GlobalParams p) {
     __shared__ uint32_t s_wave[kWaves];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t m0 = blockIdx.x * kBlock, m = m0 + tid;
+    const uint32_t m = blockIdx.x * kBlock + tid;
     const uint32_t e = m < p.M ? p.e[m] : 0u;
-    const uint2 inf = (m < p.M && p.peers) ? p.info[m] : make_uint2(0, kNone);
-    const uint32_t g0 = p.tile_prefix[blockIdx.x];
     const uint32_t incl = wave_incl_scan_add(e, lane);
     if (lane == 63) s_wave[wave] = incl;
     lds_barrier();
-    uint32_t before = 0, T = 0;
+    uint32_t before = 0;
 #pragma unroll
-    for (int u = 0; u < kWaves; ++u) {
+    for (int u = 0; u < kWaves; ++u)
         if (u < wave) before += s_wave[u];
-        T += s_wave[u];
-    }
-    const uint32_t st = before + incl - e;
-    if (m < p.M) p.offsets[m] = g0 + st;
-    if (!p.peers) return;
-    s_st[tid] = st;
-    s_inf[tid] = inf;
-    if (tid == 0) s_st[kBlock] = T;
-    lds_barrier();
-    uint32_t j = 0;
-    for (uint32_t k0 = tid; k0 < T; k0 += 4 * kBlock) {
-        uint32_t val[4], own[4];
-        bool ok[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t k = k0 + u * kBlock;
-            ok[u] = k < T;
-            if (!ok[u]) continue;
-            while (s_st[j + 1] <= k) ++j;  // owners ascend with k (empty messages are skipped)
-            const uint2 f = s_inf[j];
-            const uint32_t oi = k - s_st[j];
-            if (f.x == kLocSelf) {
-                val[u] = p.sender[m0 + j];
-            } else {
-                val[u] = (uint32_t)p.any[(uint64_t)f.x + oi + (oi >= f.y ? 1u : 0u)];
-            }
-            own[u] = m0 + j;
+    if (m < p.M) p.offsets[m] = p.tile_prefix[blockIdx.x] + before + incl - e;
+}
+
+// The outputs as one flat range over a persistent grid: output k belongs to the last message whose
+// offset is <= k (binary search over the offsets, L2-resident), and is copied from that world's
+// contiguous any-key range — so one message to a 50k-peer world spreads over the whole GPU.
+__global__ __launch_bounds__(kBlock) void global_copy_kernel(GlobalParams p) {
+    const uint32_t P = p.offsets[p.M];
+    const uint64_t lim = P < p.capacity ? P : p.capacity;
+    for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < lim; k += (uint64_t)gridDim.x * kBlock) {
+        uint32_t lo = 0, hi = p.M - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (p.offsets[mid] <= k)
+                lo = mid;
+            else
+                hi = mid - 1;
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint64_t out = (uint64_t)g0 + k0 + u * kBlock;
-            if (!ok[u] || out >= p.capacity) continue;
-            p.peers[out] = val[u];
-            if (p.msgs) p.msgs[out] = own[u];
-        }
+        const uint2 f = p.info[lo];
+        const uint32_t oi = (uint32_t)k - p.offsets[lo];
+        p.peers[k] = f.x == kLocSelf ? p.sender[lo] : (uint32_t)p.any[(uint64_t)f.x + oi + (oi >= f.y ? 1u : 0u)];
+        if (p.msgs) p.msgs[k] = lo;
     }
 }
 
@@ -204,7 +191,8 @@ int launch_route_global(wq_router* h, const uint32_t* d_world, const uint32_t* d
     sp.cnt = cur;
     hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, sp);
     WQ_HIP(h, hipGetLastError());
-    hipLaunchKernelGGL(global_emit_kernel, dim3(n_tiles), dim3(kBlock), 0, s, gp);
+    hipLaunchKernelGGL(global_offsets_kernel, dim3(n_tiles), dim3(kBlock), 0, s, gp);
+    if (gp.peers) hipLaunchKernelGGL(global_copy_kernel, dim3(kCopyGrid), dim3(kBlock), 0, s, gp);
     WQ_HIP(h, hipGetLastError());
     rw.calls++;
     return WQ_OK;
