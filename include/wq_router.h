@@ -233,6 +233,9 @@ int wq_profile_read(wq_router* h, double* kernel_ms, uint64_t* launches);
 /* ---- test hook: keep only the low `bits` bits of the 64-bit cube hash (64 = normal).
  * Forces bucket collisions so the exact-compare fallback paths are exercised. */
 int wq_debug_set_hash_bits(wq_router* h, int bits);
+/* ---- tuning hook: record slots per cube at the next full build (default 8: load <= 1/8). More
+ * slots = fewer displaced keys (fewer second probe rounds) for more HBM. */
+int wq_debug_set_record_slack(wq_router* h, uint32_t slots_per_cube);
 /* ---- test hook: how many op batches took the incremental update (wq_delta.hip), how many
  * tried it but fell back to the full rebuild (irregular keys, list space, record load), and how
  * many incremental batches needed the per-lane path (a cube with > 256 peers or > 64 changes). */

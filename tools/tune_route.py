@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--no-check", action="store_true", help="timing-only configs (wrong outputs)")
     ap.add_argument("--raw-keys", action="store_true", help="route pre-quantised keys (skips kernel 1)")
+    ap.add_argument("--slack", type=int, default=8, help="record slots per cube (wq_debug_set_record_slack)")
     a = ap.parse_args()
     import torch
     from worldql_server_amd import abi, synth
@@ -28,6 +29,7 @@ def main():
     r = Router(16, 0)
     s = torch.cuda.Stream(device=dev)
     r.set_stream(s.cuda_stream)
+    r.set_record_slack(a.slack)
     r.apply_ops(w.ops)
     pos = torch.from_numpy(w.pos).to(dev)
     world = torch.from_numpy(w.world.view(np.int32)).to(dev)

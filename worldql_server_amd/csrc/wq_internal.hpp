@@ -103,6 +103,7 @@ struct wq_router {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     uint64_t hash_mask = ~0ull;
+    uint32_t rec_slack = 8;  // record slots per cube at build (load <= 1/rec_slack)
     uint64_t hash_fallbacks = 0;
     std::string err;
 

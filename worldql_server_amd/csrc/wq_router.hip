@@ -209,6 +209,12 @@ int wq_debug_set_timeline(wq_router* h, uint64_t* d_stamps) {
     return WQ_OK;
 }
 
+int wq_debug_set_record_slack(wq_router* h, uint32_t slots_per_cube) {
+    if (!h || slots_per_cube < 2 || slots_per_cube > 1024) return WQ_E_INVALID;
+    h->rec_slack = slots_per_cube;  // takes effect at the next rebuild
+    return WQ_OK;
+}
+
 int wq_debug_set_hash_bits(wq_router* h, int bits) {
     if (!h || bits < 1 || bits > 64) return WQ_E_INVALID;
     if (h->st.n) return set_error(h, WQ_E_INVALID, "hash bits can only change on an empty table");

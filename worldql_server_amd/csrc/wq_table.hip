@@ -413,7 +413,7 @@ int table_rebuild_derived(wq_router* h) {
     // untouched slots cost memory, not time: a tick touches one line per cube whatever the capacity
     uint64_t rcap = 1024;
     int log2r = 10;
-    while (rcap < 8ull * n_cubes) {
+    while (rcap < (uint64_t)h->rec_slack * n_cubes) {
         rcap <<= 1;
         log2r++;
     }

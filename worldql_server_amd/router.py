@@ -66,6 +66,7 @@ def load_library(build_if_missing: bool = True):
         "wq_profile_enable": ([vp, i32], i32),
         "wq_profile_read": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)], i32),
         "wq_debug_set_hash_bits": ([vp, i32], i32),
+        "wq_debug_set_record_slack": ([vp, u32], i32),
         "wq_debug_set_route_config": ([vp, i32], i32),
         "wq_debug_route_config_count": ([], i32),
         "wq_debug_set_timeline": ([vp, vp], i32),
@@ -290,6 +291,9 @@ class Router:
         a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         self._check(self.lib.wq_debug_update_counts(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         return (a.value, b.value, c.value) if lanes else (a.value, b.value)
+
+    def set_record_slack(self, slots_per_cube: int) -> None:
+        self._check(self.lib.wq_debug_set_record_slack(self.h, slots_per_cube))
 
     def route_config_count(self) -> int:
         return int(self.lib.wq_debug_route_config_count())
