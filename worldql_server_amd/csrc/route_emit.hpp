@@ -25,11 +25,10 @@ struct EmitParams {
 
 // LDS of one emit row (256 messages): an image of a window of the row's output, aligned to
 // 16-byte quads of the global output, and the messages whose list is read from `list`.
-template <int STAGE>
-struct EmitRowSmem {
-    alignas(16) uint32_t op[STAGE];  // peers of window positions, in output order
-    alignas(16) uint8_t om[STAGE];   // ... and the row-local index of each position's message
-    uint32_t gq_j[kBlock];    // messages with more than kInline peers (or a full-key slot-table cube)
+// The long-list queue of one row (messages with more than kInline peers or a full-key slot-table
+// cube) and the row scan's wave totals.
+struct EmitQueue {
+    uint32_t gq_j[kBlock];    // message (row-local index)
     uint32_t gq_off[kBlock];  // ... index of the list's first peer in `list`
     uint32_t gq_skip[kBlock]; // ... skipped list index or kNone (radius mode: the list length)
     uint32_t gq_e[kBlock];    // ... outputs
@@ -37,6 +36,13 @@ struct EmitRowSmem {
     uint32_t gq_pre[kBlock + 1];  // ... prefix of their slices of the current window
     uint32_t scan_tot[kWaves];
     uint32_t n_gq;
+};
+
+template <int STAGE>
+struct EmitRowSmem {
+    alignas(16) uint32_t op[STAGE];  // peers of window positions, in output order
+    alignas(16) uint8_t om[STAGE];   // ... and the row-local index of each position's message
+    EmitQueue q;
 };
 
 struct EmitOut {
@@ -85,23 +91,23 @@ __device__ __forceinline__ uint32_t row_scan(uint32_t e, uint32_t* wave_tot, uin
 //   OnlySelf: the sender, by its own lane.
 // Every thread of the block must call it (it contains barriers); it ends with a barrier.
 template <int STAGE, int U = 8, bool RADIUS = false>
-__device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView& tv, const EmitOut& o, uint32_t m0,
+__device__ __forceinline__ void emit_row_img(uint32_t* op, uint8_t* om, EmitQueue& q_, const TableView& tv, const EmitOut& o, uint32_t m0,
                                          uint32_t e, uint2 inf, uint32_t st, uint64_t g0, uint32_t T) {
     static_assert(STAGE % 4 == 0, "STAGE: whole 16-byte quads");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) sm.n_gq = 0;
+    if (tid == 0) q_.n_gq = 0;
     lds_barrier();
     uint32_t sl = kNone, cnt = 0, skip = kNone;  // radius mode: skip holds the survivor mask
     const bool self = !RADIUS && e && (inf.x & kLocSelf);
     const uint32_t self_peer = self ? o.sender[m0 + tid] : 0u;
     if (e && !self) {
         if (inf.x & kLocGlobal) {
-            const uint32_t q = atomicAdd(&sm.n_gq, 1u);
-            sm.gq_j[q] = tid;
-            sm.gq_off[q] = (inf.x & ~kLocGlobal) + 1;
-            sm.gq_skip[q] = inf.y;
-            sm.gq_e[q] = e;
-            sm.gq_st[q] = st;
+            const uint32_t q = atomicAdd(&q_.n_gq, 1u);
+            q_.gq_j[q] = tid;
+            q_.gq_off[q] = (inf.x & ~kLocGlobal) + 1;
+            q_.gq_skip[q] = inf.y;
+            q_.gq_e[q] = e;
+            q_.gq_st[q] = st;
         } else {
             const uint32_t s24 = inf.y & kSkipNone24;
             sl = inf.x;
@@ -114,7 +120,7 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
     const int grp = lane >> 3, part = lane & 7;
     const uint4* recs4 = reinterpret_cast<const uint4*>(tv.recs);
     lds_barrier();
-    const uint32_t n_gq = sm.n_gq;
+    const uint32_t n_gq = q_.n_gq;
     // window w covers global outputs [gA + w0, gA + w0 + STAGE), gA = g0 rounded down to a quad
     const uint64_t gA = g0 & ~3ull;
     const uint32_t lead = (uint32_t)(g0 - gA);  // row output r sits at image index lead + r - w0
@@ -122,8 +128,8 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
     for (uint32_t w0 = 0; w0 < span; w0 += STAGE) {
         const uint32_t w1 = span - w0 < (uint32_t)STAGE ? span : w0 + STAGE;
         if (self && lead + st >= w0 && lead + st < w1) {
-            sm.op[lead + st - w0] = self_peer;
-            sm.om[lead + st - w0] = (uint8_t)tid;
+            op[lead + st - w0] = self_peer;
+            om[lead + st - w0] = (uint8_t)tid;
         }
 #pragma unroll 1
         for (int r0 = 0; r0 < 8; r0 += U) {
@@ -156,8 +162,8 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
                         pos = lead + q_st[u] + idx - (idx > q_skip[u] && q_skip[u] != kNone ? 1u : 0u);
                     }
                     if (pos >= w0 && pos < w1) {
-                        sm.op[pos - w0] = vv[i];
-                        sm.om[pos - w0] = j;
+                        op[pos - w0] = vv[i];
+                        om[pos - w0] = j;
                     }
                 }
             }
@@ -166,9 +172,9 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
             if (RADIUS) {
                 // re-filter each long list chunk by chunk, compacting survivors block-wide
                 for (uint32_t q = 0; q < n_gq; ++q) {
-                    const uint32_t j = sm.gq_j[q], s0 = lead + sm.gq_st[q], ej = sm.gq_e[q];
+                    const uint32_t j = q_.gq_j[q], s0 = lead + q_.gq_st[q], ej = q_.gq_e[q];
                     if (s0 >= w1 || s0 + ej <= w0) continue;  // block-uniform
-                    const uint32_t off = sm.gq_off[q], len = sm.gq_skip[q];
+                    const uint32_t off = q_.gq_off[q], len = q_.gq_skip[q];
                     const uint32_t m = m0 + j, me = o.sender[m];
                     const uint8_t rp = o.repl[m];
                     const double mx = o.pos[3ull * m], my = o.pos[3ull * m + 1], mz = o.pos[3ull * m + 2];
@@ -178,11 +184,11 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
                         const uint32_t peer = i < len ? tv.list[off + i] : 0u;
                         const bool ok = i < len && repl_keeps(rp, peer, me) && within_radius(tv, mx, my, mz, peer);
                         uint32_t tot;
-                        const uint32_t at = row_scan(ok ? 1u : 0u, sm.scan_tot, &tot);
+                        const uint32_t at = row_scan(ok ? 1u : 0u, q_.scan_tot, &tot);
                         const uint32_t pos = s0 + run + at;
                         if (ok && pos >= w0 && pos < w1) {
-                            sm.op[pos - w0] = peer;
-                            sm.om[pos - w0] = (uint8_t)j;
+                            op[pos - w0] = peer;
+                            om[pos - w0] = (uint8_t)j;
                         }
                         run += tot;
                         lds_barrier();  // scan_tot reuse
@@ -193,15 +199,15 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
                 if (tid == 0) {
                     uint32_t acc = 0;
                     for (uint32_t q = 0; q < n_gq; ++q) {
-                        const uint32_t s0 = lead + sm.gq_st[q], ej = sm.gq_e[q];
+                        const uint32_t s0 = lead + q_.gq_st[q], ej = q_.gq_e[q];
                         const uint32_t lo = s0 > w0 ? s0 : w0, hi = s0 + ej < w1 ? s0 + ej : w1;
-                        sm.gq_pre[q] = acc;
+                        q_.gq_pre[q] = acc;
                         acc += hi > lo ? hi - lo : 0u;
                     }
-                    sm.gq_pre[n_gq] = acc;
+                    q_.gq_pre[n_gq] = acc;
                 }
                 lds_barrier();
-                const uint32_t W = sm.gq_pre[n_gq];
+                const uint32_t W = q_.gq_pre[n_gq];
                 uint32_t q = 0;
                 for (uint32_t k0 = tid; k0 < W; k0 += 4 * kBlock) {
                     uint32_t val[4], dst[4], jj[4];
@@ -211,20 +217,20 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
                         const uint32_t k = k0 + u * kBlock;
                         ok[u] = k < W;
                         if (!ok[u]) continue;
-                        while (sm.gq_pre[q + 1] <= k) ++q;  // owners ascend with k
-                        const uint32_t s0 = lead + sm.gq_st[q];
+                        while (q_.gq_pre[q + 1] <= k) ++q;  // owners ascend with k
+                        const uint32_t s0 = lead + q_.gq_st[q];
                         const uint32_t lo = s0 > w0 ? s0 : w0;
-                        const uint32_t posn = lo + (k - sm.gq_pre[q]);  // image-space position
-                        const uint32_t oi = posn - s0, sk = sm.gq_skip[q];
-                        val[u] = tv.list[sm.gq_off[q] + oi + (oi >= sk ? 1u : 0u)];
+                        const uint32_t posn = lo + (k - q_.gq_pre[q]);  // image-space position
+                        const uint32_t oi = posn - s0, sk = q_.gq_skip[q];
+                        val[u] = tv.list[q_.gq_off[q] + oi + (oi >= sk ? 1u : 0u)];
                         dst[u] = posn - w0;
-                        jj[u] = sm.gq_j[q];
+                        jj[u] = q_.gq_j[q];
                     }
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         if (!ok[u]) continue;
-                        sm.op[dst[u]] = val[u];
-                        sm.om[dst[u]] = (uint8_t)jj[u];
+                        op[dst[u]] = val[u];
+                        om[dst[u]] = (uint8_t)jj[u];
                     }
                 }
             }
@@ -232,8 +238,8 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
         lds_barrier();
         // copy-out, quad t of the window by thread t % 256
         for (uint32_t qd = w0 + 4u * tid; qd < w1; qd += 4u * kBlock) {
-            const uint4 pv = *reinterpret_cast<const uint4*>(&sm.op[qd - w0]);
-            const uint32_t mv = *reinterpret_cast<const uint32_t*>(&sm.om[qd - w0]);
+            const uint4 pv = *reinterpret_cast<const uint4*>(&op[qd - w0]);
+            const uint32_t mv = *reinterpret_cast<const uint32_t*>(&om[qd - w0]);
             const uint64_t out0 = gA + qd;
             const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
             const uint32_t mw[4] = {m0 + (mv & 0xFF), m0 + ((mv >> 8) & 0xFF), m0 + ((mv >> 16) & 0xFF), m0 + (mv >> 24)};
@@ -252,6 +258,12 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
         }
         lds_barrier();  // the next window (or the caller's next row) reuses the image
     }
+}
+
+template <int STAGE, int U = 8, bool RADIUS = false>
+__device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView& tv, const EmitOut& o, uint32_t m0,
+                                         uint32_t e, uint2 inf, uint32_t st, uint64_t g0, uint32_t T) {
+    emit_row_img<STAGE, U, RADIUS>(sm.op, sm.om, sm.q, tv, o, m0, e, inf, st, g0, T);
 }
 
 

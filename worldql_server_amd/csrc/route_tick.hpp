@@ -37,6 +37,7 @@ struct TickParams {
     wq_route_counters* cnt;
     wq_route_counters* cnt_next;
     uint64_t* stamps;   // diagnostics (wq_debug_set_timeline) or nullptr
+    uint32_t n_tiles;   // 256-message tiles (one block each)
 };
 
 constexpr uint32_t kErrSpin = 4u;
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
         p.cnt_next->overflow = 0;
         p.cnt_next->error = 0;
     }
-    if (tid == 0) sm.es.n_gq = 0;
+    if (tid == 0) sm.es.q.n_gq = 0;
 
     // ---- 1. count ----
     uint64_t F_local = 0;
@@ -141,12 +142,12 @@ __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
         uint32_t slot = kNone, meta = 0;
         if (e && !self) {
             if (inf.x & kLocGlobal) {
-                const uint32_t q = atomicAdd(&sm.es.n_gq, 1u);
-                sm.es.gq_j[q] = tid;
-                sm.es.gq_off[q] = (inf.x & ~kLocGlobal) + 1;
-                sm.es.gq_skip[q] = inf.y;
-                sm.es.gq_e[q] = e;
-                sm.es.gq_st[q] = st;
+                const uint32_t q = atomicAdd(&sm.es.q.n_gq, 1u);
+                sm.es.q.gq_j[q] = tid;
+                sm.es.q.gq_off[q] = (inf.x & ~kLocGlobal) + 1;
+                sm.es.q.gq_skip[q] = inf.y;
+                sm.es.q.gq_e[q] = e;
+                sm.es.q.gq_st[q] = st;
             } else {
                 const uint32_t s24 = inf.y & kSkipNone24;
                 slot = inf.x;
@@ -184,10 +185,10 @@ __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
             }
         }
         lds_barrier();  // the long-list queue is complete
-        const uint32_t n_gq = sm.es.n_gq;
+        const uint32_t n_gq = sm.es.q.n_gq;
         for (uint32_t q = 0; q < n_gq; ++q) {
-            const uint32_t j = sm.es.gq_j[q], s0 = sm.es.gq_st[q], ej = sm.es.gq_e[q];
-            const uint32_t off = sm.es.gq_off[q], sk = sm.es.gq_skip[q];
+            const uint32_t j = sm.es.q.gq_j[q], s0 = sm.es.q.gq_st[q], ej = sm.es.q.gq_e[q];
+            const uint32_t off = sm.es.q.gq_off[q], sk = sm.es.q.gq_skip[q];
             for (uint32_t k = tid; k < ej; k += kBlock) {
                 sm.es.op[s0 + k] = tv.list[off + k + (k >= sk ? 1u : 0u)];
                 sm.es.om[s0 + k] = (uint8_t)j;

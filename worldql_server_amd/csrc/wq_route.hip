@@ -143,6 +143,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         tp.cnt = cur;
         tp.cnt_next = nxt;
         tp.stamps = rw.stamps;
+        tp.n_tiles = (uint32_t)nb;
         cfg.tick(tp, s, (unsigned)nb);
         WQ_HIP(h, hipGetLastError());
         if (pr.enabled) {
