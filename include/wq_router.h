@@ -88,6 +88,11 @@ typedef struct wq_route_counters {
     uint32_t error;        /* 4: a bounded spin gave up (WQ_E_TIMEOUT); 2: P > 2^32-1 (WQ_E_CAPACITY) */
 } wq_route_counters;
 
+/* ---- pinned host memory for the host-array entry points: buffers from wq_host_alloc move over
+ * PCIe by DMA without a staging copy (pageable buffers work too, at a fraction of the rate). */
+int wq_host_alloc(size_t bytes, void** out);
+int wq_host_free(void* p);
+
 /* ---- lifetime: replaces WorldMap::new (world_map.rs:17-22) ---- */
 int wq_router_create(uint16_t cube_size, int device, wq_router** out);
 int wq_router_destroy(wq_router* h);

@@ -3,6 +3,7 @@
   F2  per-peer send lists of a C2 tick (10M pairs, 70% of peers connected)
   F3  REMOVE_PEER of 1% / 10% of the peers on a C4 GPU's table (8 worlds x 50k peers, 10.8M entries)
   F1  1,000 GlobalMessages to C4 worlds (each reaching a whole world's 50k peers)
+  and the C2 tick through the host-array entry point (PCIe-inclusive)
 Device time with HIP events on the router's stream; one JSON line per measurement."""
 import json
 import os
@@ -61,11 +62,51 @@ def main():
                                                po.data_ptr(), mo.data_ptr()))
     print(json.dumps({"path": "F2 per-peer send lists", "workload": "C2 tick", "pairs": P, "peers": N,
                       "connected": 0.7, "ms": round(ms, 3), "pairs_per_s": P / ms * 1e3}), flush=True)
+    # the host-array boundary: wq_route_tick copies the inputs in and the CSR out over PCIe
+    r.set_stream(None)
+    out = r.route(w.pos, w.world, w.sender, w.repl, with_msgs=True)
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        out = r.route(w.pos, w.world, w.sender, w.repl, with_msgs=True)
+        ts.append((time.perf_counter() - t0) * 1e3)
+    ms = float(np.median(ts))
+    print(json.dumps({"path": "C2 tick through the host-array ABI (wq_route_tick: H2D inputs, D2H offsets, peers, msgs), pageable numpy arrays",
+                      "pairs": len(out[1]), "ms_wall": round(ms, 3), "pairs_per_s": len(out[1]) / ms * 1e3,
+                      "bytes_moved": int(M * 33 + (M + 1) * 4 + 8 * len(out[1]))}), flush=True)
+    import ctypes
+    from worldql_server_amd.router import PinnedArray
+    Pn = len(out[1])
+    pin = {k: PinnedArray(v.shape, v.dtype) for k, v in
+           (("pos", w.pos), ("world", w.world), ("sender", w.sender), ("repl", w.repl))}
+    for k, v in (("pos", w.pos), ("world", w.world), ("sender", w.sender), ("repl", w.repl)):
+        pin[k].array[...] = v
+    o_off, o_peers, o_msgs = PinnedArray((M + 1,), np.uint32), PinnedArray((Pn,), np.uint32), PinnedArray((Pn,), np.uint32)
+    n = ctypes.c_size_t()
+    vp = lambda a: ctypes.c_void_p(a.ptr.value)
+    ts = []
+    for _ in range(6):
+        t0 = time.perf_counter()
+        rc = r.lib.wq_route_tick(r.h, vp(pin["pos"]), None, vp(pin["world"]), vp(pin["sender"]), vp(pin["repl"]), M,
+                                 vp(o_off), vp(o_peers), vp(o_msgs), Pn, ctypes.byref(n))
+        ts.append((time.perf_counter() - t0) * 1e3)
+        assert rc == 0 and n.value == Pn
+    assert (o_peers.array == out[1]).all()
+    ms = float(np.median(ts[1:]))
+    print(json.dumps({"path": "C2 tick through the host-array ABI, pinned buffers (wq_host_alloc)", "pairs": Pn,
+                      "ms_wall": round(ms, 3), "pairs_per_s": Pn / ms * 1e3,
+                      "GB_per_s_pcie": (M * 33 + (M + 1) * 4 + 8 * Pn) / ms / 1e6}), flush=True)
+    for a in list(pin.values()) + [o_off, o_peers, o_msgs]:
+        a.close()
     r.close()
 
     # F3 and F1 on a C4 GPU's table
     c4 = synth_ext.config_c4(1.0, worlds=range(8))
     init = c4.initial_ops()
+    warm = Router(16, 0)  # first use of the REMOVE_PEER kernels loads their code object: not timed
+    warm.apply_ops(init[:27])
+    warm.remove_peers(np.array([0], np.uint32))
+    warm.close()
     for frac in (0.01, 0.10):
         r = Router(16, 0)
         r.set_stream(s.cuda_stream)

@@ -89,6 +89,17 @@ int read_back(wq_router* h, size_t M, const char* dout, size_t op, size_t om, si
 
 extern "C" {
 
+int wq_host_alloc(size_t bytes, void** out) {
+    if (!out || bytes == 0) return WQ_E_INVALID;
+    *out = nullptr;
+    return hipHostMalloc(out, bytes, hipHostMallocDefault) == hipSuccess ? WQ_OK : WQ_E_OOM;
+}
+
+int wq_host_free(void* p) {
+    if (!p) return WQ_E_INVALID;
+    return hipHostFree(p) == hipSuccess ? WQ_OK : WQ_E_HIP;
+}
+
 int wq_router_create(uint16_t cube_size, int device, wq_router** out) {
     if (!out || cube_size == 0) return WQ_E_INVALID;  // args.rs: cube_size is NonZeroU16
     *out = nullptr;

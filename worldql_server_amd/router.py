@@ -51,6 +51,8 @@ def load_library(build_if_missing: bool = True):
         "wq_set_stream": ([vp, vp], i32),
         "wq_get_stats": ([vp, vp], i32),
         "wq_apply_ops": ([vp, vp, sz], i32),
+        "wq_host_alloc": ([sz, ctypes.POINTER(vp)], i32),
+        "wq_host_free": ([vp], i32),
         "wq_apply_ops_device": ([vp, vp, sz], i32),
         "wq_remove_peers": ([vp, vp, sz], i32),
         "wq_route_tick": ([vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, ctypes.POINTER(sz)], i32),
@@ -88,6 +90,34 @@ def load_library(build_if_missing: bool = True):
 
 def _p(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class PinnedArray:
+    """A numpy array over pinned host memory (wq_host_alloc): DMA-able by the host-array ABI."""
+
+    def __init__(self, shape, dtype):
+        self.lib = load_library()
+        dt = np.dtype(dtype)
+        n = int(np.prod(shape)) * dt.itemsize
+        p = ctypes.c_void_p()
+        rc = self.lib.wq_host_alloc(max(n, 1), ctypes.byref(p))
+        if rc != 0:
+            raise WQError(rc, "wq_host_alloc")
+        self.ptr = p
+        buf = (ctypes.c_uint8 * max(n, 1)).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=np.uint8, count=n).view(dt).reshape(shape)
+
+    def close(self):
+        if self.ptr:
+            self.array = None
+            self.lib.wq_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class WQStats(ctypes.Structure):
