@@ -96,29 +96,72 @@ def reduce_over_ranks(t_ms: float, pairs: int, dev, world_size: int):
     return float(t.item()), float(p.item())
 
 
-def cpu_baseline(w, seconds: float) -> dict:
-    """The C restatement (oracle/wq_oracle.c: hash map world -> cube -> peer set, one message at
-    a time), single thread, on a bounded sample of the same tick."""
+def _oracle_router(w):
+    """The C restatement with the workload's table, and a chunk router over wqo_route (no sorting
+    of recipients: the reference's AHashSet order is unordered too)."""
+    import ctypes
     from oracle import oracle as orc
     o = orc.COracle(w.cube_size)
     t0 = time.perf_counter()
     o.apply_ops(w.ops)
     build_s = time.perf_counter() - t0
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+
+    def run(lo_hi):
+        lo, hi = lo_hi
+        n = hi - lo
+        offs = np.empty(n + 1, np.uint32)
+        cap = 64 * n + 64
+        peers = np.empty(cap, np.uint32)
+        pos, wo = np.ascontiguousarray(w.pos[lo:hi]), np.ascontiguousarray(w.world[lo:hi])
+        se, rp = np.ascontiguousarray(w.sender[lo:hi]), np.ascontiguousarray(w.repl[lo:hi])
+        F = ctypes.c_uint64()
+        P = o.lib.wqo_route(o.h, vp(pos), None, vp(wo), vp(se), vp(rp), n, vp(offs), vp(peers), cap, ctypes.byref(F))
+        assert P <= cap
+        return P
+
+    return o, run, build_s
+
+
+def cpu_baseline(w, seconds: float) -> dict:
+    """The C restatement (oracle/wq_oracle.c: hash map world -> cube -> peer set, one message at
+    a time), single thread, on a bounded sample of the same tick (whole chunks of 100k messages
+    until `seconds` of routing have run)."""
+    o, run, build_s = _oracle_router(w)
     M = len(w.world)
     chunk = min(M, 100_000)
     pairs, msgs, t_route, start = 0, 0, 0.0, 0
     while t_route < seconds and msgs < M:
-        sl = slice(start, start + chunk)
         t0 = time.perf_counter()
-        offs, peers, _ = o.route(w.pos[sl], w.world[sl], w.sender[sl], w.repl[sl])
+        pairs += run((start, min(M, start + chunk)))
         t_route += time.perf_counter() - t0
-        pairs += len(peers)
-        msgs += len(w.world[sl])
+        msgs += min(M, start + chunk) - start
         start += chunk
+    o.close()
     return {"value": pairs / t_route, "unit": "pairs/s", "cores": 1, "kind": "port",
             "sample": f"{msgs} of the tick's {M} messages ({pairs} pairs) routed in {t_route:.2f} s by "
                       f"oracle/wq_oracle.c on 1 host thread; table of {len(w.ops)} subscriptions built "
                       f"in {build_s:.2f} s (not timed)"}
+
+
+def cpu_baseline_mt(w, threads: int) -> dict:
+    """SURVEY.md §8(d) cpu_ref_mt: the same C restatement, read-only lookups in parallel over
+    message chunks on `threads` host threads (ctypes releases the GIL during each call); the
+    whole tick is routed."""
+    from concurrent.futures import ThreadPoolExecutor
+    o, run, _ = _oracle_router(w)
+    M = len(w.world)
+    bounds = np.linspace(0, M, 4 * threads + 1).astype(np.int64)
+    chunks = [(int(bounds[i]), int(bounds[i + 1])) for i in range(len(bounds) - 1)]
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(run, chunks[:threads]))  # warm-up
+        t0 = time.perf_counter()
+        pairs = sum(ex.map(run, chunks))
+        t = time.perf_counter() - t0
+    o.close()
+    return {"value": pairs / t, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"the whole tick ({M} messages, {pairs} pairs) in {t:.3f} s by oracle/wq_oracle.c "
+                      f"on {threads} host threads (read-only lookups, {len(chunks)} chunks)"}
 
 
 def main():
@@ -245,6 +288,9 @@ def main():
     }
     if rank == 0 and world_size == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(w, a.cpu_seconds)
+        threads = min(16, os.cpu_count() or 1)
+        if threads > 1:
+            out["cpu_baseline_mt"] = cpu_baseline_mt(w, threads)
     if rank == 0:
         print(json.dumps(out), flush=True)
     r.close()

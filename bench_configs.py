@@ -185,24 +185,19 @@ def _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s):
 
 def _cpu_route_sample(w, seconds, name):
     """The C restatement on 1 host thread, routing a bounded prefix of the tick's messages."""
-    from oracle import oracle as orc
-    o = orc.COracle(w.cube_size)
-    t0 = time.perf_counter()
-    o.apply_ops(w.ops)
-    build_s = time.perf_counter() - t0
+    o, run, build_s = bench._oracle_router(w)
     M = len(w.world)
     chunk = min(M, 50_000)
     pairs = msgs = 0
     t_route = 0.0
     start = 0
     while t_route < seconds and start < M:
-        sl = slice(start, start + chunk)
         t0 = time.perf_counter()
-        _, peers, _ = o.route(w.pos[sl], w.world[sl], w.sender[sl], w.repl[sl])
+        pairs += run((start, min(M, start + chunk)))
         t_route += time.perf_counter() - t0
-        pairs += len(peers)
-        msgs += len(w.world[sl])
+        msgs += min(M, start + chunk) - start
         start += chunk
+    o.close()
     return {"value": pairs / t_route, "unit": "pairs/s", "cores": 1, "kind": "port",
             "sample": f"{name}: {msgs} of the tick's {M} messages ({pairs} pairs) routed in {t_route:.2f} s by "
                       f"oracle/wq_oracle.c on 1 host thread; table of {len(w.ops)} subscriptions built in "
@@ -324,14 +319,23 @@ def _cpu_churn_sample(init, ticks, world, seconds):
     wz = np.full(M, w0, np.uint32)
     sender = np.flatnonzero(sel).astype(np.uint32)
     repl = np.zeros(M, np.uint8)
+    import ctypes
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    offs = np.empty(M + 1, np.uint32)
+    cap = 128 * M
+    peers = np.empty(cap, np.uint32)
+    F = ctypes.c_uint64()
     pairs = n = 0
     t = 0.0
     for ops, pos in ticks:
+        mine = np.ascontiguousarray(ops[ops["world"] == w0])
+        mpos = np.ascontiguousarray(pos[sel])
         t0 = time.perf_counter()
-        o.apply_ops(ops[ops["world"] == w0])
-        _, peers, _ = o.route(pos[sel], wz, sender, repl)
+        o.lib.wqo_apply_ops(o.h, vp(mine), len(mine))
+        P = o.lib.wqo_route(o.h, vp(mpos), None, vp(wz), vp(sender), vp(repl), M, vp(offs), vp(peers), cap,
+                            ctypes.byref(F))
         t += time.perf_counter() - t0
-        pairs += len(peers)
+        pairs += P
         n += 1
         if t >= seconds:
             break
