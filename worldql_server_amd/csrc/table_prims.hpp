@@ -29,9 +29,8 @@ __global__ void k_gather(const T* __restrict__ src, const uint32_t* __restrict__
 
 // ---- rocPRIM wrappers (temp storage in h->sort_tmp) ----
 
-template <typename K>
-int sort_pairs(wq_router* h, const K* kin, K* kout, const uint32_t* vin, uint32_t* vout, uint64_t n,
-               int end_bit) {
+template <typename K, typename V = uint32_t>
+int sort_pairs(wq_router* h, const K* kin, K* kout, const V* vin, V* vout, uint64_t n, int end_bit) {
     size_t bytes = 0;
     WQ_HIP(h, rocprim::radix_sort_pairs(nullptr, bytes, kin, kout, vin, vout, (size_t)n, 0, end_bit,
                                         h->stream));

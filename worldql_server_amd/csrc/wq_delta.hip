@@ -1,26 +1,27 @@
-// wq_delta.hip — incremental subscribe / unsubscribe batches (SURVEY.md §8(d) C4 churn).
+// wq_delta.hip — incremental subscribe / unsubscribe batches (SURVEY.md §8(d) C4 churn) and
+// REMOVE_PEER in place (§8(f) F3).
 //
 // Same semantics as the full rebuild in wq_table.hip — per (world, cube, peer) the last op of the
 // batch wins (AreaMap::add_subscription / remove_subscription, area_map.rs:72-119, applied in
 // order by thread.rs:122-146) — but the work is proportional to the batch and the cubes it
-// touches, not to the whole table:
-//   events   each op -> (packed cube key pk, peer, kind); an op whose cube has no packed key
-//            (raw off-grid keys, huge coordinates, world ids >= 1023) sends the batch to the rebuild
-//   sort     stable radix sort by (pk, peer): runs of one (cube, peer), the last op of a run wins
-//   plan     one lane per touched cube: find its record, merge-walk the cube's ascending list
-//            against its ascending changes, and count the effective adds and removes
-//   apply    one lane per changed cube: a list that still fits its capacity is edited in place
-//            (forward compaction of the removals, then a backward merge of the adds — both safe
-//            in place); a list that outgrows it moves to bump-allocated space past the used part
-//            of `list`, with 50% headroom; a new cube claims a record slot on its probe path.
-//            The record's count, list offset, capacity, Bloom signature and inline peers are
-//            rewritten from the final list.
+// touches, not to the whole table. The group path (default):
+//   events   each op -> packed cube key and its record slot (a new cube claims its record here by
+//            CAS on the probe path, count 0), and a value kind << 32 | peer
+//   sort     one stable radix sort of the values by slot over log2(capacity) bits: every cube's
+//            ops are contiguous and in op order
+//   plan     one lane per touched cube reads the record header and reserves relocation space for
+//            old count + subscribes beyond the list's capacity (one host read-back of the totals)
+//   apply    16 lanes per cube merge the cube's ops (16 at a time, sorted by (peer, op) in
+//            registers, last op of a peer wins) into its list staged in LDS, then write the list
+//            (in place, or relocated past the used part of `list` with 50% headroom) and the whole
+//            record line (count, offset, capacity, Bloom signature, inline peers)
+// Cubes beyond the group bounds (old count + ops > 128) send the batch to the per-lane path:
+// sort by (pk, peer), one lane per cube, in-place forward compaction then backward merge.
 // A cube that empties keeps its record (count 0, key kept), so every probe sequence stays intact.
 // The sorted state `st` and the any-keys are left stale and regenerated from the records only
-// when something needs them (table_materialize / table_ensure_any): REMOVE_PEER, a full rebuild,
-// any-queries, GlobalMessage, stats. A batch falls back to the full rebuild (nothing changed) when
-// an op is not regular, the relocated lists would overflow `list`, or the record table would pass
-// load 1/4.
+// when something needs them (table_materialize / table_ensure_any). A batch falls back to the full
+// rebuild (no list changed) when an op is not regular, relocations would overflow `list`, or the
+// record table would pass load 1/4.
 #include <algorithm>
 
 #include "table_prims.hpp"
@@ -65,7 +66,7 @@ __device__ __forceinline__ void op_key(const wq_op& o, double sf, int64_t si, in
 // be grouped by slot with a short radix sort. The caller guarantees free slots (load <= 1/2).
 __global__ void k_delta_events(const wq_op* __restrict__ ops, uint32_t n, double sf, int64_t si, Record* recs,
                                uint64_t rmask, int rshift, uint64_t hmask, uint64_t* pk, uint32_t* slot,
-                               uint32_t* peer, uint8_t* kind, DeltaSummary* sum) {
+                               uint32_t* peer, uint8_t* kind, uint64_t* sv, DeltaSummary* sum) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const wq_op o = ops[i];
@@ -91,10 +92,12 @@ __global__ void k_delta_events(const wq_op* __restrict__ ops, uint32_t n, double
         }
         sl = (uint32_t)j;
     }
+    const uint32_t kd = o.kind == WQ_OP_SUBSCRIBE ? 1u : 0u;
     pk[i] = p;
     slot[i] = sl;
     peer[i] = o.peer;
-    kind[i] = o.kind == WQ_OP_SUBSCRIBE ? 1 : 0;
+    kind[i] = (uint8_t)kd;
+    sv[i] = ((uint64_t)kd << 32) | o.peer;  // sorted along with the slot: no gather afterwards
 }
 
 // Sorted order -> peer / kind columns and cube heads.
@@ -318,22 +321,16 @@ __device__ __forceinline__ uint32_t lds_lower_bound(const uint32_t* a, uint32_t 
     return lo;
 }
 
-__global__ void k_delta_mark_slot(const uint32_t* __restrict__ order, const uint32_t* __restrict__ sslot,
-                                  const uint32_t* __restrict__ peer, const uint8_t* __restrict__ kind, uint32_t n,
-                                  uint32_t* sp, uint8_t* skd, uint32_t* head) {
+__global__ void k_slot_heads(const uint32_t* __restrict__ sslot, uint32_t n, uint32_t* head) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t a = order[i];
-    sp[i] = peer[a];
-    skd[i] = kind[a];
-    head[i] = (i == 0 || sslot[i] != sslot[i - 1]) ? 1u : 0u;
+    if (i < n) head[i] = (i == 0 || sslot[i] != sslot[i - 1]) ? 1u : 0u;
 }
 
 // One lane per touched cube: {slot, first op, ops, old count} and the relocation reserve.
 __global__ __launch_bounds__(kBlock) void k_delta_plan_light(const Record* __restrict__ recs,
                                                              const uint32_t* __restrict__ cube_start,
                                                              const uint32_t* __restrict__ sslot,
-                                                             const uint8_t* __restrict__ skd,
+                                                             const uint64_t* __restrict__ svs,
                                                              const DeltaSummary* sum, uint32_t n, uint4* cinfo,
                                                              uint32_t* reloc, uint64_t* part) {
     __shared__ unsigned long long acc[4];
@@ -347,7 +344,7 @@ __global__ __launch_bounds__(kBlock) void k_delta_plan_light(const Record* __res
         const uint4* line = reinterpret_cast<const uint4*>(recs + slot);
         const uint32_t oc = line[0].z, cap = line[1].z;
         uint32_t subs = 0;  // only subscribes can grow the list
-        for (uint32_t t = s0; t < s0 + nch; ++t) subs += skd[t];
+        for (uint32_t t = s0; t < s0 + nch; ++t) subs += (uint32_t)(svs[t] >> 32);
         if ((uint64_t)oc + nch > kGroupList) atomicAdd(&acc[2], 1ull);
         const uint64_t ub = (uint64_t)oc + subs;
         if (ub > cap) rw = 1 + grown((uint32_t)std::min<uint64_t>(ub, 0x7FFFFFFFull));
@@ -366,8 +363,7 @@ struct GroupLds {
 };
 
 __global__ __launch_bounds__(kBlock) void k_delta_apply_group(DeltaTable tb, const uint4* __restrict__ cinfo,
-                                                              const uint32_t* __restrict__ sp,
-                                                              const uint8_t* __restrict__ skd,
+                                                              const uint64_t* __restrict__ svs,
                                                               const DeltaSummary* sum,
                                                               const uint32_t* __restrict__ reloc,
                                                               const uint32_t* __restrict__ reloc_off,
@@ -383,24 +379,41 @@ __global__ __launch_bounds__(kBlock) void k_delta_apply_group(DeltaTable tb, con
     int64_t de = 0, dl = 0;
     uint32_t* add = sm.add[grp];
     uint32_t* rem = sm.rem[grp];
-    for (uint32_t c = blockIdx.x * kGroups + grp; c < n_dc; c += gridDim.x * kGroups) {
-        const uint4 ci = cinfo[c];
+    const uint32_t stride = gridDim.x * kGroups;
+    const uint4* recs4 = reinterpret_cast<const uint4*>(tb.recs);
+    uint32_t c = blockIdx.x * kGroups + grp;
+    // this cube's plan and record header; the next cube's are fetched while this one merges
+    uint4 ci = make_uint4(0, 0, 0, 0), h0 = ci, h1 = ci;
+    if (c < n_dc) {
+        ci = cinfo[c];
+        h0 = recs4[8ull * ci.x];
+        h1 = recs4[8ull * ci.x + 1];
+    }
+    for (; c < n_dc; c += stride) {
+        const uint32_t cn = c + stride;
+        uint4 ci_n = ci;
+        if (cn < n_dc) ci_n = cinfo[cn];
         const uint32_t slot = ci.x, s0 = ci.y, nch = ci.z, oc = ci.w;
         Record* rec = tb.recs + slot;
-        const uint4 h0 = reinterpret_cast<const uint4*>(rec)[0];
-        const uint32_t off = h0.w, cap0 = reinterpret_cast<const uint4*>(rec)[1].z;
+        const uint32_t off = h0.w, cap0 = h1.z;
         uint32_t* cur = sm.buf[grp][0];
         uint32_t* nxt = sm.buf[grp][1];
         wave_lds_sync();  // the previous cube's LDS reads are done
         for (uint32_t k = gl; k < oc; k += kG) cur[k] = tb.list[off + 1 + k];
+        uint4 h0_n = h0, h1_n = h1;
+        if (cn < n_dc) {
+            h0_n = recs4[8ull * ci_n.x];
+            h1_n = recs4[8ull * ci_n.x + 1];
+        }
         wave_lds_sync();
         uint32_t n = oc;
         bool changed = false;
         for (uint32_t t0 = 0; t0 < nch; t0 += kG) {
             const uint32_t m = std::min<uint32_t>(kG, nch - t0);
             const bool has = (uint32_t)gl < m;
-            uint64_t key = has ? (((uint64_t)sp[s0 + t0 + gl] << 32) | (uint32_t)gl) : ~0ull;
-            const uint32_t kd = has ? skd[s0 + t0 + gl] : 0u;
+            const uint64_t v = has ? svs[s0 + t0 + gl] : 0ull;
+            uint64_t key = has ? ((v << 32) | (uint32_t)gl) : ~0ull;
+            const uint32_t kd = (uint32_t)(v >> 32);
 #pragma unroll
             for (int k = 2; k <= kG; k <<= 1) {
 #pragma unroll
@@ -439,7 +452,7 @@ __global__ __launch_bounds__(kBlock) void k_delta_apply_group(DeltaTable tb, con
             nxt = t;
             n = n + nadd - nrm;
         }
-        if (!changed) continue;
+        if (changed) {
         uint32_t dst = off, cap = cap0;
         const uint32_t rl = reloc[c];
         if (rl) {
@@ -478,6 +491,10 @@ __global__ __launch_bounds__(kBlock) void k_delta_apply_group(DeltaTable tb, con
             de += (int64_t)n - (int64_t)oc;
             dl += (int64_t)(oc == 0 && n > 0) - (int64_t)(oc > 0 && n == 0);
         }
+        }  // changed
+        ci = ci_n;
+        h0 = h0_n;
+        h1 = h1_n;
     }
     if (de) atomicAdd(&acc[0], (unsigned long long)de);
     if (dl) atomicAdd(&acc[1], (unsigned long long)dl);
@@ -714,21 +731,19 @@ int delta_plan_groups(wq_router* h, uint32_t n, DeltaSummary* sum) {
     const uint32_t nb = grid_for(n);
     int bits = 1;
     while ((1ull << bits) < t.rec_cap) bits++;
-    uint32_t* idx_a = h->idx_a.as<uint32_t>();
-    uint32_t* idx_b = h->idx_b.as<uint32_t>();
-    hipLaunchKernelGGL(k_iota, dim3(nb), dim3(kBlock), 0, s, idx_a, (uint64_t)n);
-    int rc = sort_pairs<uint32_t>(h, d.slot.as<uint32_t>(), h->key32_a.as<uint32_t>(), idx_a, idx_b, n, bits);
+    // (slot, kind << 32 | peer) sorted by slot, stable: each cube's ops stay in op order
+    int rc = sort_pairs<uint32_t, uint64_t>(h, d.slot.as<uint32_t>(), h->key32_a.as<uint32_t>(), d.sv.as<uint64_t>(),
+                                            d.svs.as<uint64_t>(), n, bits);
     if (rc) return rc;
     const uint32_t* sslot = h->key32_a.as<uint32_t>();
     uint32_t* head = h->flags.as<uint32_t>();
     uint32_t* cid = h->scan.as<uint32_t>();
-    hipLaunchKernelGGL(k_delta_mark_slot, dim3(nb), dim3(kBlock), 0, s, idx_b, sslot, d.peer.as<uint32_t>(),
-                       d.kind.as<uint8_t>(), n, d.sp.as<uint32_t>(), d.skd.as<uint8_t>(), head);
+    hipLaunchKernelGGL(k_slot_heads, dim3(nb), dim3(kBlock), 0, s, sslot, n, head);
     if ((rc = scan_u32(h, head, cid, n, true))) return rc;
     uint32_t* cube_start = h->cube_start.as<uint32_t>();
     hipLaunchKernelGGL(k_delta_cubes, dim3(nb), dim3(kBlock), 0, s, head, cid, n, cube_start, sum);
     hipLaunchKernelGGL(k_delta_plan_light, dim3(nb), dim3(kBlock), 0, s, t.recs.as<Record>(), cube_start, sslot,
-                       d.skd.as<uint8_t>(), sum, n, d.plan.as<uint4>(), d.reloc.as<uint32_t>(), d.part.as<uint64_t>());
+                       d.svs.as<uint64_t>(), sum, n, d.plan.as<uint4>(), d.reloc.as<uint32_t>(), d.part.as<uint64_t>());
     hipLaunchKernelGGL(k_delta_reduce, dim3(1), dim3(kBlock), 0, s, d.part.as<uint64_t>(), nb, sum);
     return scan_u32(h, d.reloc.as<uint32_t>(), d.reloc_off.as<uint32_t>(), n, false);
 }
@@ -762,6 +777,8 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     WQ_ALLOC(h, d.peer, (uint64_t)n * 4);
     WQ_ALLOC(h, d.kind, n);
     WQ_ALLOC(h, d.sp, (uint64_t)n * 4);
+    WQ_ALLOC(h, d.sv, (uint64_t)n * 8);
+    WQ_ALLOC(h, d.svs, (uint64_t)n * 8);
     WQ_ALLOC(h, d.skd, n);
     WQ_ALLOC(h, d.plan, (uint64_t)n * 16);
     WQ_ALLOC(h, d.reloc, (uint64_t)n * 4);
@@ -784,7 +801,8 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     WQ_HIP(h, hipMemsetAsync(sum, 0, sizeof(DeltaSummary), s));
     hipLaunchKernelGGL(k_delta_events, dim3(nb), dim3(kBlock), 0, s, h->cur_ops, n, (double)h->cube_size,
                        (int64_t)h->cube_size, t.recs.as<Record>(), t.rec_cap - 1, t.rec_shift, h->hash_mask,
-                       d.pk.as<uint64_t>(), d.slot.as<uint32_t>(), d.peer.as<uint32_t>(), d.kind.as<uint8_t>(), sum);
+                       d.pk.as<uint64_t>(), d.slot.as<uint32_t>(), d.peer.as<uint32_t>(), d.kind.as<uint8_t>(),
+                       d.sv.as<uint64_t>(), sum);
     DeltaTable tb{t.recs.as<Record>(), t.rclaim.as<uint32_t>(), t.rec_cap - 1, t.rec_shift, h->hash_mask,
                   t.list.as<uint32_t>()};
     int rc = delta_plan_groups(h, n, sum);
@@ -808,7 +826,7 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     if (groups) {
         const uint32_t ng = std::min<uint32_t>((n + kGroups - 1) / kGroups, kGroupGrid);
         hipLaunchKernelGGL(k_delta_apply_group, dim3(ng), dim3(kBlock), 0, s, tb, d.plan.as<uint4>(),
-                           d.sp.as<uint32_t>(), d.skd.as<uint8_t>(), sum, d.reloc.as<uint32_t>(),
+                           d.svs.as<uint64_t>(), sum, d.reloc.as<uint32_t>(),
                            d.reloc_off.as<uint32_t>(), t.list_used, d.part.as<uint64_t>());
         // entry / live-cube deltas stay on the device until the next read-back (table_sync_delta_stats)
         hipLaunchKernelGGL(k_delta_stats, dim3(1), dim3(kBlock), 0, s, d.part.as<uint64_t>(), ng,

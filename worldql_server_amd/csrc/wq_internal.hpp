@@ -66,7 +66,8 @@ struct Table {
 // Scratch of the incremental update (wq_delta.hip).
 struct DeltaWs {
     DevBuf pk, slot, peer, kind;  // per op (u64, u32, u32, u8)
-    DevBuf sp, skd;         // per op in (pk, peer, op) order: peer, kind
+    DevBuf sp, skd;         // per op in (pk, peer, op) order: peer, kind (per-lane path)
+    DevBuf sv, svs;         // per op: kind << 32 | peer, and the same sorted by record slot (group path)
     DevBuf plan;            // uint4 per delta cube {record slot, new count, changed, -}
     DevBuf reloc, reloc_off;  // u32 per delta cube: words of a relocated list, their exclusive scan
     DevBuf part, summ;      // per-block partial sums, the summary read back

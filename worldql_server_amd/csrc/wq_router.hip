@@ -142,7 +142,7 @@ int wq_router_destroy(wq_router* h) {
                       &h->rec_keys, &h->rec_w, &h->rec_s, &h->rec_r, &h->ppos, &h->rws.agg,
                       &h->dws.pk, &h->dws.slot, &h->dws.peer, &h->dws.kind, &h->dws.sp, &h->dws.skd, &h->dws.plan,
                       &h->dws.reloc, &h->dws.reloc_off, &h->dws.part, &h->dws.summ, &h->dws.dstat,
-                      &h->dws.rm_bits};
+                      &h->dws.rm_bits, &h->dws.sv, &h->dws.svs};
     for (DevBuf* b : bufs) b->release();
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
