@@ -90,6 +90,105 @@ struct TickSmem {
 typedef uint32_t u32x4_lds __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32_a1 __attribute__((aligned(1)));
 
+// Stage the block's outputs in the LDS image in output order (caller: T <= STAGE, every thread
+// of the block, sm.q.n_gq zeroed and a barrier passed since). Inline records: the lane holds its
+// cube's peers in registers (pc) and writes each quad of them with one 16-byte and one 4-byte LDS
+// store; the sender's skipped entry, long lists (copied from `list` by the whole block) and
+// OnlySelf take slower paths. Ends with the image complete up to the caller's next barrier.
+template <int STAGE>
+__device__ __forceinline__ void stage_image(EmitRowSmem<STAGE>& es, const TableView& tv, const EmitOut& out,
+                                            uint32_t m, uint32_t e, uint2 inf, uint32_t st, const uint4 (&pc)[6]) {
+    const int tid = threadIdx.x;
+    const bool self = e && (inf.x & kLocSelf);
+    uint32_t slot = kNone, meta = 0;
+    if (e && !self) {
+        if (inf.x & kLocGlobal) {
+            const uint32_t q = atomicAdd(&es.q.n_gq, 1u);
+            es.q.gq_j[q] = tid;
+            es.q.gq_off[q] = (inf.x & ~kLocGlobal) + 1;
+            es.q.gq_skip[q] = inf.y;
+            es.q.gq_e[q] = e;
+            es.q.gq_st[q] = st;
+        } else {
+            const uint32_t s24 = inf.y & kSkipNone24;
+            slot = inf.x;
+            meta = (inf.y >> 24) | ((s24 == kSkipNone24 ? 0xFFu : s24) << 8);
+        }
+    }
+    if (self) {
+        es.op[st] = out.sender[m];
+        es.om[st] = (uint8_t)tid;
+    }
+    if (slot != kNone) {  // inline record: the peers are in this lane's registers
+        const uint32_t cnt = meta & 0xFF, skip = meta >> 8;
+        const uint8_t j = (uint8_t)tid;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t i0 = 4u * k;  // first peer index of chunk 2 + k
+            if (i0 >= cnt) continue;
+            const uint4 c = pc[k];
+            if (i0 + 4 <= cnt && (skip == 0xFFu || skip < i0)) {
+                // four peers, none of them the sender: one quad
+                const uint32_t pos = st + i0 - (skip != 0xFFu ? 1u : 0u);
+                *reinterpret_cast<u32x4_lds*>(&es.op[pos]) = u32x4_lds{c.x, c.y, c.z, c.w};
+                *reinterpret_cast<u32_a1*>(&es.om[pos]) = 0x01010101u * j;
+            } else {
+                const uint32_t vv[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t idx = i0 + i;
+                    if (idx >= cnt || idx == skip) continue;
+                    const uint32_t pos = st + idx - (skip != 0xFFu && idx > skip ? 1u : 0u);
+                    es.op[pos] = vv[i];
+                    es.om[pos] = j;
+                }
+            }
+        }
+    }
+    lds_barrier();  // the long-list queue is complete
+    const uint32_t n_gq = es.q.n_gq;
+    for (uint32_t q = 0; q < n_gq; ++q) {
+        const uint32_t j = es.q.gq_j[q], s0 = es.q.gq_st[q], ej = es.q.gq_e[q];
+        const uint32_t off = es.q.gq_off[q], sk = es.q.gq_skip[q];
+        for (uint32_t k = tid; k < ej; k += kBlock) {
+            es.op[s0 + k] = tv.list[off + k + (k >= sk ? 1u : 0u)];
+            es.om[s0 + k] = (uint8_t)j;
+        }
+    }
+}
+
+// Copy a complete image of T outputs to the global output at g0 (every thread of the block; the
+// image is complete and a barrier passed): 16-byte quads aligned to the global output, the
+// block's first and last quads (shared with its neighbours) word by word.
+template <int STAGE>
+__device__ __forceinline__ void copy_image_out(const EmitRowSmem<STAGE>& es, const EmitOut& out, uint32_t m0,
+                                               uint64_t g0, uint32_t T) {
+    const int tid = threadIdx.x;
+    const uint64_t gA = g0 & ~3ull;
+    const uint32_t lead = (uint32_t)(g0 - gA);
+    const uint32_t span = lead + T;
+    for (uint32_t qd = 4u * tid; qd < span; qd += 4u * kBlock) {
+        // image index of global output gA + qd + i is qd + i - lead
+        const uint64_t out0 = gA + qd;
+        if (qd >= lead && qd + 4 <= span && out0 + 4 <= out.capacity) {
+            const u32x4_lds pv = *reinterpret_cast<const u32x4_lds*>(&es.op[qd - lead]);
+            const uint32_t mv = *reinterpret_cast<const u32_a1*>(&es.om[qd - lead]);
+            *reinterpret_cast<uint4*>(out.peers + out0) = make_uint4(pv.x, pv.y, pv.z, pv.w);
+            if (out.msgs)
+                *reinterpret_cast<uint4*>(out.msgs + out0) = make_uint4(
+                    m0 + (mv & 0xFF), m0 + ((mv >> 8) & 0xFF), m0 + ((mv >> 16) & 0xFF), m0 + (mv >> 24));
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i) {
+                if (qd + i >= lead && qd + i < span && out0 + i < out.capacity) {
+                    out.peers[out0 + i] = es.op[qd + i - lead];
+                    if (out.msgs) out.msgs[out0 + i] = m0 + es.om[qd + i - lead];
+                }
+            }
+        }
+    }
+}
+
 template <bool RAW_KEYS, int STAGE, int U>
 __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
     // U: record lines in flight per lane in the fallback emit_row
@@ -137,64 +236,7 @@ __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
 
     // ---- 3. stage the block's outputs in LDS (if they fit) ----
     const bool fits = T <= (uint32_t)STAGE && p.out.peers;  // block-uniform
-    const bool self = e && (inf.x & kLocSelf);
-    if (fits) {
-        uint32_t slot = kNone, meta = 0;
-        if (e && !self) {
-            if (inf.x & kLocGlobal) {
-                const uint32_t q = atomicAdd(&sm.es.q.n_gq, 1u);
-                sm.es.q.gq_j[q] = tid;
-                sm.es.q.gq_off[q] = (inf.x & ~kLocGlobal) + 1;
-                sm.es.q.gq_skip[q] = inf.y;
-                sm.es.q.gq_e[q] = e;
-                sm.es.q.gq_st[q] = st;
-            } else {
-                const uint32_t s24 = inf.y & kSkipNone24;
-                slot = inf.x;
-                meta = (inf.y >> 24) | ((s24 == kSkipNone24 ? 0xFFu : s24) << 8);
-            }
-        }
-        if (self) {
-            sm.es.op[st] = p.out.sender[m];
-            sm.es.om[st] = (uint8_t)tid;
-        }
-        if (slot != kNone) {  // inline record: the peers are in this lane's registers
-            const uint32_t cnt = meta & 0xFF, skip = meta >> 8;
-            const uint8_t j = (uint8_t)tid;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                const uint32_t i0 = 4u * k;  // first peer index of chunk 2 + k
-                if (i0 >= cnt) continue;
-                const uint4 c = pc[0][k];
-                if (i0 + 4 <= cnt && (skip == 0xFFu || skip < i0)) {
-                    // four peers, none of them the sender: one quad
-                    const uint32_t pos = st + i0 - (skip != 0xFFu ? 1u : 0u);
-                    *reinterpret_cast<u32x4_lds*>(&sm.es.op[pos]) = u32x4_lds{c.x, c.y, c.z, c.w};
-                    *reinterpret_cast<u32_a1*>(&sm.es.om[pos]) = 0x01010101u * j;
-                } else {
-                    const uint32_t vv[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const uint32_t idx = i0 + i;
-                        if (idx >= cnt || idx == skip) continue;
-                        const uint32_t pos = st + idx - (skip != 0xFFu && idx > skip ? 1u : 0u);
-                        sm.es.op[pos] = vv[i];
-                        sm.es.om[pos] = j;
-                    }
-                }
-            }
-        }
-        lds_barrier();  // the long-list queue is complete
-        const uint32_t n_gq = sm.es.q.n_gq;
-        for (uint32_t q = 0; q < n_gq; ++q) {
-            const uint32_t j = sm.es.q.gq_j[q], s0 = sm.es.q.gq_st[q], ej = sm.es.q.gq_e[q];
-            const uint32_t off = sm.es.q.gq_off[q], sk = sm.es.q.gq_skip[q];
-            for (uint32_t k = tid; k < ej; k += kBlock) {
-                sm.es.op[s0 + k] = tv.list[off + k + (k >= sk ? 1u : 0u)];
-                sm.es.om[s0 + k] = (uint8_t)j;
-            }
-        }
-    }
+    if (fits) stage_image<STAGE>(sm.es, tv, p.out, m, e, inf, st, pc[0]);
 
     // ---- 4. look-back (wave 0), publish the inclusive prefix ----
     if (wave == 0) {
@@ -234,33 +276,8 @@ __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
     // ---- 5. offsets, copy-out ----
     if (m < p.in.M) p.offsets[m] = (uint32_t)(g0 + st);
     if (p.out.peers) {
-        if (fits) {
-            const uint64_t gA = g0 & ~3ull;
-            const uint32_t lead = (uint32_t)(g0 - gA);
-            const uint32_t span = lead + T;
-            for (uint32_t qd = 4u * tid; qd < span; qd += 4u * kBlock) {
-                // image index of global output gA + qd + i is qd + i - lead
-                const uint64_t out0 = gA + qd;
-                if (qd >= lead && qd + 4 <= span && out0 + 4 <= p.out.capacity) {
-                    const u32x4_lds pv = *reinterpret_cast<const u32x4_lds*>(&sm.es.op[qd - lead]);
-                    const uint32_t mv = *reinterpret_cast<const u32_a1*>(&sm.es.om[qd - lead]);
-                    *reinterpret_cast<uint4*>(p.out.peers + out0) = make_uint4(pv.x, pv.y, pv.z, pv.w);
-                    if (p.out.msgs)
-                        *reinterpret_cast<uint4*>(p.out.msgs + out0) = make_uint4(
-                            m0 + (mv & 0xFF), m0 + ((mv >> 8) & 0xFF), m0 + ((mv >> 16) & 0xFF), m0 + (mv >> 24));
-                } else {
-#pragma unroll
-                    for (uint32_t i = 0; i < 4; ++i) {
-                        if (qd + i >= lead && qd + i < span && out0 + i < p.out.capacity) {
-                            p.out.peers[out0 + i] = sm.es.op[qd + i - lead];
-                            if (p.out.msgs) p.out.msgs[out0 + i] = m0 + sm.es.om[qd + i - lead];
-                        }
-                    }
-                }
-            }
-        } else {
-            emit_row<STAGE, U>(sm.es, tv, p.out, m0, e, inf, st, g0, T);
-        }
+        if (fits) copy_image_out<STAGE>(sm.es, p.out, m0, g0, T);
+        else emit_row<STAGE, U>(sm.es, tv, p.out, m0, e, inf, st, g0, T);
     }
     if (stamp) p.stamps[4 * b + 3] = __builtin_amdgcn_s_memrealtime();
 }

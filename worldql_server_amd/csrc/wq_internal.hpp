@@ -83,6 +83,7 @@ struct RouteWs {
     DevBuf info;   // uint2[M]: locators, count pass -> emit pass
     DevBuf e;      // u32[M]: filtered counts
     DevBuf tiles;  // u32[2 * n_count_blocks]: block totals, then their exclusive prefix
+    DevBuf spill;  // per-block output images of the count+spill tick (route config 7)
     DevBuf agg;    // u64[2 * blocks]: look-back and candidate granules of the single-launch tick
     uint64_t agg_zeroed = 0;
     uint64_t* stamps = nullptr;  // wq_debug_set_timeline

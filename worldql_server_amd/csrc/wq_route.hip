@@ -19,6 +19,7 @@
 #include "route_scan.hpp"
 #include "route_tick.hpp"
 #include "route_radius.hpp"
+#include "route_spill.hpp"
 
 namespace wq {
 
@@ -26,6 +27,8 @@ namespace wq {
 // host side
 // ------------------------------------------------------------------------------------------
 namespace {
+constexpr int kSpillStage = 2816;
+
 struct Cfg {
     int count_tile;  // messages per tile_total entry
     void (*count)(const CountParams&, hipStream_t, unsigned);
@@ -33,7 +36,8 @@ struct Cfg {
     // single-launch tick (route_tick.hpp): its LDS image positions, or 0 for three launches
     int tick_stage;
     void (*tick)(const TickParams&, hipStream_t, unsigned);
-    const void* unused;
+    // count+spill / tile_scan / copy (route_spill.hpp): image positions per block, or 0
+    int spill_stage;
 };
 
 template <int IPT, int MINW, bool FULL = false>
@@ -52,8 +56,9 @@ void launch_tick(const TickParams& p, hipStream_t s, unsigned grid) {
         hipLaunchKernelGGL((tick_kernel<false, STAGE, U>), dim3(grid), dim3(kBlock), 0, s, p);
 }
 
-#define WQ_CFG3(cipt, minw, stage) {kBlock * cipt, &launch_count<cipt, minw>, stage, 0, nullptr, nullptr}
-#define WQ_CFG1(stage, u) {kBlock, &launch_count<1, 8>, 4096, stage, &launch_tick<stage, u>, nullptr}
+#define WQ_CFG3(cipt, minw, stage) {kBlock * cipt, &launch_count<cipt, minw>, stage, 0, nullptr, 0}
+#define WQ_CFG1(stage, u) {kBlock, &launch_count<1, 8>, 4096, stage, &launch_tick<stage, u>, 0}
+#define WQ_CFGS(stage) {kBlock, &launch_count<1, 8>, 4096, 0, nullptr, stage}
 // Three launches: count (messages per lane, min waves per SIMD) / tile_scan / emit. One launch:
 // messages per block; its three-launch fallback (too many blocks to be resident) is count 4/2.
 const Cfg kCfgs[] = {
@@ -64,8 +69,10 @@ const Cfg kCfgs[] = {
     WQ_CFG3(4, 2, 4096 + 2),  // 4
     WQ_CFG1(3072, 2),         // 5: 21.6 KB LDS -> 7 blocks per CU (65.6 us)
     WQ_CFG1(2560, 2),         // 6: C2 blocks overflow the image (78 us)
+    WQ_CFGS(kSpillStage),     // 7: count+spill / tile_scan / copy, no block waits on another
 };
 #undef WQ_CFG1
+#undef WQ_CFGS
 #undef WQ_CFG3
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -145,6 +152,51 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         tp.stamps = rw.stamps;
         tp.n_tiles = (uint32_t)nb;
         cfg.tick(tp, s, (unsigned)nb);
+        WQ_HIP(h, hipGetLastError());
+        if (pr.enabled) {
+            WQ_HIP(h, hipEventRecord(pr.stop[pr.used], s));
+            pr.used++;
+        }
+        rw.calls++;
+        return WQ_OK;
+    }
+
+    if (cfg.spill_stage && !radius) {  // count+spill / tile_scan / copy
+        const uint64_t nb = (M + kBlock - 1) / kBlock;
+        WQ_ALLOC(h, rw.info, M * sizeof(uint2));
+        WQ_ALLOC(h, rw.e, M * 4);
+        WQ_ALLOC(h, rw.tiles, nb * 12);
+        if (capacity) WQ_ALLOC(h, rw.spill, nb * (uint64_t)kSpillStage * 5);
+        SpillParams sp;
+        sp.in = in;
+        sp.t = tv;
+        sp.out = EmitOut{d_sender, capacity ? d_peers : nullptr, d_msgs, capacity, d_pos, d_repl};
+        sp.offsets = d_offsets;
+        sp.e = rw.e.as<uint32_t>();
+        sp.info = rw.info.as<uint2>();
+        sp.tile_total = rw.tiles.as<uint32_t>();
+        sp.tile_F = sp.tile_total + 2 * nb;
+        sp.tile_prefix = sp.tile_total + nb;
+        sp.spill_p = capacity ? rw.spill.as<uint32_t>() : nullptr;
+        sp.spill_m = capacity ? reinterpret_cast<uint8_t*>(sp.spill_p + nb * kSpillStage) : nullptr;
+        sp.cnt_next = nxt;
+        if (in.keys)
+            hipLaunchKernelGGL((spill_count_kernel<true, kSpillStage>), dim3(nb), dim3(kBlock), 0, s, sp);
+        else
+            hipLaunchKernelGGL((spill_count_kernel<false, kSpillStage>), dim3(nb), dim3(kBlock), 0, s, sp);
+        WQ_HIP(h, hipGetLastError());
+        TileScanParams tsp;
+        tsp.tile_total = sp.tile_total;
+        tsp.tile_F = sp.tile_F;
+        tsp.tile_prefix = rw.tiles.as<uint32_t>() + nb;
+        tsp.n_tiles = (uint32_t)nb;
+        tsp.offsets = d_offsets;
+        tsp.M = (uint32_t)M;
+        tsp.capacity = capacity;
+        tsp.cnt = cur;
+        hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, tsp);
+        WQ_HIP(h, hipGetLastError());
+        hipLaunchKernelGGL((spill_copy_kernel<kSpillStage, 2>), dim3(nb), dim3(kBlock), 0, s, sp);
         WQ_HIP(h, hipGetLastError());
         if (pr.enabled) {
             WQ_HIP(h, hipEventRecord(pr.stop[pr.used], s));
