@@ -1,6 +1,7 @@
 """CPU: host-side logic — world names, synthetic generator, the C ABI's exported symbols and
 record layouts, the host instance of the quantiser, and tick batching (flush-on-reorder)."""
 import ctypes
+import glob
 import os
 import re
 import subprocess
@@ -48,10 +49,12 @@ def test_config_shapes():
 
 
 def _header_functions():
-    with open(os.path.join(ROOT, "include", "wq_router.h")) as f:
-        txt = f.read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(wq_[a-z0-9_]+)\s*\(", txt)))
+    names = set()
+    for h in sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))):  # wq_router.h, wq_codec.h
+        with open(h) as f:
+            txt = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+        names |= set(re.findall(r"\b(wq_[a-z0-9_]+)\s*\(", txt))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():
@@ -61,7 +64,7 @@ def test_library_exports_every_declared_symbol():
         build()
     lib = ctypes.CDLL(LIB)  # loading needs no GPU; nothing below computes
     names = _header_functions()
-    assert "wq_route_tick_device" in names and len(names) >= 17
+    assert "wq_route_tick_device" in names and "wq_decode_messages" in names and len(names) >= 19
     for n in names:
         assert hasattr(lib, n), n
 

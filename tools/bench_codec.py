@@ -1,0 +1,56 @@
+"""Throughput of the host wire codec (wq_decode_messages) on a tick of C2-sized
+LocalMessage frames (1M frames, one world, random sender uuids and positions), 1 and N threads,
+next to the Python restatement (oracle/fbs_oracle.py) on a bounded sample.
+Usage: python tools/bench_codec.py [--frames N] [--threads T]"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+import uuid
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=1_000_000)
+    ap.add_argument("--threads", type=int, default=16)
+    a = ap.parse_args()
+    from fbs_builder import message
+    from worldql_server_amd import codec
+    from oracle import fbs_oracle
+    r = random.Random(0x5EED0002)
+    senders = [str(uuid.UUID(int=r.getrandbits(128))) for _ in range(1000)]
+    proto = [message(instruction=7, sender_uuid=s, world_name="world", replication=0,
+                     position=(r.uniform(-512, 512), r.uniform(-512, 512), r.uniform(-512, 512)))
+             for s in senders]
+    frames = [proto[i % len(proto)] for i in range(a.frames)]
+    data, offsets = codec.pack_frames(frames)
+    res = {"frames": a.frames, "bytes": int(len(data)), "frame_bytes": len(proto[0]), "host_cpus": os.cpu_count()}
+    out = np.zeros(a.frames, dtype=codec.DECODED_DTYPE)  # reused, pages resident (as a server's)
+    out[:] = 0
+    for t in (1, a.threads):
+        best = 1e9
+        for _ in range(3):
+            t0 = time.perf_counter()
+            codec.decode_packed(data, offsets, t, out=out)
+            best = min(best, time.perf_counter() - t0)
+        assert (out["status"] == 0).all()
+        res[f"threads_{t}"] = {"s": best, "frames_per_s": a.frames / best, "GB_per_s": len(data) / best / 1e9}
+    n_py = 20000
+    t0 = time.perf_counter()
+    for f in frames[:n_py]:
+        fbs_oracle.decode(f)
+    dt = time.perf_counter() - t0
+    res["python_restatement"] = {"frames": n_py, "frames_per_s": n_py / dt}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -18,6 +18,9 @@ LIB = os.path.join(PKG, "libwq_router.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["wq_route.hip", "wq_global.hip", "wq_query.hip", "wq_table.hip", "wq_delta.hip", "wq_shard.hip", "wq_peers.hip", "wq_router.hip"]
+HOST_SOURCES = ["wq_codec.cpp"]
+CXX = os.environ.get("CXX", "g++")
+HOST_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-pthread", "-Wall"]
 HEADERS = ["wq_device.hpp", "wq_internal.hpp", "route_common.hpp", "route_count.hpp", "route_scan.hpp", "route_emit.hpp", "route_tick.hpp", "route_radius.hpp", "route_spill.hpp", "table_prims.hpp"]
 # No fast-math and no FMA contraction: coord_clamp must reproduce Rust's f64 op sequence.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
@@ -44,8 +47,20 @@ def build(force: bool = False, verbose: bool = False) -> str:
                 print(" ".join(cmd), flush=True)
             subprocess.check_call(cmd)
             relink = True
+    # host-only C++ (the wire codec): g++, no device code
+    codec_h = _mtime(os.path.join(ROOT, "include", "wq_codec.h"))
+    for src in HOST_SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILD, src.replace(".cpp", ".o"))
+        objs.append(o)
+        if force or _mtime(o) < max(_mtime(s), codec_h):
+            cmd = [CXX, *HOST_FLAGS, "-I", os.path.join(ROOT, "include"), "-c", s, "-o", o]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.check_call(cmd)
+            relink = True
     if relink or any(_mtime(o) > _mtime(LIB) for o in objs):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB, *objs]
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-pthread", "-o", LIB, *objs]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)

@@ -1,0 +1,120 @@
+"""Python binding of the host wire codec (include/wq_codec.h).
+
+`decode_batch` runs the C++ batch decoder of libwq_router.so (wq_codec.cpp) over a list of
+received frames: FlatBuffers verification and Message decode as in
+worldql_server/src/structures/message.rs:136-142 / :60-114, one structured record per frame.
+`decode_messages` turns those records into the `processing.Message` events the tick loop takes,
+dropping frames that fail to decode exactly as the ZeroMQ ingress does
+(transport/zeromq/incoming.rs:39-45). `sanitize_world_name` is the C restatement of
+utils/world_names.rs:54-87. Host code only: no GPU is needed.
+"""
+from __future__ import annotations
+
+import ctypes
+import uuid as _uuid
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from .router import load_library
+from .subscriptions import Vector3
+
+DEC_OK, DEC_INVALID_FLATBUFFER, DEC_MISSING_FIELD, DEC_BAD_UUID = 0, 1, 2, 3
+INSTRUCTION_NAMES = ["Heartbeat", "Handshake", "PeerConnect", "PeerDisconnect", "AreaSubscribe",
+                     "AreaUnsubscribe", "GlobalMessage", "LocalMessage", "RecordCreate", "RecordRead",
+                     "RecordUpdate", "RecordDelete", "RecordReply"]  # WorldQLFB_generated.rs:56-68
+SANITIZE_ERRORS = {1: "IsGlobalWorld", 2: "ZeroLength", 3: "InvalidStart", 4: "InvalidChars", 5: "TooLong"}
+
+# struct wq_decoded_msg (include/wq_codec.h), 72 bytes
+DECODED_DTYPE = np.dtype([
+    ("status", np.int32), ("instruction", np.uint8), ("replication", np.uint8),
+    ("has_position", np.uint8), ("has_parameter", np.uint8), ("sender_uuid", np.uint8, (16,)),
+    ("position", np.float64, (3,)), ("world_off", np.uint32), ("world_len", np.uint32),
+    ("param_off", np.uint32), ("param_len", np.uint32), ("n_records", np.uint32), ("n_entities", np.uint32),
+])
+assert DECODED_DTYPE.itemsize == 72
+
+_sig_done = False
+
+
+def _lib():
+    global _sig_done
+    lib = load_library()
+    if not _sig_done:
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        lib.wq_decode_messages.argtypes = [vp, vp, sz, vp, ctypes.c_int]
+        lib.wq_decode_messages.restype = ctypes.c_int
+        lib.wq_sanitize_world_name.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+        lib.wq_sanitize_world_name.restype = ctypes.c_int
+        _sig_done = True
+    return lib
+
+
+def pack_frames(frames: Sequence[bytes]):
+    """Concatenate frames into one byte array + n+1 offsets (the decoder's input layout)."""
+    lens = np.fromiter((len(f) for f in frames), dtype=np.uint64, count=len(frames))
+    offsets = np.zeros(len(frames) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offsets[1:])
+    data = np.frombuffer(b"".join(frames), dtype=np.uint8) if frames else np.zeros(0, np.uint8)
+    return data, offsets
+
+
+def decode_packed(data: np.ndarray, offsets: np.ndarray, n_threads: int = 0, out=None) -> np.ndarray:
+    """`out`: a reusable DECODED_DTYPE array of at least n records (a server keeps one per tick)."""
+    n = len(offsets) - 1
+    if out is None:
+        out = np.zeros(max(n, 0), dtype=DECODED_DTYPE)
+    elif out.dtype != DECODED_DTYPE or len(out) < n or not out.flags.c_contiguous:
+        raise ValueError("out: a contiguous DECODED_DTYPE array of >= n records")
+    if n <= 0:
+        return out
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    buf = data if len(data) else np.zeros(1, np.uint8)
+    rc = _lib().wq_decode_messages(buf.ctypes.data, offsets.ctypes.data, n, out.ctypes.data, int(n_threads))
+    if rc != 0:
+        raise ValueError(f"wq_decode_messages: invalid arguments ({rc})")
+    return out[:n]
+
+
+def decode_batch(frames: Sequence[bytes], n_threads: int = 0) -> np.ndarray:
+    """One DECODED_DTYPE record per frame (byte ranges are relative to each frame)."""
+    data, offsets = pack_frames(frames)
+    return decode_packed(data, offsets, n_threads)
+
+
+def decode_messages(frames: Sequence[bytes], n_threads: int = 0):
+    """`processing.Message` per frame, or None where Message::deserialize fails (the frame the
+    ingress drops). Instruction codes outside 0..12 become "Unknown"."""
+    from .processing import Message
+    recs = decode_batch(frames, n_threads)
+    out: List[Optional[Message]] = []
+    for f, r in zip(frames, recs):
+        if r["status"] != DEC_OK:
+            out.append(None)
+            continue
+        ins = int(r["instruction"])
+        w0, wl = int(r["world_off"]), int(r["world_len"])
+        pos = Vector3(*map(float, r["position"])) if r["has_position"] else None
+        out.append(Message(instruction=INSTRUCTION_NAMES[ins] if ins < len(INSTRUCTION_NAMES) else "Unknown",
+                           sender_uuid=_uuid.UUID(bytes=bytes(r["sender_uuid"])),
+                           world_name=f[w0:w0 + wl].decode("utf-8"), position=pos,
+                           replication=int(r["replication"])))
+    return out
+
+
+class SanitizeCError(ValueError):
+    def __init__(self, kind: str):
+        super().__init__(kind)
+        self.kind = kind
+
+
+def sanitize_world_name(name: str) -> str:
+    """C restatement of world_names.rs:54-87 (raises SanitizeCError with the variant name)."""
+    raw = name.encode("utf-8")
+    out = ctypes.create_string_buffer(64)
+    n = ctypes.c_size_t(0)
+    rc = _lib().wq_sanitize_world_name(raw, len(raw), out, 64, ctypes.byref(n))
+    if rc != 0:
+        raise SanitizeCError(SANITIZE_ERRORS.get(rc, f"error {rc}"))
+    return out.raw[:n.value].decode("ascii")
