@@ -1,6 +1,5 @@
 """Throughput of the host wire codec (wq_decode_messages) on a tick of C2-sized
-LocalMessage frames (1M frames, one world, random sender uuids and positions), 1 and N threads,
-next to the Python restatement (oracle/fbs_oracle.py) on a bounded sample.
+LocalMessage frames (1M frames, one world, random sender uuids and positions), 1 and N threads.
 Usage: python tools/bench_codec.py [--frames N] [--threads T]"""
 import argparse
 import json
@@ -24,7 +23,6 @@ def main():
     a = ap.parse_args()
     from fbs_builder import message
     from worldql_server_amd import codec
-    from oracle import fbs_oracle
     r = random.Random(0x5EED0002)
     senders = [str(uuid.UUID(int=r.getrandbits(128))) for _ in range(1000)]
     proto = [message(instruction=7, sender_uuid=s, world_name="world", replication=0,
@@ -43,12 +41,6 @@ def main():
             best = min(best, time.perf_counter() - t0)
         assert (out["status"] == 0).all()
         res[f"threads_{t}"] = {"s": best, "frames_per_s": a.frames / best, "GB_per_s": len(data) / best / 1e9}
-    n_py = 20000
-    t0 = time.perf_counter()
-    for f in frames[:n_py]:
-        fbs_oracle.decode(f)
-    dt = time.perf_counter() - t0
-    res["python_restatement"] = {"frames": n_py, "frames_per_s": n_py / dt}
     print(json.dumps(res))
 
 
