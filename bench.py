@@ -40,8 +40,8 @@ METRIC = "routed msg→peer pairs/sec per tick at 1/2/4/8 GPUs; % HBM roofline"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
-                    help="c2 = the headline (BASELINE.json configs[1]); c3/c4/c5 = SURVEY.md §8(d)")
+    ap.add_argument("--config", choices=["c1", "c2", "c3", "c4", "c5"], default="c2",
+                    help="c2 = the headline (BASELINE.json configs[1]); c1/c3/c4/c5 = SURVEY.md §8(d)")
     ap.add_argument("--steps", type=int, default=None, help="timed ticks (default 50; c4 20, c3/c5 10)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed ticks (default 10; c3/c4/c5 2)")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink C2 (tests only; 1.0 = the headline)")
@@ -52,9 +52,9 @@ def parse():
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "r01_pmc_route.json"))
     a = ap.parse_args()
     if a.steps is None:
-        a.steps = {"c2": 50, "c3": 10, "c4": 20, "c5": 10}[a.config]
+        a.steps = {"c1": 50, "c2": 50, "c3": 10, "c4": 20, "c5": 10}[a.config]
     if a.warmup is None:
-        a.warmup = 10 if a.config == "c2" else 2
+        a.warmup = 10 if a.config in ("c1", "c2") else 2
     return a
 
 

@@ -1,9 +1,11 @@
-"""bench.py --config c3 | c4 | c5: the SURVEY.md §8(d) configurations past the headline.
+"""bench.py --config c1 | c3 | c4 | c5: the SURVEY.md §8(d) configurations beside the headline.
 
 Every mode prints one JSON line in bench.py's format (metric = routed pairs/s; value = all ranks'
 pairs over the max-over-ranks time of the timed ticks). Inputs are generated and uploaded before
 the timed region; a tick's timed work is everything the tick does on the GPU.
 
+  c1  the reference's CPU-sized case (1k peers, 10k messages): GPU tick beside cpu_ref_1t and
+      cpu_server_faithful_1t (the broadcast_to scan).
   c3  1M peers x 3x3x3 (S = 27M), 10M messages/tick, 90% from 256 Zipf-weighted Gaussian hotspots.
       N = 1: the whole configuration on one GPU. N > 1: strong scaling through the cube-hash sharded
       path (worldql_server_amd/sharded.py; every rank ingests M/N messages, RCCL all-to-all).
@@ -28,7 +30,7 @@ from bench import HBM_PEAK_GBS, METRIC, algorithmic_bytes, reduce_over_ranks
 
 
 def run(a, rank, world_size, local_rank, dev):
-    return {"c3": run_c3, "c4": run_c4, "c5": run_c5}[a.config](a, rank, world_size, local_rank, dev)
+    return {"c1": run_c1, "c3": run_c3, "c4": run_c4, "c5": run_c5}[a.config](a, rank, world_size, local_rank, dev)
 
 
 def _emit(out, rank):
@@ -46,6 +48,110 @@ def _line(a, world_size, value, ms_per_step, scaling, workload, config, roofline
 def _counters(cnt):
     from worldql_server_amd import abi
     return cnt.cpu().numpy().view(abi.COUNTERS_DTYPE)
+
+
+# ---- C1 ---------------------------------------------------------------------------------------
+
+def _cpu_c1(w, repeats: int):
+    """C1 on 1 host thread, whole tick, by the C restatement: cpu_ref_1t (wqo_route) and
+    cpu_server_faithful_1t (wqo_route_faithful: + PeerMap::broadcast_to's per-message recipient
+    set and O(|PeerMap|) scan over all 1,000 connected peers, peer_map.rs:151-163)."""
+    import ctypes
+    o, run, build_s = bench._oracle_router(w)
+    M = len(w.world)
+    vp = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+    run((0, M))
+    t0 = time.perf_counter()
+    for _ in range(repeats):
+        P = run((0, M))
+    t_ref = (time.perf_counter() - t0) / repeats
+    connected = np.arange(w.n_peers, dtype=np.uint32)  # every peer connected, map order = id order
+    offs = np.empty(M + 1, np.uint32)
+    peers = np.empty(64 * M + 64, np.uint32)
+    pos, wo, se, rp = (np.ascontiguousarray(x) for x in (w.pos, w.world, w.sender, w.repl))
+    f = o.lib.wqo_route_faithful
+    f.restype = ctypes.c_size_t
+    f.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_size_t]
+    t0 = time.perf_counter()
+    for _ in range(repeats):
+        P2 = f(o.h, vp(pos), vp(wo), vp(se), vp(rp), M, vp(connected), len(connected), vp(offs), vp(peers),
+               len(peers))
+    t_faith = (time.perf_counter() - t0) / repeats
+    o.close()
+    assert P2 == P, (P, P2)
+    samp = f"the whole C1 tick ({M} messages, {P} pairs), mean of {repeats} runs, oracle/wq_oracle.c, 1 host thread"
+    return ({"value": P / t_ref, "unit": "pairs/s", "cores": 1, "kind": "port", "sample": "cpu_ref_1t: " + samp},
+            {"value": P / t_faith, "unit": "pairs/s", "cores": 1, "kind": "port",
+             "sample": "cpu_server_faithful_1t (broadcast_to set + O(|PeerMap|) scan per message): " + samp})
+
+
+def run_c1(a, rank, world_size, local_rank, dev):
+    """BASELINE.json configs[0]: 1 world, 1k peers x 1 cube, 10k messages in U[-64,64)^3 — the
+    reference's CPU-sized case. One GPU (world_size > 1 runs a replica per rank, weak)."""
+    import torch
+    from worldql_server_amd import synth
+    from worldql_server_amd.router import Router
+    w = synth.config_c1()
+    M = len(w.world)
+    r = Router(w.cube_size, local_rank)
+    stream = torch.cuda.Stream(device=dev)
+    r.set_stream(stream.cuda_stream)
+    r.apply_ops(w.ops)
+    pos = torch.from_numpy(w.pos).to(dev)
+    world = torch.from_numpy(w.world.view(np.int32)).to(dev)
+    sender = torch.from_numpy(w.sender.view(np.int32)).to(dev)
+    repl = torch.from_numpy(w.repl).to(dev)
+    offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    r.route_device(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
+                   0, 0, 0, cnt.data_ptr())
+    torch.cuda.synchronize(dev)
+    P = int(_counters(cnt)[0]["n_pairs"])
+    cap = P + 1024
+    peers = torch.empty(cap, dtype=torch.int32, device=dev)
+    args = (pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
+            peers.data_ptr(), 0, cap)
+    for _ in range(a.warmup):
+        r.route_device(*args, 0)
+    r.route_device(*args, cnt.data_ptr())
+    torch.cuda.synchronize(dev)
+    c = _counters(cnt)[0]
+    F = int(c["n_candidates"])
+    assert c["overflow"] == 0 and c["error"] == 0, c
+    if world_size > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(a.steps):
+        r.route_device(*args, 0)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world_size > 1:
+        torch.distributed.barrier()
+    t_max_ms, pairs_all = reduce_over_ranks(ev0.elapsed_time(ev1), P, dev, world_size)
+    r.profile_enable(True)
+    for _ in range(a.steps):
+        r.route_device(*args, 0)
+    k_ms, launches = r.profile_read()
+    r.profile_enable(False)
+    k_s = k_ms / launches / 1e3
+    B = algorithmic_bytes(M, F, P)
+    out = _line(a, world_size, pairs_all * a.steps / (t_max_ms / 1e3), t_max_ms / a.steps, "weak",
+                "C1: 1 world, 1k peers x 1 cube, 10k LocalMessages/tick, U[-64,64)^3, cube_size 16, ExceptSelf "
+                "(BASELINE.json configs[0], the reference's CPU case; launch-latency bound on a GPU)",
+                {"messages_per_tick": M, "peers": w.n_peers, "pairs_per_tick": P, "candidates_per_tick": F,
+                 "parallelism": f"replicas x{world_size}"},
+                {"bound": "hbm", "achieved": B / k_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": B / k_s / 1e9 / HBM_PEAK_GBS, "traffic": None, "kernel": "route tick (single launch)",
+                 "kernel_avg_us": k_s * 1e6, "algorithmic_bytes": B},
+                "synthetic (splitmix64, SURVEY.md §8(d) C1 generator)")
+    if rank == 0 and world_size == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"], out["cpu_baseline_faithful"] = _cpu_c1(w, 20)
+    r.close()
+    _emit(out, rank)
 
 
 # ---- C3 ---------------------------------------------------------------------------------------

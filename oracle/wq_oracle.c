@@ -475,6 +475,57 @@ size_t wqo_route(const wqo_world_map* wm, const double* pos, const int64_t* keys
     return P;
 }
 
+/* cpu_server_faithful_1t: wqo_route per message, then what
+ * PeerMap::broadcast_to does with the recipients (worldql_server/src/transport/peer_map.rs:151-163):
+ * collect them into a new hash set (:156), then filter EVERY connected peer of the PeerMap against
+ * it (:157-160, O(|PeerMap|) per message). connected[0 .. n_connected) is the PeerMap's iteration
+ * order; the output per message is in that order. Returns P (pairs actually sent). */
+size_t wqo_route_faithful(const wqo_world_map* wm, const double* pos, const uint32_t* world,
+                          const uint32_t* sender, const uint8_t* repl, size_t M, const uint32_t* connected,
+                          size_t n_connected, uint32_t* offsets, uint32_t* peers, size_t cap) {
+    size_t P = 0;
+    uint32_t* tmp = NULL;
+    size_t tcap = 0;
+    uint32_t* set = NULL; /* open addressing, 0xFFFFFFFF = empty; rebuilt per message like AHashSet::collect */
+    size_t scap = 0;
+    for (size_t m = 0; m < M; ++m) {
+        if (offsets) offsets[m] = (uint32_t)P;
+        const size_t n = wqo_route(wm, pos + 3 * m, NULL, world + m, sender + m, repl + m, 1, NULL, NULL, 0, NULL);
+        if (!wm_get(wm, world[m])) continue; /* local_message.rs:52-56: no broadcast at all */
+        /* otherwise broadcast_to runs even for an empty recipient set (:60-86), scanning the map */
+        if (n > tcap) {
+            tcap = 2 * n;
+            tmp = (uint32_t*)realloc(tmp, tcap * sizeof(uint32_t));
+        }
+        if (n) wqo_route(wm, pos + 3 * m, NULL, world + m, sender + m, repl + m, 1, NULL, tmp, n, NULL);
+        size_t need = 16;
+        while (need < 2 * n) need <<= 1;
+        if (need > scap) {
+            scap = need;
+            set = (uint32_t*)realloc(set, scap * sizeof(uint32_t));
+        }
+        memset(set, 0xFF, need * sizeof(uint32_t));
+        for (size_t i = 0; i < n; ++i) {
+            size_t h = (tmp[i] * 0x9E3779B1u) & (need - 1);
+            while (set[h] != 0xFFFFFFFFu && set[h] != tmp[i]) h = (h + 1) & (need - 1);
+            set[h] = tmp[i];
+        }
+        for (size_t j = 0; j < n_connected; ++j) {
+            const uint32_t q = connected[j];
+            size_t h = (q * 0x9E3779B1u) & (need - 1);
+            while (set[h] != 0xFFFFFFFFu && set[h] != q) h = (h + 1) & (need - 1);
+            if (set[h] == q) {
+                if (peers && P < cap) peers[P] = q;
+                P++;
+            }
+        }
+    }
+    if (offsets) offsets[M] = (uint32_t)P;
+    free(tmp);
+    free(set);
+    return P;
+}
+
 /* C5 (an extension the reference does not have): handle_local_message's
  * recipients (wqo_route) intersected with the exact Euclidean radius predicate
  *   dx = mx - px; dy = my - py; dz = mz - pz; keep iff (dx*dx + dy*dy) + dz*dz <= r*r

@@ -61,6 +61,12 @@ size_t wqo_route(const wqo_world_map* wm, const double* pos, const int64_t* keys
                  const uint32_t* world, const uint32_t* sender, const uint8_t* repl, size_t M,
                  uint32_t* offsets, uint32_t* peers, size_t cap, uint64_t* n_candidates);
 
+/* cpu_server_faithful_1t: wqo_route + PeerMap::broadcast_to's per-message recipient set and
+ * O(|PeerMap|) connected-peer scan (peer_map.rs:151-163); output per message in connected[] order. */
+size_t wqo_route_faithful(const wqo_world_map* wm, const double* pos, const uint32_t* world,
+                          const uint32_t* sender, const uint8_t* repl, size_t M, const uint32_t* connected,
+                          size_t n_connected, uint32_t* offsets, uint32_t* peers, size_t cap);
+
 /* C5 extension: wqo_route's recipients with the exact radius predicate
  * (dx*dx + dy*dy) + dz*dz <= r*r in f64, d = message position - peer position; peers >= n_pos
  * have no position and are dropped. */

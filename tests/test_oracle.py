@@ -173,3 +173,35 @@ def test_oracle_global_matches_world_peers():
         all_ = wp[int(world[i])]
         want = [q for q in all_ if q == s] if r == 2 else (all_ if r == 1 else [q for q in all_ if q != s])
         assert peers[offs[i]:offs[i + 1]].tolist() == want
+
+
+def test_server_faithful_route_is_route_intersect_connected():
+    """cpu_server_faithful_1t (wqo_route_faithful, peer_map.rs:151-163): per message, the
+    recipients of wqo_route that are connected, in PeerMap order."""
+    import ctypes
+    from oracle import oracle as orc
+    from worldql_server_amd import synth
+    w = synth.config_c1(repl_mode="mixed")
+    o = orc.COracle(w.cube_size)
+    o.apply_ops(w.ops)
+    offs, peers, _ = o.route(w.pos, w.world, w.sender, w.repl)
+    vp = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+    f = o.lib.wqo_route_faithful
+    f.restype = ctypes.c_size_t
+    f.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_size_t]
+    M = len(w.world)
+    rng = np.random.default_rng(5)
+    for connected in (np.arange(w.n_peers, dtype=np.uint32)[::-1].copy(),
+                      rng.permutation(w.n_peers)[: w.n_peers // 3].astype(np.uint32)):
+        fo = np.empty(M + 1, np.uint32)
+        fp = np.empty(64 * M + 64, np.uint32)
+        args = [vp(np.ascontiguousarray(x)) for x in (w.pos, w.world, w.sender, w.repl)]
+        P = f(o.h, *args, M, vp(connected), len(connected), vp(fo), vp(fp), len(fp))
+        cs = set(connected.tolist())
+        rank = {p: i for i, p in enumerate(connected.tolist())}
+        for m in range(M):
+            want = sorted((p for p in peers[offs[m]:offs[m + 1]].tolist() if p in cs), key=rank.get)
+            assert fp[fo[m]:fo[m + 1]].tolist() == want, m
+        assert fo[M] == P
+    o.close()
