@@ -329,3 +329,22 @@ def test_full_c2_size_properties():
     got = np.concatenate([peers[offs[i]:offs[i + 1]] for i in idx])
     assert (got == o_peers).all()
     assert 0.8e7 < len(peers) < 1.3e7  # P ≈ 1.0e7
+
+
+def test_many_blocks_changing_tick_sizes():
+    """Ticks of many 256-message blocks whose sizes grow, shrink and cross look-back windows (64
+    blocks), alternating the single-launch tick (config 0: tagged granules, no clearing between
+    calls) with the three-launch and spill shapes (1, 7) that share the counter ring."""
+    w = synth.config_c2(repl_mode="mixed", scale=0.2)
+    r = mk_router(16)
+    o = orc.COracle(16)
+    r.apply_ops(w.ops)
+    o.apply_ops(w.ops)
+    window = 64 * 256
+    sizes = [3 * window + 17, 5 * 256, 7 * window + 1, 100, 2 * window, 2 * window, 12 * window - 3]
+    cfgs = [0, 0, 1, 0, 7, 0, 0]
+    for M, cfg in zip(sizes, cfgs):
+        assert M <= len(w.world)
+        r.set_route_config(cfg)
+        _compare(r, o, w.pos[:M], w.world[:M], w.sender[:M], w.repl[:M])
+    r.set_route_config(0)

@@ -1,5 +1,5 @@
 """Times every compiled route-kernel shape on the C2 tick (kernel-only HIP events) and checks
-that all shapes produce identical outputs. Usage: python tools/tune_route.py [--scale S]"""
+that all shapes produce identical outputs. Usage: python tools/tune_route.py [--scale S] [--workload c2|c3]"""
 import argparse
 import json
 import os
@@ -19,12 +19,17 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="timing-only configs (wrong outputs)")
     ap.add_argument("--raw-keys", action="store_true", help="route pre-quantised keys (skips kernel 1)")
     ap.add_argument("--slack", type=int, default=8, help="record slots per cube (wq_debug_set_record_slack)")
+    ap.add_argument("--workload", choices=["c2", "c3"], default="c2")
     a = ap.parse_args()
     import torch
     from worldql_server_amd import abi, synth
     from worldql_server_amd.router import Router
     dev = torch.device("cuda:0")
-    w = synth.config_c2(scale=a.scale)
+    if a.workload == "c3":
+        from worldql_server_amd import synth_ext
+        w = synth_ext.config_c3(scale=a.scale)
+    else:
+        w = synth.config_c2(scale=a.scale)
     M = len(w.world)
     r = Router(16, 0)
     s = torch.cuda.Stream(device=dev)
@@ -37,6 +42,12 @@ def main():
     repl = torch.from_numpy(w.repl).to(dev)
     offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
     cap = 12 * M
+    if a.workload == "c3":  # heavy fan-out: size the outputs with a counts-only call
+        cnt0 = torch.zeros(24, dtype=torch.uint8, device=dev)
+        r.route_device(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
+                       0, 0, 0, cnt0.data_ptr())
+        torch.cuda.synchronize()
+        cap = int(cnt0.cpu().numpy().view(abi.COUNTERS_DTYPE)[0]["n_pairs"]) + 1024
     peers = torch.empty(cap, dtype=torch.int32, device=dev)
     msgs = torch.empty(cap, dtype=torch.int32, device=dev)
     cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
@@ -59,10 +70,11 @@ def main():
             torch.cuda.synchronize()
             c = cnt.cpu().numpy().view(abi.COUNTERS_DTYPE)[0]
             P = int(c["n_pairs"])
-            h = (offs.cpu().numpy().tobytes(), peers[:P].cpu().numpy().tobytes(), msgs[:P].cpu().numpy().tobytes())
+            h = (offs.clone(), peers[:P].clone(), msgs[:P].clone())  # compared on the device
             if ref is None:
                 ref = h
-            assert a.no_check or h == ref, f"cfg {cfg} differs"
+            assert a.no_check or all(torch.equal(x, y) for x, y in zip(h, ref)), f"cfg {cfg} differs"
+            del h
             r.profile_enable(True)
             for _ in range(a.steps):
                 r.route_device(*args, **kw)
