@@ -185,6 +185,7 @@ def run_c3(a, rank, world_size, local_rank, dev):
                    0, 0, 0, cnt.data_ptr())
     torch.cuda.synchronize(dev)
     P = int(_counters(cnt)["n_pairs"][0])
+    r.set_fanout_hint(P / M)  # a server passes its previous tick's P / M; C3's ~42 picks count/scan/emit
     cap = P + 1024
     peers = torch.empty(cap, dtype=torch.int32, device=dev)
     msgs = torch.empty(cap, dtype=torch.int32, device=dev)
@@ -220,7 +221,8 @@ def run_c3(a, rank, world_size, local_rank, dev):
                  "parallelism": "1 GPU", "table_build_s": round(build_s, 3), "generate_s": round(gen_s, 1)},
                 {"bound": "hbm", "achieved": B / k_avg_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": B / k_avg_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                 "kernel": "route tick (single launch: tick_kernel)", "kernel_avg_us": k_avg_s * 1e6,
+                 "kernel": ("route tick (count / tile_scan / emit launches, wq_set_fanout_hint)" if P / M >= 16
+                            else "route tick (single launch: tick_kernel)"), "kernel_avg_us": k_avg_s * 1e6,
                  "algorithmic_bytes": B},
                 "synthetic (splitmix64, SURVEY.md §8(d) C3 generator)")
     if not a.no_cpu_baseline:
@@ -256,6 +258,7 @@ def _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s):
         P_in = int(res.peers.shape[0])
         P_own, F_own = be.read_counters()
         R = sr.last_recv
+        r.set_fanout_hint(P_own / max(R, 1))  # the owner's tick shape from its warm-up fan-out
         dist.barrier()
         torch.cuda.synchronize(dev)
         t_wall = time.perf_counter()

@@ -148,6 +148,15 @@ int wq_set_peer_positions(wq_router* h, const double* pos, size_t n_peers);
 int wq_set_peer_positions_device(wq_router* h, const double* d_pos, size_t n_peers);
 int wq_set_radius(wq_router* h, double radius);
 
+/* ---- tick shape: the caller's expected recipients per message (e.g. its previous tick's
+ * n_pairs / M; no reference counterpart — the Rust loop routes one message at a time,
+ * thread.rs:125-146). At >= WQ_HEAVY_FANOUT the tick runs as count / scan / emit launches, whose
+ * emit writes each block's outputs straight to HBM without holding a block that waits on its
+ * predecessors (C3: 2.18 -> 1.76 ms); below it, the single launch (C2). Results are identical
+ * either way; 0 (the default) means the single launch. */
+#define WQ_HEAVY_FANOUT 16.0
+int wq_set_fanout_hint(wq_router* h, double pairs_per_message);
+
 /* ---- F1: GlobalMessage to a named world (worldql_server/src/processing/global_message.rs:36-84)
  * Message m goes to every peer subscribed to at least one cube of world[m]
  * (AreaMap::get_subscribed_any_peers, area_map.rs:65-67), in ascending peer order, filtered by

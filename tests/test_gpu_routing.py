@@ -348,3 +348,25 @@ def test_many_blocks_changing_tick_sizes():
         r.set_route_config(cfg)
         _compare(r, o, w.pos[:M], w.world[:M], w.sender[:M], w.repl[:M])
     r.set_route_config(0)
+
+
+def test_fanout_hint_selects_identical_shape():
+    """wq_set_fanout_hint >= WQ_HEAVY_FANOUT (count / scan / emit with direct heavy emit) gives
+    the same CSR as the single launch, on heavy fan-out (60 peers per cube) and on C2-like input."""
+    r = mk_router(16)
+    o = orc.COracle(16)
+    n_cubes, per_cube = 40, 60
+    cx = np.repeat(np.arange(n_cubes) * 16.0 + 8.0, per_cube)
+    pos = np.stack([cx, np.full_like(cx, 8.0), np.full_like(cx, -8.0)], 1)
+    ops = abi.ops_array(np.zeros(len(cx), np.uint32), np.arange(len(cx), dtype=np.uint32),
+                        np.zeros(len(cx), np.uint8), pos=pos)
+    r.apply_ops(ops)
+    o.apply_ops(ops)
+    rng = synth.SplitMix64(77)
+    M = 20000
+    mpos = np.stack([rng.below(n_cubes, M) * 16.0 + rng.uniform(0.5, 15.5, M), rng.uniform(0.5, 15.5, M),
+                     -rng.uniform(0.5, 15.5, M)], 1)
+    args = (mpos, np.zeros(M, np.uint32), rng.below(n_cubes * per_cube, M), rng.below(3, M).astype(np.uint8))
+    for hint in (0.0, 60.0, float("nan"), 16.0):
+        r.set_fanout_hint(hint)
+        _compare(r, o, *args)

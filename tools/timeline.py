@@ -1,6 +1,6 @@
-"""Per-block phase timeline of the single-launch tick on the C2 workload (s_memrealtime, 100 MHz).
+"""Per-block phase timeline of the single-launch tick on the C2 (or C3) workload (s_memrealtime, 100 MHz).
 Prints percentiles over blocks of: start offset, count phase, prefix wait, emit phase, end offset.
-Usage: python tools/timeline.py [--cfg N] [--scale S]"""
+Usage: python tools/timeline.py [--cfg N] [--scale S] [--workload c2|c3]"""
 import argparse
 import os
 import sys
@@ -15,12 +15,17 @@ def main():
     ap.add_argument("--cfg", type=int, default=0)
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--dump", default="")
+    ap.add_argument("--workload", choices=["c2", "c3"], default="c2")
     a = ap.parse_args()
     import torch
     from worldql_server_amd import synth
     from worldql_server_amd.router import Router
     dev = torch.device("cuda:0")
-    w = synth.config_c2(scale=a.scale)
+    if a.workload == "c3":
+        from worldql_server_amd import synth_ext
+        w = synth_ext.config_c3(scale=a.scale)
+    else:
+        w = synth.config_c2(scale=a.scale)
     M = len(w.world)
     r = Router(16, 0)
     r.set_stream(torch.cuda.current_stream(dev).cuda_stream)  # stamps are zeroed on this stream
@@ -31,7 +36,7 @@ def main():
     sender = torch.from_numpy(w.sender.view(np.int32)).to(dev)
     repl = torch.from_numpy(w.repl).to(dev)
     offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
-    cap = 12 * M
+    cap = (50 if a.workload == "c3" else 12) * M
     peers = torch.empty(cap, dtype=torch.int32, device=dev)
     msgs = torch.empty(cap, dtype=torch.int32, device=dev)
     stamps = torch.zeros(4 * 65536, dtype=torch.int64, device=dev)

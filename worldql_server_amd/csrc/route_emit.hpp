@@ -267,6 +267,86 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
 }
 
 
+// Heavy fan-out (T > STAGE, e.g. C3's hotspots): instead of emit_row's windows, which re-read the
+// block's 256 record lines once per STAGE outputs, the block's outputs are written straight to
+// the global output, one output per thread and pass: output r (row-local) belongs to the message
+// j with st[j] <= r < st[j] + e[j] (binary search over the row's exclusive prefixes in LDS), and
+// its peer comes from the record's inline words (L2-resident since the count read them), the
+// cube's list, or the sender (OnlySelf). Consecutive threads write consecutive outputs, so every
+// store instruction is one contiguous 256-word run. The image's LDS is reused for the per-message
+// descriptors: op[0..255] st, op[256..511] source, op[512..767] skipped index, om[0..255] kind.
+constexpr uint8_t kDirNone = 0, kDirInline = 1, kDirList = 2, kDirSelf = 3;
+
+template <int STAGE>
+__device__ __forceinline__ void direct_meta(EmitRowSmem<STAGE>& es, const EmitOut& out, uint32_t m, uint32_t e,
+                                            uint2 inf, uint32_t st) {
+    static_assert(STAGE >= 3 * kBlock, "the descriptors live in the image's LDS");
+    const int tid = threadIdx.x;
+    uint8_t kind = kDirNone;
+    uint32_t src = 0, skip = kNone;
+    if (e) {
+        if (inf.x & kLocSelf) {
+            kind = kDirSelf;
+            src = out.sender[m];
+        } else if (inf.x & kLocGlobal) {
+            kind = kDirList;
+            src = (inf.x & ~kLocGlobal) + 1;
+            skip = inf.y;
+        } else {
+            kind = kDirInline;
+            src = inf.x;
+            const uint32_t s24 = inf.y & kSkipNone24;
+            skip = s24 == kSkipNone24 ? kNone : s24;
+        }
+    }
+    es.op[tid] = st;
+    es.op[kBlock + tid] = src;
+    es.op[2 * kBlock + tid] = skip;
+    es.om[tid] = kind;
+}
+
+template <int STAGE, int R>
+__device__ __forceinline__ void emit_direct(const EmitRowSmem<STAGE>& es, const TableView& tv, const EmitOut& out,
+                                            uint32_t m0, uint64_t g0, uint32_t T) {
+    // R: outputs per thread per pass, R loads in flight before the stores. 16 in the emit pass
+    // (C3: 2.0 -> 1.76 ms); the single-launch tick takes 4, since the kernel's register count,
+    // and so its residency, is set by its largest path (16 there costs C2 4 us)
+    const uint32_t* recs32 = reinterpret_cast<const uint32_t*>(tv.recs);
+    for (uint32_t r0 = threadIdx.x; r0 < T; r0 += R * kBlock) {
+        uint32_t peer[R], msg[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            const uint32_t r = r0 + u * kBlock;
+            peer[u] = 0;
+            msg[u] = 0;
+            if (r >= T) continue;
+            uint32_t lo = 0, n = kBlock;  // last j with st[j] <= r (st[0] = 0)
+#pragma unroll
+            for (int it = 0; it < 8; ++it) {
+                const uint32_t half = n >> 1;
+                if (es.op[lo + half] <= r) lo += half;
+                n -= half;
+            }
+            const uint32_t k = r - es.op[lo], src = es.op[kBlock + lo], sk = es.op[2 * kBlock + lo];
+            const uint32_t idx = k + (k >= sk ? 1u : 0u);
+            const uint8_t kind = es.om[lo];
+            peer[u] = kind == kDirSelf ? src
+                      : kind == kDirList ? tv.list[(uint64_t)src + idx]
+                                         : recs32[(uint64_t)src * 32 + kInlineWord0 + idx];
+            msg[u] = m0 + lo;
+        }
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            const uint32_t r = r0 + u * kBlock;
+            const uint64_t o = g0 + r;
+            if (r < T && o < out.capacity) {
+                out.peers[o] = peer[u];
+                if (out.msgs) out.msgs[o] = msg[u];
+            }
+        }
+    }
+}
+
 // Pass 3 of the three-launch tick: one 256-message row per block. CSR offsets = count-block
 // prefix (tile_scan) + the in-block prefix, then emit_row.
 template <int STAGE, int U, bool RADIUS = false>
@@ -292,6 +372,12 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(EmitParams p) {
     for (int u = 0; u < kWaves; ++u) g += part_tot[u];
     if (m < p.M) p.offsets[m] = g + st;
     if (!p.peers) return;  // counts-only call: offsets are all that is asked for
+    if (!RADIUS && T > (uint32_t)STAGE) {  // block-uniform: heavy fan-out, no windows
+        direct_meta<STAGE>(sm, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl}, m, e, inf, st);
+        lds_barrier();
+        emit_direct<STAGE, 16>(sm, p.t, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl}, m0, g, T);
+        return;
+    }
     emit_row<STAGE, U, RADIUS>(sm, p.t, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl}, m0, e, inf,
                                st, g, T);
 }

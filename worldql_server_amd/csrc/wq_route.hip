@@ -75,6 +75,7 @@ const Cfg kCfgs[] = {
 #undef WQ_CFGS
 #undef WQ_CFG3
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+constexpr int kCfgHeavy = 1;  // the default shape under wq_set_fanout_hint >= WQ_HEAVY_FANOUT
 
 }  // namespace
 
@@ -112,7 +113,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
                  uint32_t* d_peers, uint32_t* d_msgs, size_t capacity) {
     hipStream_t s = h->stream;
     RouteWs& rw = h->rws;
-    const Cfg& cfg = kCfgs[h->route_cfg];
+    const Cfg& cfg = kCfgs[h->route_cfg == 0 && h->heavy_fanout ? kCfgHeavy : h->route_cfg];
     wq_route_counters *cur, *nxt;
     int rc0 = route_counters(h, M, d_offsets, &cur, &nxt);
     if (rc0 || !cur) return rc0;

@@ -199,6 +199,12 @@ int wq_set_radius(wq_router* h, double radius) {
     return WQ_OK;
 }
 
+int wq_set_fanout_hint(wq_router* h, double pairs_per_message) {
+    if (!h) return WQ_E_INVALID;
+    h->heavy_fanout = pairs_per_message >= WQ_HEAVY_FANOUT;  // NaN compares false: single launch
+    return WQ_OK;
+}
+
 int wq_debug_set_route_config(wq_router* h, int cfg) {
     if (!h || cfg < 0 || cfg >= route_config_count()) return WQ_E_INVALID;
     h->route_cfg = cfg;

@@ -76,6 +76,7 @@ def load_library(build_if_missing: bool = True):
         "wq_set_peer_positions": ([vp, vp, sz], i32),
         "wq_set_peer_positions_device": ([vp, vp, sz], i32),
         "wq_set_radius": ([vp, ctypes.c_double], i32),
+        "wq_set_fanout_hint": ([vp, ctypes.c_double], i32),
         "wq_shard_ops": ([vp, vp, sz, u32, vp], i32),
         "wq_shard_messages_device": ([vp, vp, vp, vp, vp, vp, sz, u32, vp, vp], i32),
         "wq_route_records_device": ([vp, vp, sz, vp, vp, vp, sz, vp], i32),
@@ -285,6 +286,11 @@ class Router:
 
     def set_radius(self, radius: float) -> None:
         self._check(self.lib.wq_set_radius(self.h, float(radius)))
+
+    def set_fanout_hint(self, pairs_per_message: float) -> None:
+        """Expected recipients per message (e.g. the previous tick's P / M): >= 16 selects the
+        count / scan / emit tick shape (wq_set_fanout_hint)."""
+        self._check(self.lib.wq_set_fanout_hint(self.h, float(pairs_per_message)))
 
     def set_stream(self, stream_ptr: int | None) -> None:
         self._check(self.lib.wq_set_stream(self.h, stream_ptr or None))
