@@ -382,28 +382,55 @@ __global__ __launch_bounds__(kBlock) void k_delta_apply_group(DeltaTable tb, con
     const uint32_t stride = gridDim.x * kGroups;
     const uint4* recs4 = reinterpret_cast<const uint4*>(tb.recs);
     uint32_t c = blockIdx.x * kGroups + grp;
-    // this cube's plan and record header; the next cube's are fetched while this one merges
-    uint4 ci = make_uint4(0, 0, 0, 0), h0 = ci, h1 = ci;
+    // Software pipeline over the group's cubes c, c + stride, ...: while cube c merges, the next
+    // cube's list (<= kGroupList words: kPref per lane) is in flight in registers and the header
+    // of the one after it is being fetched, so a cube's list latency is paid once per group, not
+    // once per cube. (Lists of different cubes are disjoint, and a relocated list moves to fresh
+    // space, so prefetching never reads words this group or another is about to write.)
+    constexpr int kPref = (int)(kGroupList / kG);
+    uint4 ci = make_uint4(0, 0, 0, 0), h0 = ci, h1 = ci, ci_n = ci, h0_n = ci, h1_n = ci;
+    uint32_t pref[kPref];
     if (c < n_dc) {
         ci = cinfo[c];
+        if (c + stride < n_dc) ci_n = cinfo[c + stride];
         h0 = recs4[8ull * ci.x];
         h1 = recs4[8ull * ci.x + 1];
+        if (c + stride < n_dc) {
+            h0_n = recs4[8ull * ci_n.x];
+            h1_n = recs4[8ull * ci_n.x + 1];
+        }
+#pragma unroll
+        for (int k = 0; k < kPref; ++k) {
+            const uint32_t i = (uint32_t)(gl + k * kG);
+            pref[k] = i < ci.w ? tb.list[h0.w + 1 + i] : 0u;
+        }
     }
     for (; c < n_dc; c += stride) {
-        const uint32_t cn = c + stride;
-        uint4 ci_n = ci;
-        if (cn < n_dc) ci_n = cinfo[cn];
+        const uint32_t cn = c + stride, cnn = c + 2 * stride;
+        uint4 ci_nn = ci_n;
+        if (cnn < n_dc) ci_nn = cinfo[cnn];
         const uint32_t slot = ci.x, s0 = ci.y, nch = ci.z, oc = ci.w;
         Record* rec = tb.recs + slot;
         const uint32_t off = h0.w, cap0 = h1.z;
         uint32_t* cur = sm.buf[grp][0];
         uint32_t* nxt = sm.buf[grp][1];
         wave_lds_sync();  // the previous cube's LDS reads are done
-        for (uint32_t k = gl; k < oc; k += kG) cur[k] = tb.list[off + 1 + k];
-        uint4 h0_n = h0, h1_n = h1;
-        if (cn < n_dc) {
-            h0_n = recs4[8ull * ci_n.x];
-            h1_n = recs4[8ull * ci_n.x + 1];
+#pragma unroll
+        for (int k = 0; k < kPref; ++k) {
+            const uint32_t i = (uint32_t)(gl + k * kG);
+            if (i < oc) cur[i] = pref[k];
+        }
+        if (cn < n_dc) {  // the next cube's list (its header arrived during the previous cube)
+#pragma unroll
+            for (int k = 0; k < kPref; ++k) {
+                const uint32_t i = (uint32_t)(gl + k * kG);
+                pref[k] = i < ci_n.w ? tb.list[h0_n.w + 1 + i] : 0u;
+            }
+        }
+        uint4 h0_nn = h0_n, h1_nn = h1_n;
+        if (cnn < n_dc) {
+            h0_nn = recs4[8ull * ci_nn.x];
+            h1_nn = recs4[8ull * ci_nn.x + 1];
         }
         wave_lds_sync();
         uint32_t n = oc;
@@ -495,6 +522,9 @@ __global__ __launch_bounds__(kBlock) void k_delta_apply_group(DeltaTable tb, con
         ci = ci_n;
         h0 = h0_n;
         h1 = h1_n;
+        ci_n = ci_nn;
+        h0_n = h0_nn;
+        h1_n = h1_nn;
     }
     if (de) atomicAdd(&acc[0], (unsigned long long)de);
     if (dl) atomicAdd(&acc[1], (unsigned long long)dl);
