@@ -45,6 +45,20 @@ def _line(a, world_size, value, ms_per_step, scaling, workload, config, roofline
             "config": {"workload": workload, **config}, "roofline": roofline}
 
 
+def _pmc_traffic(name: str, M: int, P: int):
+    """HBM bytes per tick from a committed rocprofv3 --pmc summary (tools/pmc_route.sh +
+    tools/pmc_summary.py) of the same workload, or None when there is none for this (M, P)."""
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    if d.get("messages_per_tick") != M or d.get("pairs_per_tick") != P:
+        return None
+    return d["hbm_bytes_per_launch"]
+
+
 def _counters(cnt):
     from worldql_server_amd import abi
     return cnt.cpu().numpy().view(abi.COUNTERS_DTYPE)
@@ -220,7 +234,7 @@ def run_c3(a, rank, world_size, local_rank, dev):
                  "cubes": int(st["n_cubes"]), "pairs_per_tick": P, "candidates_per_tick": F,
                  "parallelism": "1 GPU", "table_build_s": round(build_s, 3), "generate_s": round(gen_s, 1)},
                 {"bound": "hbm", "achieved": B / k_avg_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                 "frac": B / k_avg_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                 "frac": B / k_avg_s / 1e9 / HBM_PEAK_GBS, "traffic": _pmc_traffic("r01_pmc_route_c3.json", M, P),
                  "kernel": ("route tick (count / tile_scan / emit launches, wq_set_fanout_hint)" if P / M >= 16
                             else "route tick (single launch: tick_kernel)"), "kernel_avg_us": k_avg_s * 1e6,
                  "algorithmic_bytes": B},
