@@ -153,7 +153,9 @@ int wq_set_radius(wq_router* h, double radius);
  * thread.rs:125-146). At >= WQ_HEAVY_FANOUT the tick runs as count / scan / emit launches, whose
  * emit writes each block's outputs straight to HBM without holding a block that waits on its
  * predecessors (C3: 2.18 -> 1.76 ms); below it, the single launch (C2). Results are identical
- * either way; 0 (the default) means the single launch. */
+ * either way. Until the caller sets a hint, the host-array wq_route_tick sets it itself from each
+ * tick's n_pairs / M (device-pointer ticks never read their counters back, so they keep the last
+ * value; the initial one is the single launch). */
 #define WQ_HEAVY_FANOUT 16.0
 int wq_set_fanout_hint(wq_router* h, double pairs_per_message);
 

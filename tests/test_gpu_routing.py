@@ -370,3 +370,23 @@ def test_fanout_hint_selects_identical_shape():
     for hint in (0.0, 60.0, float("nan"), 16.0):
         r.set_fanout_hint(hint)
         _compare(r, o, *args)
+
+
+def test_auto_fanout_shape_from_host_ticks():
+    """Without a hint, each host-array tick picks the next tick's shape from its own P / M (here
+    ~60 pairs per message: the second tick runs count / scan / emit); results stay identical."""
+    r = mk_router(16)
+    o = orc.COracle(16)
+    n_cubes, per_cube = 30, 60
+    cx = np.repeat(np.arange(n_cubes) * 16.0 + 8.0, per_cube)
+    pos = np.stack([cx, np.full_like(cx, 8.0), np.full_like(cx, 8.0)], 1)
+    ops = abi.ops_array(np.zeros(len(cx), np.uint32), np.arange(len(cx), dtype=np.uint32),
+                        np.zeros(len(cx), np.uint8), pos=pos)
+    r.apply_ops(ops)
+    o.apply_ops(ops)
+    rng = synth.SplitMix64(91)
+    for M in (9000, 9000, 300):
+        mpos = np.stack([rng.below(n_cubes, M) * 16.0 + rng.uniform(0.5, 15.5, M), rng.uniform(0.5, 15.5, M),
+                         rng.uniform(0.5, 15.5, M)], 1)
+        _compare(r, o, mpos, np.zeros(M, np.uint32), rng.below(n_cubes * per_cube, M),
+                 rng.below(3, M).astype(np.uint8))

@@ -129,6 +129,7 @@ struct wq_router {
     wq::DevBuf shard_hist, rec_keys, rec_w, rec_s, rec_r;
     int route_cfg = 0;  // route kernel shapes (wq_route.hip kCfgs)
     bool heavy_fanout = false;  // wq_set_fanout_hint: default shape -> kCfgHeavy
+    bool fanout_auto = true;    // until wq_set_fanout_hint: wq_route_tick sets heavy_fanout from its P / M
     // host-pointer convenience buffers
     wq::DevBuf h_in, h_out;
     // C5 radius filter (wq_set_radius / wq_set_peer_positions)

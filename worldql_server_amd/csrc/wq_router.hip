@@ -202,6 +202,7 @@ int wq_set_radius(wq_router* h, double radius) {
 int wq_set_fanout_hint(wq_router* h, double pairs_per_message) {
     if (!h) return WQ_E_INVALID;
     h->heavy_fanout = pairs_per_message >= WQ_HEAVY_FANOUT;  // NaN compares false: single launch
+    h->fanout_auto = false;  // the caller decides from now on
     return WQ_OK;
 }
 
@@ -333,7 +334,10 @@ int wq_route_tick(wq_router* h, const double* pos, const int64_t* keys, const ui
                           cap ? reinterpret_cast<uint32_t*>(dout + op) : nullptr,
                           (msgs && cap) ? reinterpret_cast<uint32_t*>(dout + om) : nullptr, cap);
     if (rc) return rc;
-    return read_back(h, M, dout, op, om, cap, capacity, offsets, peers, msgs, n_pairs);
+    rc = read_back(h, M, dout, op, om, cap, capacity, offsets, peers, msgs, n_pairs);
+    if ((rc == WQ_OK || rc == WQ_E_CAPACITY) && h->fanout_auto && M)  // the next tick's shape
+        h->heavy_fanout = (double)*n_pairs >= WQ_HEAVY_FANOUT * (double)M;
+    return rc;
 }
 
 int wq_route_global_device(wq_router* h, const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
