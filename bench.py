@@ -40,28 +40,76 @@ METRIC = "routed msg→peer pairs/sec per tick at 1/2/4/8 GPUs; % HBM roofline"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=["c1", "c2", "c3", "c4", "c5"], default="c2",
-                    help="c2 = the headline (BASELINE.json configs[1]); c1/c3/c4/c5 = SURVEY.md §8(d)")
-    ap.add_argument("--steps", type=int, default=None, help="timed ticks (default 50; c4 20, c3/c5 10)")
+    ap.add_argument("--config", choices=["c1", "c2", "c3", "c4", "c5"], default=None,
+                    help="default: the headline, C3 (north_star's 1M peers / 10M messages per tick) with the C2 "
+                         "line nested under extra.c2 at N = 1; c1..c5 = one SURVEY.md §8(d) config alone")
+    ap.add_argument("--no-extra", action="store_true", help="headline only (skip the nested C2 line)")
+    ap.add_argument("--steps", type=int, default=None, help="timed ticks (default c3/c5 10, c4 20, c1/c2 50)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed ticks (default 10; c3/c4/c5 2)")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink C2 (tests only; 1.0 = the headline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline's routing work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shard", choices=["world", "cube"], default="world",
                     help="multi-GPU partitioning (see module docstring)")
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "r01_pmc_route.json"))
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "r02_pmc_route.json"),
+                    help="rocprofv3 --pmc summary of the C2 tick (roofline.traffic)")
     a = ap.parse_args()
+    a.headline = a.config is None
+    if a.headline:
+        a.config = "c3"
+    _default_steps(a)
+    return a
+
+
+def _default_steps(a):
     if a.steps is None:
         a.steps = {"c1": 50, "c2": 50, "c3": 10, "c4": 20, "c5": 10}[a.config]
     if a.warmup is None:
         a.warmup = 10 if a.config in ("c1", "c2") else 2
-    return a
 
 
 def algorithmic_bytes(M: int, F: int, P: int) -> int:
     """B = M*(24 pos + 4 world + 4 sender + 1 repl) + M*32 bucket record
     + F*4 candidate ids + P*8 (u32 msg, u32 peer) + (M+1)*4 CSR offsets."""
     return 69 * M + 4 * F + 8 * P + 4
+
+
+def timed_ticks(tick, steps: int, stream, dev, world_size: int, routers=()) -> float:
+    """The timed region of every bench line: barrier + synchronize, `steps` calls of tick() between
+    two HIP events on the launch stream, synchronize + barrier; milliseconds. Afterwards every
+    router's sticky health words (wq_route_health) must be clean — the run's counters were never
+    read, so this is what proves no timed tick gave up a spin or overflowed its capacity."""
+    import torch
+    import torch.distributed as dist
+    for r in routers:
+        r.route_health()  # clear whatever the untimed ticks left
+    if world_size > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(steps):
+        tick()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world_size > 1:
+        dist.barrier()
+    for r in routers:
+        r.check_health()
+    return ev0.elapsed_time(ev1)
+
+
+def roofline(B: int, tick_s: float, kernel: str, traffic=None, event_us=None) -> dict:
+    """roofline for a tick moving B algorithmic bytes in tick_s seconds: the
+    time is the timed region's ms_per_step (every launch of the tick, back to back), never the
+    event-bracketed per-launch time, which carries event overhead (event_us, for reference)."""
+    achieved = B / tick_s / 1e9
+    out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kernel, "tick_us": tick_s * 1e6,
+           "algorithmic_bytes": B}
+    if event_us is not None:
+        out["kernel_event_us"] = event_us
+    return out
 
 
 def shard_workload(rank: int, scale: float = 1.0):
@@ -179,10 +227,27 @@ def main():
 
     if a.config != "c2":
         import bench_configs
-        return bench_configs.run(a, rank, world_size, local_rank, dev)
-    if a.shard == "cube":
-        return run_cube(a, rank, world_size, local_rank, dev)
+        out = bench_configs.run(a, rank, world_size, local_rank, dev)
+    elif a.shard == "cube":
+        out = run_cube(a, rank, world_size, local_rank, dev)
+    else:
+        out = run_c2(a, rank, world_size, local_rank, dev)
+    if a.headline and world_size == 1 and not a.no_extra:
+        # the C2 line (BASELINE.json configs[1]) beside the C3 headline, with its own steps
+        import copy
+        a2 = copy.copy(a)
+        a2.config, a2.steps, a2.warmup, a2.headline = "c2", None, None, False
+        _default_steps(a2)
+        out["extra"] = {"c2": run_c2(a2, rank, world_size, local_rank, dev)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world_size > 1:
+        dist.destroy_process_group()
 
+
+def run_c2(a, rank, world_size, local_rank, dev) -> dict:
+    """C2 (BASELINE.json configs[1]): one world per GPU, 100k peers x 27 cubes, 1M messages."""
+    import torch
     from worldql_server_amd import abi
     from worldql_server_amd.router import Router
 
@@ -228,20 +293,7 @@ def main():
     P, F = int(c["n_pairs"]), int(c["n_candidates"])
     assert c["overflow"] == 0 and c["error"] == 0, c
 
-    if world_size > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t_wall = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(a.steps):
-        tick()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    t_wall = time.perf_counter() - t_wall
-    if world_size > 1:
-        dist.barrier()
-    t_ms = ev0.elapsed_time(ev1)
+    t_ms = timed_ticks(tick, a.steps, stream, dev, world_size, [r])
     t_max_ms, pairs_all = reduce_over_ranks(t_ms, P, dev, world_size)
 
     # kernel-only time of the route launch: HIP events recorded on the launch stream around
@@ -253,7 +305,6 @@ def main():
     r.profile_enable(False)
     k_avg_s = k_ms / launches / 1e3
     B = algorithmic_bytes(M, F, P)
-    achieved = B / k_avg_s / 1e9
     traffic = None
     if os.path.exists(a.pmc_file):
         with open(a.pmc_file) as f:
@@ -281,21 +332,16 @@ def main():
             "cubes": int(st["n_cubes"]), "pairs_per_tick": P, "candidates_per_tick": F,
             "parallelism": f"world-sharded x{world_size}", "table_build_s": round(build_s, 3),
         },
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "route tick (single launch: tick_kernel)", "kernel_avg_us": k_avg_s * 1e6,
-                     "algorithmic_bytes": B},
+        "roofline": roofline(B, t_max_ms / a.steps / 1e3, "route tick (single launch: tick_kernel)", traffic,
+                             k_avg_s * 1e6),
     }
     if rank == 0 and world_size == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(w, a.cpu_seconds)
         threads = min(16, os.cpu_count() or 1)
         if threads > 1:
             out["cpu_baseline_mt"] = cpu_baseline_mt(w, threads)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
     r.close()
-    if world_size > 1:
-        dist.destroy_process_group()
+    return out
 
 
 def run_cube(a, rank, world_size, local_rank, dev):
@@ -374,11 +420,8 @@ def run_cube(a, rank, world_size, local_rank, dev):
     if rank == 0 and world_size == 1 and not a.no_cpu_baseline:
         w1 = shard_workload(0, a.scale)
         out["cpu_baseline"] = cpu_baseline(w1, a.cpu_seconds)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
     r.close()
-    if world_size > 1:
-        dist.destroy_process_group()
+    return out
 
 
 if __name__ == "__main__":

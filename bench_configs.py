@@ -26,16 +26,13 @@ import time
 import numpy as np
 
 import bench
-from bench import HBM_PEAK_GBS, METRIC, algorithmic_bytes, reduce_over_ranks
+from bench import HBM_PEAK_GBS, METRIC, algorithmic_bytes, reduce_over_ranks, roofline, timed_ticks
+
+PMC_C3 = "r02_pmc_route_c3.json"  # rocprofv3 --pmc summary of the C3 tick (tools/pmc_route.sh)
 
 
 def run(a, rank, world_size, local_rank, dev):
     return {"c1": run_c1, "c3": run_c3, "c4": run_c4, "c5": run_c5}[a.config](a, rank, world_size, local_rank, dev)
-
-
-def _emit(out, rank):
-    if rank == 0:
-        print(json.dumps(out), flush=True)
 
 
 def _line(a, world_size, value, ms_per_step, scaling, workload, config, roofline, data):
@@ -134,18 +131,8 @@ def run_c1(a, rank, world_size, local_rank, dev):
     c = _counters(cnt)[0]
     F = int(c["n_candidates"])
     assert c["overflow"] == 0 and c["error"] == 0, c
-    if world_size > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for _ in range(a.steps):
-        r.route_device(*args, 0)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world_size > 1:
-        torch.distributed.barrier()
-    t_max_ms, pairs_all = reduce_over_ranks(ev0.elapsed_time(ev1), P, dev, world_size)
+    t_ms = timed_ticks(lambda: r.route_device(*args, 0), a.steps, stream, dev, world_size, [r])
+    t_max_ms, pairs_all = reduce_over_ranks(t_ms, P, dev, world_size)
     r.profile_enable(True)
     for _ in range(a.steps):
         r.route_device(*args, 0)
@@ -158,14 +145,12 @@ def run_c1(a, rank, world_size, local_rank, dev):
                 "(BASELINE.json configs[0], the reference's CPU case; launch-latency bound on a GPU)",
                 {"messages_per_tick": M, "peers": w.n_peers, "pairs_per_tick": P, "candidates_per_tick": F,
                  "parallelism": f"replicas x{world_size}"},
-                {"bound": "hbm", "achieved": B / k_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                 "frac": B / k_s / 1e9 / HBM_PEAK_GBS, "traffic": None, "kernel": "route tick (single launch)",
-                 "kernel_avg_us": k_s * 1e6, "algorithmic_bytes": B},
+                roofline(B, t_max_ms / a.steps / 1e3, "route tick (single launch)", None, k_s * 1e6),
                 "synthetic (splitmix64, SURVEY.md §8(d) C1 generator)")
     if rank == 0 and world_size == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"], out["cpu_baseline_faithful"] = _cpu_c1(w, 20)
     r.close()
-    _emit(out, rank)
+    return out
 
 
 # ---- C3 ---------------------------------------------------------------------------------------
@@ -212,13 +197,7 @@ def run_c3(a, rank, world_size, local_rank, dev):
     c = _counters(cnt)[0]
     P, F = int(c["n_pairs"]), int(c["n_candidates"])
     assert c["overflow"] == 0 and c["error"] == 0, c
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for _ in range(a.steps):
-        r.route_device(*args, 0)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    t_ms = ev0.elapsed_time(ev1)
+    t_ms = timed_ticks(lambda: r.route_device(*args, 0), a.steps, stream, dev, 1, [r])
     r.profile_enable(True)
     for _ in range(a.steps):
         r.route_device(*args, 0)
@@ -226,6 +205,8 @@ def run_c3(a, rank, world_size, local_rank, dev):
     r.profile_enable(False)
     k_avg_s = k_ms / launches / 1e3
     B = algorithmic_bytes(M, F, P)
+    kernel = ("route tick (count / tile_scan / emit launches, wq_set_fanout_hint)" if P / M >= 16
+              else "route tick (single launch: tick_kernel)")
     out = _line(a, 1, P * a.steps / (t_ms / 1e3), t_ms / a.steps, "strong",
                 "C3: 1M peers x 3x3x3, 10M LocalMessages/tick, 256 Zipf(1) Gaussian hotspots (sigma 128) + 10% "
                 "uniform in U[-4096,4096)^3, cube_size 16, ExceptSelf, whole configuration on one GPU"
@@ -233,16 +214,12 @@ def run_c3(a, rank, world_size, local_rank, dev):
                 {"messages_per_tick": M, "peers": w.n_peers, "subscriptions": int(st["n_entries"]),
                  "cubes": int(st["n_cubes"]), "pairs_per_tick": P, "candidates_per_tick": F,
                  "parallelism": "1 GPU", "table_build_s": round(build_s, 3), "generate_s": round(gen_s, 1)},
-                {"bound": "hbm", "achieved": B / k_avg_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                 "frac": B / k_avg_s / 1e9 / HBM_PEAK_GBS, "traffic": _pmc_traffic("r01_pmc_route_c3.json", M, P),
-                 "kernel": ("route tick (count / tile_scan / emit launches, wq_set_fanout_hint)" if P / M >= 16
-                            else "route tick (single launch: tick_kernel)"), "kernel_avg_us": k_avg_s * 1e6,
-                 "algorithmic_bytes": B},
+                roofline(B, t_ms / a.steps / 1e3, kernel, _pmc_traffic(PMC_C3, M, P), k_avg_s * 1e6),
                 "synthetic (splitmix64, SURVEY.md §8(d) C3 generator)")
     if not a.no_cpu_baseline:
         out["cpu_baseline"] = _cpu_route_sample(w, a.cpu_seconds, "C3")
-    _emit(out, rank)
     r.close()
+    return out
 
 
 def _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s):
@@ -301,9 +278,8 @@ def _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s):
                  "frac": B / k_avg_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
                  "kernel": "route tick on rank 0's shard", "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
                 "synthetic (splitmix64, SURVEY.md §8(d) C3 generator)")
-    _emit(out, rank)
     r.close()
-    dist.destroy_process_group()
+    return out
 
 
 def _cpu_route_sample(w, seconds, name):
@@ -423,10 +399,8 @@ def run_c4(a, rank, world_size, local_rank, dev):
                 "synthetic (splitmix64, SURVEY.md §8(d) C4 generator)")
     if rank == 0 and world_size == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = _cpu_churn_sample(init, ticks, c4.world, a.cpu_seconds)
-    _emit(out, rank)
     r.close()
-    if world_size > 1:
-        dist.destroy_process_group()
+    return out
 
 
 def _cpu_churn_sample(init, ticks, world, seconds):
@@ -516,8 +490,57 @@ def run_c5(a, rank, world_size, local_rank, dev):
                  "kernel": "whole tick (incremental update + positions + radius route); route launches alone below",
                  "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
                 "synthetic (splitmix64, SURVEY.md §8(d) C5 generator)")
-    _emit(out, rank)
     r.close()
+    if not a.no_cpu_baseline:
+        out["cpu_baseline"] = _cpu_c5_sample(init, [t[0] for t in ticks[:a.warmup + 1]], ticks[a.warmup][1],
+                                             c5.radius, a.cpu_seconds)
+    return out
+
+
+def _cpu_c5_sample(init, tick_ops, pos_after, radius, seconds):
+    """C5 on 1 host thread by the C restatement, one whole tick estimated from two timed parts:
+      route  the tick's 1M messages with the radius filter (wqo_route_radius), on a table brought
+             to the tick's state in checker mode (wqo_set_fast; the route itself is the same code);
+      churn  a strided sample of the tick's ops applied to a FAITHFUL table (the reference's
+             O(#cubes) scan per unsubscribe, area_map.rs:113-116), scaled to all of the tick's ops.
+    value = pairs of the tick / (t_route + n_ops * t_per_op). The tables are built untimed."""
+    import ctypes
+    from oracle import oracle as orc
+    vp = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    M = len(pos_after)
+    fast = orc.COracle(16)
+    fast.set_fast(True)
+    fast.apply_ops(init)
+    for ops in tick_ops:  # the table as the first timed tick sees it
+        fast.apply_ops(ops)
+    world = np.zeros(M, np.uint32)
+    sender = np.arange(M, dtype=np.uint32)
+    repl = np.zeros(M, np.uint8)
+    offs = np.empty(M + 1, np.uint32)
+    t0 = time.perf_counter()
+    P = fast.lib.wqo_route_radius(fast.h, vp(np.ascontiguousarray(pos_after)), vp(world), vp(sender), vp(repl), M,
+                                  vp(np.ascontiguousarray(pos_after)), M, float(radius), vp(offs), None, 0, None)
+    t_route = time.perf_counter() - t0
+    fast.close()
+    faith = orc.COracle(16)
+    faith.apply_ops(init)
+    n_ops = len(ops)
+    stride = max(1, n_ops // 4096)
+    sample = np.ascontiguousarray(ops[::stride])
+    done, t_ops = 0, 0.0
+    while done < len(sample) and t_ops < seconds / 2:
+        chunk = sample[done:done + 64]
+        t0 = time.perf_counter()
+        faith.apply_ops(chunk)
+        t_ops += time.perf_counter() - t0
+        done += len(chunk)
+    faith.close()
+    t_tick = t_route + n_ops * (t_ops / done)
+    return {"value": P / t_tick, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"C5 tick estimate: {M} messages routed with the radius filter in {t_route:.2f} s "
+                      f"({P} pairs) + {done} of the tick's {n_ops} churn ops (every {stride}th) applied with the "
+                      f"reference's O(#cubes) unsubscribe scan in {t_ops:.2f} s, scaled to all {n_ops} ops: "
+                      f"{t_tick:.1f} s per tick, oracle/wq_oracle.c on 1 host thread"}
 
 
 def _run_c5_sharded(a, rank, world_size, local_rank, dev):
@@ -586,6 +609,54 @@ def _run_c5_sharded(a, rank, world_size, local_rank, dev):
                 {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                  "traffic": None, "kernel": "whole sharded tick (update + exchange + radius route)"},
                 "synthetic (splitmix64, SURVEY.md §8(d) C5 generator)")
-    _emit(out, rank)
     r.close()
-    dist.destroy_process_group()
+    if not a.no_cpu_baseline:
+        out["cpu_baseline"] = _cpu_c5_sample(init, [t[0] for t in ticks[:a.warmup + 1]], ticks[a.warmup][1],
+                                             c5.radius, a.cpu_seconds)
+    return out
+
+
+def _cpu_c5_sample(init, tick_ops, pos_after, radius, seconds):
+    """C5 on 1 host thread by the C restatement, one whole tick estimated from two timed parts:
+      route  the tick's 1M messages with the radius filter (wqo_route_radius), on a table brought
+             to the tick's state in checker mode (wqo_set_fast; the route itself is the same code);
+      churn  a strided sample of the tick's ops applied to a FAITHFUL table (the reference's
+             O(#cubes) scan per unsubscribe, area_map.rs:113-116), scaled to all of the tick's ops.
+    value = pairs of the tick / (t_route + n_ops * t_per_op). The tables are built untimed."""
+    import ctypes
+    from oracle import oracle as orc
+    vp = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    M = len(pos_after)
+    fast = orc.COracle(16)
+    fast.set_fast(True)
+    fast.apply_ops(init)
+    for ops in tick_ops:  # the table as the first timed tick sees it
+        fast.apply_ops(ops)
+    world = np.zeros(M, np.uint32)
+    sender = np.arange(M, dtype=np.uint32)
+    repl = np.zeros(M, np.uint8)
+    offs = np.empty(M + 1, np.uint32)
+    t0 = time.perf_counter()
+    P = fast.lib.wqo_route_radius(fast.h, vp(np.ascontiguousarray(pos_after)), vp(world), vp(sender), vp(repl), M,
+                                  vp(np.ascontiguousarray(pos_after)), M, float(radius), vp(offs), None, 0, None)
+    t_route = time.perf_counter() - t0
+    fast.close()
+    faith = orc.COracle(16)
+    faith.apply_ops(init)
+    n_ops = len(ops)
+    stride = max(1, n_ops // 4096)
+    sample = np.ascontiguousarray(ops[::stride])
+    done, t_ops = 0, 0.0
+    while done < len(sample) and t_ops < seconds / 2:
+        chunk = sample[done:done + 64]
+        t0 = time.perf_counter()
+        faith.apply_ops(chunk)
+        t_ops += time.perf_counter() - t0
+        done += len(chunk)
+    faith.close()
+    t_tick = t_route + n_ops * (t_ops / done)
+    return {"value": P / t_tick, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"C5 tick estimate: {M} messages routed with the radius filter in {t_route:.2f} s "
+                      f"({P} pairs) + {done} of the tick's {n_ops} churn ops (every {stride}th) applied with the "
+                      f"reference's O(#cubes) unsubscribe scan in {t_ops:.2f} s, scaled to all {n_ops} ops: "
+                      f"{t_tick:.1f} s per tick, oracle/wq_oracle.c on 1 host thread"}

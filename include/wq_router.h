@@ -129,8 +129,8 @@ int wq_route_tick(wq_router* h, const double* pos, const int64_t* keys, const ui
                   const uint32_t* sender, const uint8_t* repl, size_t n_msgs, uint32_t* offsets,
                   uint32_t* peers, uint32_t* msgs, size_t capacity, size_t* n_pairs);
 /* Asynchronous form on device pointers; nothing is read back. counters (device pointer to a
- * wq_route_counters) receives P, F and the overflow / error flags. Pairs beyond `capacity`
- * are not written. */
+ * wq_route_counters) receives P, F and the overflow / error flags (also kept sticky for
+ * wq_route_health). Pairs beyond `capacity` are not written. */
 int wq_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_keys,
                          const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
                          size_t n_msgs, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs,
@@ -157,6 +157,8 @@ int wq_set_radius(wq_router* h, double radius);
  * tick's n_pairs / M (device-pointer ticks never read their counters back, so they keep the last
  * value; the initial one is the single launch). */
 #define WQ_HEAVY_FANOUT 16.0
+/* A negative or NaN hint hands the choice back to the automatic rule (host-array ticks of >= 256
+ * messages set the next tick's shape from their own n_pairs / M). */
 int wq_set_fanout_hint(wq_router* h, double pairs_per_message);
 
 /* ---- F1: GlobalMessage to a named world (worldql_server/src/processing/global_message.rs:36-84)
@@ -164,7 +166,8 @@ int wq_set_fanout_hint(wq_router* h, double pairs_per_message);
  * (AreaMap::get_subscribed_any_peers, area_map.rs:65-67), in ascending peer order, filtered by
  * repl[m] like LocalMessage: ExceptSelf drops sender[m], OnlySelf keeps only sender[m] (if it is
  * subscribed in that world), IncludingSelf keeps every peer. A world with no subscriptions yields
- * nothing (global_message.rs:50-54). Output, capacity and counters as wq_route_tick. The "@global"
+ * nothing (global_message.rs:50-54). Output, capacity and counters as wq_route_tick. The host-array
+ * form rejects WQ_WORLD_INVALID (WQ_E_INVALID); the device form routes it to nobody. The "@global"
  * broadcast to every connected peer (global_message.rs:18-35) is a peer-map operation and has no
  * table entry point. */
 int wq_route_global(wq_router* h, const uint32_t* world, const uint32_t* sender, const uint8_t* repl,
@@ -240,6 +243,14 @@ int wq_peer_major_device(wq_router* h, const uint32_t* d_offsets, const uint32_t
                          size_t n_pairs, const uint32_t* d_connected, uint32_t n_peers,
                          uint32_t* d_peer_offsets, uint32_t* d_msgs_out);
 
+/* ---- health of asynchronous ticks ----
+ * OR of wq_route_counters.error (error_bits) and of .overflow over every route / global call since
+ * the previous wq_route_health on this handle; reading clears them (synchronises the stream). A
+ * normal tick never writes them, so a caller that runs many _device ticks without reading their
+ * counters checks the whole run here: error bit 4 = a bounded spin gave up (WQ_E_TIMEOUT), 2 =
+ * more than 2^32-1 pairs in one tick; overflow = some tick's pairs exceeded its capacity. */
+int wq_route_health(wq_router* h, uint32_t* error_bits, uint32_t* overflow);
+
 /* ---- instrumentation ----
  * When enabled, every route launch is bracketed by HIP events on the launch stream;
  * wq_profile_read returns the summed kernel-only milliseconds and launch count (and resets). */
@@ -260,6 +271,9 @@ int wq_debug_update_counts(wq_router* h, uint64_t* incremental, uint64_t* rebuil
 /* ---- tuning hook: select a compiled route-kernel shape (messages per thread, expansion chunk);
  * 0 is the default. Results are identical for every shape. */
 int wq_debug_set_route_config(wq_router* h, int cfg);
+/* The tick shape the next default-config tick takes (heavy_fanout = count / scan / emit) and
+ * whether it is still chosen automatically (no hint set, or reset by a negative hint). */
+int wq_debug_route_shape(wq_router* h, int* heavy_fanout, int* fanout_auto);
 /* Number of route kernel configurations (valid cfg values are 0 .. n-1). */
 int wq_debug_route_config_count(void);
 /* Diagnostics: when d_stamps is non-null, the single-launch tick writes four s_memrealtime stamps

@@ -128,6 +128,13 @@ def load_c_oracle():
     lib.wqo_route_radius.restype = sz
     lib.wqo_route_global.argtypes = [vp, vp, vp, vp, sz, vp, vp, sz]
     lib.wqo_route_global.restype = sz
+    lib.wqo_set_fast.argtypes = [vp, i32]
+    lib.wqo_set_fast.restype = i32
+    lib.wqo_route_check.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, sz, ctypes.c_double, vp, vp,
+                                    ctypes.POINTER(sz)]
+    lib.wqo_route_check.restype = sz
+    lib.wqo_route_faithful.argtypes = [vp] * 5 + [sz, vp, sz, vp, vp, sz]
+    lib.wqo_route_faithful.restype = sz
     _lib = lib
     return lib
 
@@ -222,6 +229,47 @@ class COracle:
         sort_within_segments(offsets, peers)
         return offsets, peers, F.value
 
+
+    def set_fast(self, on: bool = True) -> None:
+        """Checker mode for full-size churn (wqo_set_fast): same results, no O(#cubes) scan per
+        unsubscribe. Only on an empty map; never for the timed CPU baseline."""
+        if self.lib.wqo_set_fast(self.h, int(on)) != 0:
+            raise ValueError("wqo_set_fast needs an empty map")
+
+    def route_check(self, pos, world, sender, repl, got_offsets, got_peers, keys=None, peer_pos=None,
+                    radius: float = 0.0):
+        """(number of messages whose recipients differ from got_offsets / got_peers, first such
+        message or M) — wqo_route_check, for ticks too large to sort in numpy."""
+        world = np.ascontiguousarray(world, dtype=np.uint32)
+        M = len(world)
+        sender = np.ascontiguousarray(sender, dtype=np.uint32)
+        repl = np.ascontiguousarray(repl, dtype=np.uint8)
+        pos_a = None if pos is None else np.ascontiguousarray(pos, dtype=np.float64).reshape(-1, 3)
+        keys_a = None if keys is None else np.ascontiguousarray(keys, dtype=np.int64).reshape(-1, 3)
+        pp = None if peer_pos is None else np.ascontiguousarray(peer_pos, dtype=np.float64).reshape(-1, 3)
+        go = np.ascontiguousarray(got_offsets, dtype=np.uint32)
+        gp = np.ascontiguousarray(got_peers, dtype=np.uint32)
+        assert len(go) == M + 1
+        first = ctypes.c_size_t()
+        bad = self.lib.wqo_route_check(self.h, _ptr(pos_a), _ptr(keys_a), _ptr(world), _ptr(sender), _ptr(repl), M,
+                                       _ptr(pp), 0 if pp is None else len(pp), float(radius), _ptr(go), _ptr(gp),
+                                       ctypes.byref(first))
+        return int(bad), int(first.value)
+
+    def route_faithful(self, pos, world, sender, repl, connected):
+        """cpu_server_faithful_1t (wqo_route_faithful): handle_local_message + PeerMap::broadcast_to
+        (peer_map.rs:151-163) with the PeerMap iterating `connected` in order. Returns
+        (offsets[M+1], peers in connected order per message)."""
+        world = np.ascontiguousarray(world, dtype=np.uint32)
+        M = len(world)
+        args = (self.h, _ptr(np.ascontiguousarray(pos, dtype=np.float64).reshape(-1, 3)), _ptr(world),
+                _ptr(np.ascontiguousarray(sender, dtype=np.uint32)), _ptr(np.ascontiguousarray(repl, dtype=np.uint8)), M)
+        conn = np.ascontiguousarray(connected, dtype=np.uint32)
+        offsets = np.zeros(M + 1, dtype=np.uint32)
+        P = self.lib.wqo_route_faithful(*args, _ptr(conn), len(conn), _ptr(offsets), None, 0)
+        peers = np.zeros(max(P, 1), dtype=np.uint32)
+        self.lib.wqo_route_faithful(*args, _ptr(conn), len(conn), _ptr(offsets), _ptr(peers), P)
+        return offsets, peers[:P]
 
     def route_radius(self, pos, world, sender, repl, peer_pos, radius: float):
         """C5: route() intersected with the exact radius predicate (wq_oracle.c wqo_route_radius)."""

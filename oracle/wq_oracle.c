@@ -249,10 +249,55 @@ static void cm_remove(cube_map* m, cube_slot* c) {
     m->n_full--;
 }
 
-/* AreaMap, worldql_server/src/subscriptions/area_map.rs:10-17 */
+/* u32 -> u32 counter map (fast mode, below): open addressing, no deletion (a zero count stays) */
+typedef struct {
+    uint32_t* key;
+    uint32_t* val;
+    uint8_t* st;
+    size_t cap, n;
+} u32_count;
+
+static void uc_init(u32_count* c) {
+    c->cap = 16;
+    c->key = (uint32_t*)calloc(c->cap, sizeof(uint32_t));
+    c->val = (uint32_t*)calloc(c->cap, sizeof(uint32_t));
+    c->st = (uint8_t*)calloc(c->cap, 1);
+    c->n = 0;
+}
+static void uc_free(u32_count* c) {
+    free(c->key);
+    free(c->val);
+    free(c->st);
+}
+static uint32_t* uc_slot(u32_count* c, uint32_t k) {
+    if ((c->n + 1) * 2 > c->cap) {
+        u32_count old = *c;
+        c->cap *= 2;
+        c->key = (uint32_t*)calloc(c->cap, sizeof(uint32_t));
+        c->val = (uint32_t*)calloc(c->cap, sizeof(uint32_t));
+        c->st = (uint8_t*)calloc(c->cap, 1);
+        c->n = 0;
+        for (size_t i = 0; i < old.cap; ++i)
+            if (old.st[i]) *uc_slot(c, old.key[i]) = old.val[i];
+        uc_free(&old);
+    }
+    size_t m = c->cap - 1, i = mix64(k) & m;
+    while (c->st[i] && c->key[i] != k) i = (i + 1) & m;
+    if (!c->st[i]) {
+        c->st[i] = 1;
+        c->key[i] = k;
+        c->val[i] = 0;
+        c->n++;
+    }
+    return &c->val[i];
+}
+
+/* AreaMap, worldql_server/src/subscriptions/area_map.rs:10-17. `cubes_of` is only kept in fast
+ * mode (wqo_set_fast): the number of cubes of this world holding each peer. */
 typedef struct {
     cube_map map;
     u32_set subscribed_peers;
+    u32_count cubes_of;
 } area_map;
 
 /* WorldMap, world_map.rs:10-13 (world names are interned to u32 ids on the host) */
@@ -263,9 +308,16 @@ typedef struct {
 
 struct wqo_world_map {
     uint16_t cube_size;
+    int fast; /* wqo_set_fast */
     world_slot* w;
     size_t cap, n;
 };
+
+int wqo_set_fast(wqo_world_map* wm, int fast) {
+    if (wm->n) return -1; /* only on an empty map: the per-peer cube counts start at zero */
+    wm->fast = fast != 0;
+    return 0;
+}
 
 wqo_world_map* wqo_create(uint16_t cube_size) {
     wqo_world_map* wm = (wqo_world_map*)calloc(1, sizeof(*wm));
@@ -281,6 +333,7 @@ void wqo_destroy(wqo_world_map* wm) {
         if (wm->w[i].am) {
             cm_free(&wm->w[i].am->map);
             us_free(&wm->w[i].am->subscribed_peers);
+            uc_free(&wm->w[i].am->cubes_of);
             free(wm->w[i].am);
         }
     free(wm->w);
@@ -318,6 +371,7 @@ static area_map* wm_get_mut(wqo_world_map* wm, uint32_t world) {
     am = (area_map*)calloc(1, sizeof(area_map));
     cm_init(&am->map);
     us_init(&am->subscribed_peers);
+    uc_init(&am->cubes_of);
     wm_put(wm, world, am);
     wm->n++;
     return am;
@@ -336,21 +390,33 @@ static void to_cube_area(int key_is_raw, const void* key_or_pos, uint16_t size, 
 }
 
 /* area_map.rs:72-85 */
-static int am_add(area_map* am, uint32_t peer, const int64_t k[3]) {
+static int am_add(area_map* am, uint32_t peer, const int64_t k[3], int fast) {
     cube_slot* c = cm_insert(&am->map, k);
     us_insert(&am->subscribed_peers, peer);
-    return ps_insert(&c->set, peer);
+    const int added = ps_insert(&c->set, peer);
+    if (fast && added) ++*uc_slot(&am->cubes_of, peer);
+    return added;
 }
 
-/* area_map.rs:88-119, including the O(#cubes) scan at :113 */
-static int am_remove(area_map* am, uint32_t peer, const int64_t k[3]) {
+/* area_map.rs:88-119, including the O(#cubes) scan at :113. Fast mode answers the scan's question
+ * ("does any other cube still hold the peer?") from the per-peer cube count instead: the same
+ * answer, because a peer is in subscribed_peers exactly when some cube set holds it (add inserts
+ * into both, remove_peer removes from both, and this function keeps it) — for the test checker
+ * only, never for the timed CPU baseline, which keeps the reference's scan. */
+static int am_remove(area_map* am, uint32_t peer, const int64_t k[3], int fast) {
     cube_slot* c = cm_find(&am->map, k);
     if (!c) return 0; /* :92-94 */
     int removed = ps_remove(&c->set, peer);
     if (c->set.n == 0) cm_remove(&am->map, c); /* :108-110 */
     int has_other = 0;
-    for (size_t i = 0; i < am->map.cap && !has_other; ++i)
-        if (am->map.s[i].st == SLOT_FULL && ps_find(&am->map.s[i].set, peer) >= 0) has_other = 1;
+    if (fast) {
+        uint32_t* n = uc_slot(&am->cubes_of, peer);
+        if (removed) --*n;
+        has_other = *n > 0;
+    } else {
+        for (size_t i = 0; i < am->map.cap && !has_other; ++i)
+            if (am->map.s[i].st == SLOT_FULL && ps_find(&am->map.s[i].set, peer) >= 0) has_other = 1;
+    }
     if (!has_other) us_remove(&am->subscribed_peers, peer);
     return removed;
 }
@@ -358,6 +424,7 @@ static int am_remove(area_map* am, uint32_t peer, const int64_t k[3]) {
 /* area_map.rs:124-135: empty sets are kept */
 static int am_remove_peer(area_map* am, uint32_t peer) {
     us_remove(&am->subscribed_peers, peer);
+    if (am->cubes_of.n) *uc_slot(&am->cubes_of, peer) = 0;
     int removed = 0;
     for (size_t i = 0; i < am->map.cap; ++i)
         if (am->map.s[i].st == SLOT_FULL && ps_remove(&am->map.s[i].set, peer)) removed = 1;
@@ -368,14 +435,14 @@ int wqo_add_subscription(wqo_world_map* wm, uint32_t world, uint32_t peer, int k
                          const void* key_or_pos) {
     int64_t k[3];
     to_cube_area(key_is_raw, key_or_pos, wm->cube_size, k);
-    return am_add(wm_get_mut(wm, world), peer, k);
+    return am_add(wm_get_mut(wm, world), peer, k, wm->fast);
 }
 
 int wqo_remove_subscription(wqo_world_map* wm, uint32_t world, uint32_t peer, int key_is_raw,
                             const void* key_or_pos) {
     int64_t k[3];
     to_cube_area(key_is_raw, key_or_pos, wm->cube_size, k);
-    return am_remove(wm_get_mut(wm, world), peer, k); /* get_mut creates (area_unsubscribe.rs:189) */
+    return am_remove(wm_get_mut(wm, world), peer, k, wm->fast); /* get_mut creates (area_unsubscribe.rs:189) */
 }
 
 /* world_map.rs:41-61 */
@@ -606,4 +673,45 @@ void wqo_counts(const wqo_world_map* wm, uint64_t* n_entries, uint64_t* n_cubes)
     }
     *n_entries = e;
     *n_cubes = c;
+}
+
+/* Checker for large ticks: routes every message like wqo_route (or wqo_route_radius when
+ * peer_pos != NULL), sorts its recipients ascending and compares them with the message's slice of
+ * a candidate CSR (got_offsets[M+1], got_peers[], ascending per message, as the GPU path writes
+ * it). Returns the number of messages that differ; *first_bad (nullable) gets the first one, or M. */
+static int cmp_u32(const void* a, const void* b) {
+    const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+    return (x > y) - (x < y);
+}
+
+size_t wqo_route_check(const wqo_world_map* wm, const double* pos, const int64_t* keys, const uint32_t* world,
+                       const uint32_t* sender, const uint8_t* repl, size_t M, const double* peer_pos, size_t n_pos,
+                       double radius, const uint32_t* got_offsets, const uint32_t* got_peers, size_t* first_bad) {
+    size_t bad = 0, first = M, cap = 1024;
+    uint32_t* buf = (uint32_t*)malloc(cap * sizeof(uint32_t));
+    uint32_t off[2];
+    for (size_t m = 0; m < M; ++m) {
+        const double* pm = pos ? pos + 3 * m : NULL;
+        const int64_t* km = keys ? keys + 3 * m : NULL;
+        size_t n = peer_pos ? wqo_route_radius(wm, pm, world + m, sender + m, repl + m, 1, peer_pos, n_pos, radius,
+                                               off, buf, cap, NULL)
+                            : wqo_route(wm, pm, km, world + m, sender + m, repl + m, 1, off, buf, cap, NULL);
+        if (n > cap) {
+            while (cap < n) cap *= 2;
+            buf = (uint32_t*)realloc(buf, cap * sizeof(uint32_t));
+            n = peer_pos ? wqo_route_radius(wm, pm, world + m, sender + m, repl + m, 1, peer_pos, n_pos, radius, off,
+                                            buf, cap, NULL)
+                         : wqo_route(wm, pm, km, world + m, sender + m, repl + m, 1, off, buf, cap, NULL);
+        }
+        qsort(buf, n, sizeof(uint32_t), cmp_u32);
+        const size_t g0 = got_offsets[m], g1 = got_offsets[m + 1];
+        int same = g1 >= g0 && g1 - g0 == n && (n == 0 || memcmp(buf, got_peers + g0, n * sizeof(uint32_t)) == 0);
+        if (!same) {
+            if (first == M) first = m;
+            bad++;
+        }
+    }
+    free(buf);
+    if (first_bad) *first_bad = first;
+    return bad;
 }

@@ -77,6 +77,17 @@ size_t wqo_route_radius(const wqo_world_map* wm, const double* pos, const uint32
 size_t wqo_route_global(const wqo_world_map* wm, const uint32_t* world, const uint32_t* sender, const uint8_t* repl,
                         size_t M, uint32_t* offsets, uint32_t* peers, size_t cap);
 
+/* Fast mode for the test checker (call on an empty map): remove_subscription answers its
+ * O(#cubes) "any other cube?" scan (area_map.rs:113-116) from per-peer cube counts — the same
+ * result (see wq_oracle.c), so full-size churn configs can be checked. Returns -1 if not empty.
+ * The timed CPU baseline never sets it. */
+int wqo_set_fast(wqo_world_map* wm, int fast);
+/* Routes each message (wqo_route, or wqo_route_radius when peer_pos != NULL), sorts its recipients
+ * and compares them with got_offsets / got_peers (ascending per message). Returns the number of
+ * differing messages; *first_bad gets the first (or M). */
+size_t wqo_route_check(const wqo_world_map* wm, const double* pos, const int64_t* keys, const uint32_t* world,
+                       const uint32_t* sender, const uint8_t* repl, size_t M, const double* peer_pos, size_t n_pos,
+                       double radius, const uint32_t* got_offsets, const uint32_t* got_peers, size_t* first_bad);
 /* Stats for tests: number of live (world,cube,peer) entries and of non-empty cubes. */
 void wqo_counts(const wqo_world_map* wm, uint64_t* n_entries, uint64_t* n_cubes);
 

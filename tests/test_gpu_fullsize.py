@@ -1,0 +1,259 @@
+"""GPU parity at the FULL sizes of SURVEY.md §8(d) — C3 (10M messages, 27M subscriptions), C4 (8
+worlds x 50k peers, churn ticks through the device-op path the bench times) and C5 (1M entities,
+6.4M churn ops, radius filter) — against the C restatement (oracle/wq_oracle.c).
+
+Bar: bit-exact per message. The oracle routes each message, sorts its recipients and compares them
+with the GPU's CSR slice (wqo_route_check), so a 4.2e8-pair tick needs no host sort. Churn configs
+use the oracle's checker mode (wqo_set_fast: the same sets without remove_subscription's O(#cubes)
+scan, pinned against the faithful scan in tests/test_oracle.py).
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from worldql_server_amd import abi, synth, synth_ext
+
+pytestmark = pytest.mark.gpu
+
+
+def _router():
+    from worldql_server_amd.router import Router
+    return Router(16, 0)
+
+
+def _ops_dev(ops, dev):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(ops).view(np.uint8).copy()).to(dev)
+
+
+def test_c3_full_tick_exact_vs_oracle():
+    """The whole C3 tick (1M peers x 27 cubes, 10M hotspot messages, P = 4.17e8) in both tick shapes:
+    count / scan / emit (the bench's shape, fan-out hint ~42) and the single launch (whose blocks
+    overflow the LDS image and emit directly); the second pass with mixed replication codes."""
+    w = synth_ext.config_c3()
+    M = len(w.world)
+    r = _router()
+    r.apply_ops(w.ops)
+    o = orc.COracle(16)
+    o.apply_ops(w.ops)
+    assert r.stats()["n_entries"] == o.counts()[0] == 27_000_000
+
+    r.set_fanout_hint(42.0)
+    assert r.route_shape() == (True, False)
+    offs, peers, _ = r.route(w.pos, w.world, w.sender, w.repl)
+    assert int(offs[M]) == len(peers) > 4e8
+    bad, first = o.route_check(w.pos, w.world, w.sender, w.repl, offs, peers)
+    assert bad == 0, f"{bad} messages differ, first {first}"
+    del peers
+
+    repl = synth.stream(3, 77).below(4, M).astype(np.uint8)  # 3 = unknown code: ExceptSelf
+    r.set_fanout_hint(0.0)
+    assert r.route_shape() == (False, False)
+    offs2, peers2, _ = r.route(w.pos, w.world, w.sender, repl)
+    bad, first = o.route_check(w.pos, w.world, w.sender, repl, offs2, peers2)
+    assert bad == 0, f"{bad} messages differ, first {first}"
+    assert r.route_health()[0] == 0  # no error bits (the overflow word holds route()'s capacity retries)
+
+
+def test_c4_full_churn_ticks_exact_vs_oracle():
+    """8 worlds x 50k peers (one GPU's share of C4, 10.8M subscriptions), three churn ticks of ~630k
+    unsubscribe / subscribe ops applied through wq_apply_ops_device, then 400k messages each."""
+    import torch
+    dev = torch.device("cuda:0")
+    c4 = synth_ext.config_c4(worlds=range(8))
+    init = c4.initial_ops()
+    r = _router()
+    r.apply_ops(init)
+    o = orc.COracle(16)
+    o.set_fast(True)
+    o.apply_ops(init)
+    for tick in range(3):
+        ops, pos, wo, se, rp = c4.step()
+        assert len(ops) > 500_000
+        d = _ops_dev(ops, dev)
+        torch.cuda.synchronize()
+        r.apply_ops_device(d.data_ptr(), len(ops))
+        o.apply_ops(ops)
+        if tick == 1:
+            rp = synth.stream(4, 500).below(3, len(wo)).astype(np.uint8)
+        offs, peers, _ = r.route(pos, wo, se, rp)
+        assert len(peers) > 1e7
+        bad, first = o.route_check(pos, wo, se, rp, offs, peers)
+        assert bad == 0, f"tick {tick}: {bad} messages differ, first {first}"
+        assert r.stats()["n_entries"] == o.counts()[0]
+    inc, fb = r.update_counts()
+    assert inc >= 3 and fb == 0  # the ticks took the incremental path, as in the bench
+    for wid in (0, 3, 7):
+        assert (r.world_peers(wid) == o.world_peers(wid)).all()
+
+
+def test_c5_full_tick_radius_exact_vs_oracle():
+    """1M moving entities: the 27M-subscription table, one move's ~6.4M churn ops through
+    wq_apply_ops_device, new positions, then 1M messages with the r = 16 radius filter."""
+    import torch
+    dev = torch.device("cuda:0")
+    c5 = synth_ext.config_c5()
+    init = c5.initial_ops()
+    r = _router()
+    r.apply_ops(init)
+    o = orc.COracle(16)
+    o.set_fast(True)
+    o.apply_ops(init)
+    r.set_radius(c5.radius)
+    ops = c5.step()
+    assert len(ops) > 5_000_000
+    d = _ops_dev(ops, dev)
+    pp = torch.from_numpy(c5.pos).to(dev)
+    torch.cuda.synchronize()
+    r.apply_ops_device(d.data_ptr(), len(ops))
+    r.set_peer_positions_device(pp.data_ptr(), c5.n)
+    o.apply_ops(ops)
+    pos, wo, se, rp = c5.messages()
+    offs, peers, _ = r.route(pos, wo, se, rp)
+    assert 1e6 < len(peers) < 5e6
+    bad, first = o.route_check(pos, wo, se, rp, offs, peers, peer_pos=c5.pos, radius=c5.radius)
+    assert bad == 0, f"{bad} messages differ, first {first}"
+    assert r.stats()["n_entries"] == o.counts()[0]
+
+
+def test_large_worlds_and_minecraft_scale_coordinates():
+    """World ids >= 1023 (up to 2^32 - 2) and coordinates out to +-3e7 (cube_area.rs:23-44 takes
+    any f64; world_map.rs:31-36 creates worlds without bound), mixed with small keys, raw keys at
+    the i64 limits and the 2^17-cube boundary of the packed record key."""
+    rng = np.random.default_rng(5)
+    worlds = np.array([0, 1022, 1023, 4096, 0x7FFFFFFF, 0xFFFFFFFE], np.uint32)
+    n_peers = 3000
+    peer_w = worlds[rng.integers(0, len(worlds), n_peers)]
+    scale = np.where(rng.random(n_peers) < 0.5, 3e7, 64.0)
+    ppos = rng.uniform(-1, 1, (n_peers, 3)) * scale[:, None]
+    edge = 131072.0 * 16.0  # 2^17 cubes of 16
+    ppos[:200] = rng.choice([edge - 8, edge + 8, -edge - 8, -edge + 8, edge, -edge], (200, 3))
+    ops = synth_ext._neighbourhood_ops(peer_w, ppos, 16)
+    raw = abi.ops_array(np.full(4, 4096, np.uint32), np.arange(4), np.zeros(4, np.uint8),
+                        key=[[2**63 - 1, 0, 16], [-2**63, -2**63, -2**63], [edge, edge, edge], [5, 6, 7]])
+    ops = abi.concat_ops([ops, raw])
+    r, o = _router(), orc.COracle(16)
+    r.apply_ops(ops)
+    o.apply_ops(ops)
+    assert r.stats()["n_entries"] == o.counts()[0]
+    M = 60_000
+    src = rng.integers(0, n_peers, M)
+    mpos = ppos[src] + rng.uniform(-20, 20, (M, 3))
+    mw = peer_w[src]
+    mw[::97] = 77  # a world nobody subscribed in
+    se = rng.integers(0, n_peers, M).astype(np.uint32)
+    se[::3] = src[::3]  # the sender often is a subscriber of the cube
+    rp = rng.integers(0, 4, M).astype(np.uint8)
+    offs, peers, _ = r.route(mpos, mw, se, rp)
+    bad, first = o.route_check(mpos, mw, se, rp, offs, peers)
+    assert bad == 0, f"{bad} messages differ, first {first}"
+    assert len(peers) > M  # real fan-out on the large-key cubes, not an empty tick
+    keys = np.array([[2**63 - 1, 0, 16], [-2**63, -2**63, -2**63], [edge, edge, edge], [5, 6, 7]], np.int64)
+    kw = np.full(4, 4096, np.uint32)
+    offs, peers, _ = r.route(None, kw, np.full(4, 9, np.uint32), np.ones(4, np.uint8), keys=keys)
+    bad, _ = o.route_check(None, kw, np.full(4, 9, np.uint32), np.ones(4, np.uint8), offs, peers, keys=keys)
+    assert bad == 0 and len(peers) >= 4
+
+
+def test_peer_major_vs_broadcast_to_restatement():
+    """F2 against the oracle's PeerMap::broadcast_to restatement (wqo_route_faithful,
+    peer_map.rs:151-163: recipients re-collected, then every connected peer of the map filtered
+    against them) — not against the GPU's own CSR: for each connected peer, the messages it is sent."""
+    import torch
+    from worldql_server_amd.router import Router
+    w = synth.config_c2(repl_mode="mixed", scale=0.02)
+    M = len(w.world)
+    r = Router(16, 0)
+    r.apply_ops(w.ops)
+    o = orc.COracle(16)
+    o.apply_ops(w.ops)
+    rng = np.random.default_rng(8)
+    n_peers = w.n_peers
+    conn_ids = np.flatnonzero(rng.random(n_peers) < 0.7).astype(np.uint32)
+    rng.shuffle(conn_ids)  # the PeerMap's own iteration order
+    f_offs, f_peers = o.route_faithful(w.pos, w.world, w.sender, w.repl, conn_ids)
+    # the faithful sends, transposed: per connected peer, its messages ascending
+    f_msg = np.repeat(np.arange(M, dtype=np.uint32), np.diff(f_offs.astype(np.int64)))
+    order = np.lexsort((f_msg, f_peers))
+    want_po = np.searchsorted(f_peers[order], np.arange(n_peers + 1), side="left").astype(np.uint32)
+    want_m = f_msg[order]
+
+    offs, peers, _ = r.route(w.pos, w.world, w.sender, w.repl)
+    bits = np.zeros(((n_peers + 31) // 32) * 32, bool)
+    bits[conn_ids] = True
+    connected = np.packbits(bits, bitorder="little").view(np.uint32)
+    dev = torch.device("cuda:0")
+    r.set_stream(torch.cuda.current_stream().cuda_stream)
+    t_off = torch.from_numpy(offs.view(np.int32)).to(dev)
+    t_peers = torch.from_numpy(peers.view(np.int32)).to(dev)
+    t_conn = torch.from_numpy(connected.view(np.int32)).to(dev)
+    po = torch.empty(n_peers + 1, dtype=torch.int32, device=dev)
+    mo = torch.empty(max(len(peers), 1), dtype=torch.int32, device=dev)
+    r.peer_major_device(t_off.data_ptr(), t_peers.data_ptr(), M, len(peers), t_conn.data_ptr(), n_peers,
+                        po.data_ptr(), mo.data_ptr())
+    torch.cuda.synchronize()
+    got_po = po.cpu().numpy().view(np.uint32)
+    assert (got_po == want_po).all()
+    assert got_po[-1] == len(f_peers) > 0
+    assert (mo.cpu().numpy().view(np.uint32)[:got_po[-1]] == want_m).all()
+    r.set_stream(None)
+
+
+def test_global_message_to_reserved_world():
+    """the device form routes world 0xFFFFFFFF to nobody (no wrapped range, no read past
+    the any-keys); the host form rejects it."""
+    import torch
+    from worldql_server_amd.router import WQError
+    r = _router()
+    ops = abi.ops_array(np.array([0, 0, 5, 0xFFFFFFFE], np.uint32), [1, 2, 3, 4], [0, 0, 0, 0],
+                        pos=np.ones((4, 3)))
+    r.apply_ops(ops)
+    dev = torch.device("cuda:0")
+    r.set_stream(torch.cuda.current_stream().cuda_stream)
+    wo = torch.from_numpy(np.array([0xFFFFFFFF, 0, 0xFFFFFFFE, 0xFFFFFFFF], np.uint32).view(np.int32)).to(dev)
+    se = torch.zeros(4, dtype=torch.int32, device=dev)
+    rp = torch.ones(4, dtype=torch.uint8, device=dev)
+    offs = torch.empty(5, dtype=torch.int32, device=dev)
+    peers = torch.full((64,), -1, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+    r.route_global_device(wo.data_ptr(), se.data_ptr(), rp.data_ptr(), 4, offs.data_ptr(), peers.data_ptr(), None,
+                          64, cnt.data_ptr())
+    torch.cuda.synchronize()
+    assert offs.cpu().numpy().tolist() == [0, 0, 2, 3, 3]
+    assert sorted(peers.cpu().numpy()[:3].tolist()) == [1, 2, 4]
+    c = cnt.cpu().numpy().view(abi.COUNTERS_DTYPE)[0]
+    assert c["n_pairs"] == 3 and c["error"] == 0 and c["overflow"] == 0
+    r.set_stream(None)
+    with pytest.raises(WQError) as e:
+        r.route_global(np.array([0xFFFFFFFF], np.uint32), np.zeros(1, np.uint32), np.ones(1, np.uint8))
+    assert e.value.code == abi.WQ_E_INVALID
+
+
+def test_route_health_reports_overflow_of_async_ticks():
+    """wq_route_health: a run of _device ticks is checked afterwards without reading any counters —
+    clean ticks leave it (0, 0); one tick with too small a capacity sets the overflow word."""
+    import torch
+    w = synth.config_c2(scale=0.01)
+    r = _router()
+    r.apply_ops(w.ops)
+    dev = torch.device("cuda:0")
+    r.set_stream(torch.cuda.current_stream().cuda_stream)
+    M = len(w.world)
+    pos = torch.from_numpy(w.pos).to(dev)
+    wo = torch.from_numpy(w.world.view(np.int32)).to(dev)
+    se = torch.from_numpy(w.sender.view(np.int32)).to(dev)
+    rp = torch.from_numpy(w.repl).to(dev)
+    offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    peers = torch.empty(40 * M, dtype=torch.int32, device=dev)
+    r.route_health()
+    for cap in (40 * M, 40 * M, 40 * M):
+        r.route_device(pos.data_ptr(), wo.data_ptr(), se.data_ptr(), rp.data_ptr(), M, offs.data_ptr(),
+                       peers.data_ptr(), None, cap)
+    assert r.route_health() == (0, 0)
+    r.route_device(pos.data_ptr(), wo.data_ptr(), se.data_ptr(), rp.data_ptr(), M, offs.data_ptr(),
+                   peers.data_ptr(), None, 100)
+    r.route_device(pos.data_ptr(), wo.data_ptr(), se.data_ptr(), rp.data_ptr(), M, offs.data_ptr(),
+                   peers.data_ptr(), None, 40 * M)
+    assert r.route_health() == (0, 1)
+    assert r.route_health() == (0, 0)  # reading clears
+    r.set_stream(None)

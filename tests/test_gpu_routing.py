@@ -385,8 +385,24 @@ def test_auto_fanout_shape_from_host_ticks():
     r.apply_ops(ops)
     o.apply_ops(ops)
     rng = synth.SplitMix64(91)
+    assert r.route_shape() == (False, True)  # a fresh handle: single launch, automatic
     for M in (9000, 9000, 300):
         mpos = np.stack([rng.below(n_cubes, M) * 16.0 + rng.uniform(0.5, 15.5, M), rng.uniform(0.5, 15.5, M),
                          rng.uniform(0.5, 15.5, M)], 1)
         _compare(r, o, mpos, np.zeros(M, np.uint32), rng.below(n_cubes * per_cube, M),
                  rng.below(3, M).astype(np.uint8))
+        assert r.route_shape() == (True, True)  # ~40 pairs per message: count / scan / emit next
+    # a one-message query (AreaMap::get_subscribed_peers) must not pick the shape of real ticks
+    r.route(np.array([[8.0, 8.0, 8.0]]), np.zeros(1, np.uint32), np.zeros(1, np.uint32),
+            np.ones(1, np.uint8))
+    assert r.route_shape() == (True, True)
+    r.route(np.full((400, 3), -5000.0), np.zeros(400, np.uint32), np.zeros(400, np.uint32),
+            np.zeros(400, np.uint8))  # an empty tick of >= one block: back to the single launch
+    assert r.route_shape() == (False, True)
+    r.set_fanout_hint(100.0)
+    assert r.route_shape() == (True, False)
+    r.route(np.full((400, 3), -5000.0), np.zeros(400, np.uint32), np.zeros(400, np.uint32),
+            np.zeros(400, np.uint8))
+    assert r.route_shape() == (True, False)  # the caller's hint holds
+    r.set_fanout_hint(-1.0)
+    assert r.route_shape()[1] is True  # a negative hint hands the choice back

@@ -166,6 +166,11 @@ class OracleBackedRouter:
         offs, peers, _ = self.o.route(pos, world, sender, repl, keys=keys)
         return offs, peers, None
 
+    def route_global(self, world, sender, repl, with_msgs=False):
+        self.calls.append(("global", len(world)))
+        offs, peers = self.o.route_global(world, sender, repl)
+        return offs, peers, None
+
     def is_subscribed(self, world, peer, raw, k):
         k = np.asarray(k).reshape(-1, 3)
         return np.array([self.o.is_subscribed(int(w), int(p), raw, kk) for w, p, kk in zip(world, peer, k)])
@@ -197,7 +202,7 @@ def test_tick_batching_preserves_sequential_order():
         Message(LOCAL_MESSAGE, "c", "@global", v),          # dropped
         Message(LOCAL_MESSAGE, "c", "world", None),         # dropped (no position)
         Message(LOCAL_MESSAGE, "c", "0bad", v),             # dropped (InvalidStart)
-        Message(LOCAL_MESSAGE, "c", "nowhere", v),          # no such world -> []
+        Message(LOCAL_MESSAGE, "c", "nowhere", v),          # no such world -> nothing broadcast
         Message(DISCONNECT, "c"),
         Message(LOCAL_MESSAGE, "b", "world", v, abi.REPL_INCLUDING_SELF),  # -> []
         Message(LOCAL_MESSAGE, "x", "world_one", v),        # -> [b]
@@ -208,10 +213,58 @@ def test_tick_batching_preserves_sequential_order():
     assert sorted(res[5]) == ["a", "c"]
     assert res[7] == ["c"]
     assert res[8] is None and res[9] is None and res[10] is None
-    assert res[11] == []
+    assert res[11] is None
     assert res[13] == [] and res[14] == ["b"]
     kinds = [c[0] for c in r.calls]
     assert kinds == ["ops", "route", "ops", "route", "ops", "route", "ops", "route"]
+
+
+def test_global_messages_and_peer_id_recycling():
+    """GlobalMessage runs interleave with LocalMessages in one read run (thread.rs:134); a
+    disconnected peer's id is recycled for the next new peer (peer_map.rs:121-141)."""
+    from worldql_server_amd.processing import (AREA_SUBSCRIBE, DISCONNECT, GLOBAL_MESSAGE, LOCAL_MESSAGE, Message,
+                                               PeerMapBroadcast, SubscriptionProcessor)
+    from worldql_server_amd.subscriptions import Vector3, WorldMap
+    r = OracleBackedRouter(16)
+    wm = WorldMap(16, router=r)
+    seen = []
+    proc = SubscriptionProcessor(wm, broadcast=lambda ev, rec: seen.append((ev.sender_uuid, rec)))
+    v, far = Vector3(1.0, 2.0, 3.0), Vector3(500.0, 2.0, 3.0)
+    res = proc.process_tick([
+        Message(AREA_SUBSCRIBE, "a", "world", v),
+        Message(AREA_SUBSCRIBE, "b", "world", far),
+        Message(GLOBAL_MESSAGE, "a", "world"),                          # -> [b]
+        Message(LOCAL_MESSAGE, "b", "world", v),                        # -> [a]
+        Message(GLOBAL_MESSAGE, "a", "world", None, abi.REPL_ONLY_SELF),  # -> [a]
+        Message(GLOBAL_MESSAGE, "z", "@global", None, 7),               # PeerMap broadcast, ExceptSelf
+        Message(GLOBAL_MESSAGE, "a", "nowhere"),                        # no such world: nothing
+        Message(GLOBAL_MESSAGE, "a", "0bad"),                           # invalid name: dropped
+        Message(DISCONNECT, "a"),
+        Message(GLOBAL_MESSAGE, "b", "world", None, abi.REPL_INCLUDING_SELF),  # -> [b]
+        Message(AREA_SUBSCRIBE, "c", "world", v),                        # takes a's recycled id
+        Message(LOCAL_MESSAGE, "b", "world", v),                        # -> [c]
+    ])
+    assert res[2] == ["b"] and res[3] == ["a"] and res[4] == ["a"]
+    assert res[5] == PeerMapBroadcast(abi.REPL_EXCEPT_SELF, "z")
+    assert res[6] is None and res[7] is None
+    assert res[9] == ["b"] and res[11] == ["c"]
+    assert [s[0] for s in seen] == ["a", "b", "a", "z", "b", "b"]  # arrival order
+    assert wm.peer_ids.high_water == 2 and len(wm.peer_ids) == 2
+    kinds = [c[0] for c in r.calls]
+    assert kinds == ["ops", "route", "global", "ops", "global", "ops", "route"]
+
+
+def test_random_interleaving_vs_sequential_reference():
+    """Flush-on-reorder over 2,000 random events (sub / unsub / disconnect / Local / Global, bad
+    names, missing positions, unknown replication codes) in ticks of 1..97 events, against the
+    reference loop applied one event at a time (tests/seq_reference.py). CPU backend; the GPU
+    version is tests/test_gpu_processing.py."""
+    from tests.seq_reference import check_ticks, random_events
+    from worldql_server_amd.processing import SubscriptionProcessor
+    from worldql_server_amd.subscriptions import WorldMap
+    wm = WorldMap(16, router=OracleBackedRouter(16))
+    n = check_ticks(SubscriptionProcessor(wm), random_events(2000, seed=7), [1, 2, 5, 97, 13, 40])
+    assert n > 100
 
 
 def test_facade_reference_kats_on_oracle_backend(kats):

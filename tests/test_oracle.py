@@ -205,3 +205,30 @@ def test_server_faithful_route_is_route_intersect_connected():
             assert fp[fo[m]:fo[m + 1]].tolist() == want, m
         assert fo[M] == P
     o.close()
+
+
+def test_fast_mode_matches_faithful_scan():
+    """wqo_set_fast (the checker mode of the full-size churn tests) answers remove_subscription's
+    O(#cubes) scan (area_map.rs:113-116) from per-peer cube counts: identical sets on a churn-heavy
+    op stream with duplicate / absent unsubscribes and REMOVE_PEER, world by world."""
+    from worldql_server_amd import abi
+    rng = np.random.default_rng(3)
+    n = 20000
+    kinds = rng.choice(3, n, p=[0.5, 0.45, 0.05]).astype(np.uint8)
+    world = rng.integers(0, 3, n).astype(np.uint32)
+    peer = rng.integers(0, 50, n).astype(np.uint32)
+    world[kinds == abi.OP_REMOVE_PEER] = np.where(rng.random(int((kinds == 2).sum())) < 0.5, 0xFFFFFFFF, 1)
+    pos = rng.uniform(-40, 40, (n, 3))
+    ops = abi.ops_array(world, peer, kinds, pos=pos)
+    a, b = orc.COracle(16), orc.COracle(16)
+    b.set_fast(True)
+    for lo in range(0, n, 1000):
+        a.apply_ops(ops[lo:lo + 1000])
+        b.apply_ops(ops[lo:lo + 1000])
+        assert a.counts() == b.counts()
+        for w in range(3):
+            assert (a.world_peers(w) == b.world_peers(w)).all()
+            for p in range(0, 50, 7):
+                assert a.is_subscribed_any(w, p) == b.is_subscribed_any(w, p)
+    with pytest.raises(ValueError):
+        b.set_fast(False)  # only on an empty map

@@ -53,6 +53,21 @@ __device__ __forceinline__ uint32_t wave_msg(int wave, uint32_t q) {
     return (q >> 6) * kBlock + wave * 64 + (q & 63);
 }
 
+// Error / overflow bits of a route call go to its counters and, sticky across calls, to the
+// handle's two health words {error OR, overflow OR} (wq_route_health), so a run of asynchronous
+// ticks whose counters were never read back can still be checked afterwards. Only ever reached
+// when something is wrong: a normal tick never touches the health words.
+__device__ __forceinline__ void flag_route(wq_route_counters* c, uint32_t* health, uint32_t err, uint32_t ovf) {
+    if (err) {
+        atomicOr(&c->error, err);
+        if (health) atomicOr(health, err);
+    }
+    if (ovf) {
+        atomicOr(&c->overflow, ovf);
+        if (health) atomicOr(health + 1, ovf);
+    }
+}
+
 struct RouteIn {
     const double* pos;
     const int64_t* keys;

@@ -28,6 +28,7 @@ struct CountParams {
                            // would serialise ~1k blocks at ~90 adds/us)
     wq_route_counters* cnt;
     wq_route_counters* cnt_next;
+    uint32_t* health;  // sticky {error, overflow} words (flag_route)
 };
 
 // e / locator once count, membership and list position are known (local_message.rs:60-86)
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
         }
         p.tile_F[blockIdx.x] = Fb > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Fb;
         p.tile_total[blockIdx.x] = Eb > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Eb;
-        if (Eb > 0xFFFFFFFFull) atomicOr(&p.cnt->error, 2u);
+        if (Eb > 0xFFFFFFFFull) flag_route(p.cnt, p.health, 2u, 0u);
     }
 }
 

@@ -21,6 +21,7 @@ struct TileScanParams {
     uint32_t M;
     uint64_t capacity;
     wq_route_counters* cnt;
+    uint32_t* health;  // sticky {error, overflow} words (flag_route)
 };
 
 __device__ __forceinline__ uint64_t wave_incl_scan_add64(uint64_t v, int lane) {
@@ -65,8 +66,8 @@ static __global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScan
         const uint64_t P = carry;
         p.offsets[p.M] = (uint32_t)P;
         p.cnt->n_pairs = P;
-        if (P > p.capacity) atomicOr(&p.cnt->overflow, 1u);
-        if (P > 0xFFFFFFFFull) atomicOr(&p.cnt->error, 2u);  // u32 CSR offsets cannot hold it
+        // u32 CSR offsets cannot hold more than 2^32-1 pairs: error bit 2
+        flag_route(p.cnt, p.health, P > 0xFFFFFFFFull ? 2u : 0u, P > p.capacity ? 1u : 0u);
     }
 }
 

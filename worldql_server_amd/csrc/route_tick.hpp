@@ -36,7 +36,8 @@ struct TickParams {
     uint32_t tag;       // this call's tag, 1 .. 2^30-1, differs from the previous call's
     wq_route_counters* cnt;
     wq_route_counters* cnt_next;
-    uint64_t* stamps;   // diagnostics (wq_debug_set_timeline) or nullptr
+    uint32_t* health;   // sticky {error, overflow} words (flag_route)
+    uint64_t* stamps;  // diagnostics (wq_debug_set_timeline) or nullptr
     uint32_t n_tiles;   // 256-message tiles (one block each)
 };
 
@@ -254,10 +255,10 @@ __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
             const uint64_t P = pre + T;
             p.offsets[p.in.M] = (uint32_t)P;
             p.cnt->n_pairs = P;
-            if (P > p.out.capacity) atomicOr(&p.cnt->overflow, 1u);
-            if (P > 0xFFFFFFFFull) atomicOr(&p.cnt->error, 2u);  // u32 CSR offsets cannot hold it
+            // u32 CSR offsets cannot hold more than 2^32-1 pairs: error bit 2
+            flag_route(p.cnt, p.health, P > 0xFFFFFFFFull ? 2u : 0u, P > p.out.capacity ? 1u : 0u);
         }
-        if (__any(gave_up) && lane == 0) atomicOr(&p.cnt->error, kErrSpin);
+        if (__any(gave_up) && lane == 0) flag_route(p.cnt, p.health, kErrSpin, 0u);
         if (lane == 0) sm.pre = pre;
     }
     if (b == NB - 1) {  // ... and sums every block's candidate count, all four waves polling
@@ -265,9 +266,10 @@ __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
         uint64_t F = 0;
         for (uint32_t k = tid; k < NB; k += kBlock) F += (uint32_t)poll_granule(p.fgran + k, p.tag, &gave_up);
         F = wave_sum_u64(F);
+        const bool any_gave_up = __any(gave_up);  // the whole wave votes, not lane 0 alone
         if (lane == 0) {
             atomicAdd(reinterpret_cast<unsigned long long*>(&p.cnt->n_candidates), (unsigned long long)F);
-            if (__any(gave_up)) atomicOr(&p.cnt->error, kErrSpin);
+            if (any_gave_up) flag_route(p.cnt, p.health, kErrSpin, 0u);
         }
     }
     lds_barrier();

@@ -37,6 +37,18 @@ __device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t* a, uint64_t 
     return lo;
 }
 
+__device__ __forceinline__ uint64_t upper_bound_u64(const uint64_t* a, uint64_t n, uint64_t v) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (a[mid] <= v)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
 struct GlobalParams {
     const uint32_t* world;
     const uint32_t* sender;
@@ -72,8 +84,10 @@ __global__ __launch_bounds__(kBlock) void global_count_kernel(GlobalParams p) {
     if (m < p.M) {
         const uint64_t w = p.world[m], me = p.sender[m];
         const uint8_t rp = p.repl[m];
+        // the world's range [lo, hi): hi is the upper bound of (w << 32) | 0xFFFFFFFF, which —
+        // unlike (w + 1) << 32 — does not wrap for w = 0xFFFFFFFF (WQ_WORLD_INVALID: no keys, empty)
         const uint64_t lo = lower_bound_u64(p.any, p.n_any, w << 32);
-        const uint64_t hi = lower_bound_u64(p.any, p.n_any, (w + 1) << 32);
+        const uint64_t hi = upper_bound_u64(p.any, p.n_any, (w << 32) | 0xFFFFFFFFull);
         cnt = (uint32_t)(hi - lo);
         const uint64_t at = lower_bound_u64(p.any, p.n_any, (w << 32) | me);
         const bool has = at < hi && p.any[at] == ((w << 32) | me);
@@ -189,6 +203,7 @@ int launch_route_global(wq_router* h, const uint32_t* d_world, const uint32_t* d
     sp.M = (uint32_t)M;
     sp.capacity = capacity;
     sp.cnt = cur;
+    sp.health = route_health(h);
     hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, sp);
     WQ_HIP(h, hipGetLastError());
     hipLaunchKernelGGL(global_offsets_kernel, dim3(n_tiles), dim3(kBlock), 0, s, gp);

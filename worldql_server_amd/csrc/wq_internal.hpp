@@ -156,6 +156,9 @@ inline TableView table_view(const wq_router* h) {
     v.r2 = h->radius > 0.0 ? h->radius * h->radius : -1.0;
     return v;
 }
+// Sticky {error OR, overflow OR} words of every route / global call since the last
+// wq_route_health: the first 8 bytes of the route workspace (route_counters allocates it).
+inline uint32_t* route_health(wq_router* h) { return h->rws.buf.as<uint32_t>(); }
 // wq_route.hip
 int route_config_count();
 // The tick's counter slots (this call's, the next call's); *cur == nullptr when M == 0 (offsets[0]

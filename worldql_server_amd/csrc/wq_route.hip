@@ -85,7 +85,8 @@ int route_counters(wq_router* h, size_t M, uint32_t* d_offsets, wq_route_counter
                    wq_route_counters** nxt_out) {
     hipStream_t s = h->stream;
     RouteWs& rw = h->rws;
-    // workspace: [pad 64][counters x2 (32 B each)] — each call's count pass zeroes the next slot
+    // workspace: [health u32 x2, pad to 64][counters x2 (24 B each)] — each call's count pass
+    // zeroes the next slot; the health words are only cleared by wq_route_health
     if (!rw.buf.p) {
         WQ_ALLOC(h, rw.buf, 128);
         WQ_HIP(h, hipMemsetAsync(rw.buf.p, 0, 128, s));
@@ -150,6 +151,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         tp.tag = (uint32_t)(rw.calls % ((1ull << 30) - 1)) + 1u;
         tp.cnt = cur;
         tp.cnt_next = nxt;
+        tp.health = route_health(h);
         tp.stamps = rw.stamps;
         tp.n_tiles = (uint32_t)nb;
         cfg.tick(tp, s, (unsigned)nb);
@@ -195,6 +197,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         tsp.M = (uint32_t)M;
         tsp.capacity = capacity;
         tsp.cnt = cur;
+        tsp.health = route_health(h);
         hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, tsp);
         WQ_HIP(h, hipGetLastError());
         hipLaunchKernelGGL((spill_copy_kernel<kSpillStage, 2>), dim3(nb), dim3(kBlock), 0, s, sp);
@@ -225,6 +228,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     cp.tile_F = tile_F;
     cp.cnt = cur;
     cp.cnt_next = nxt;
+    cp.health = route_health(h);
     if (radius)
         hipLaunchKernelGGL(count_radius_kernel, dim3(n_count), dim3(kBlock), 0, s, cp);
     else
@@ -240,6 +244,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     sp.M = (uint32_t)M;
     sp.capacity = capacity;
     sp.cnt = cur;
+    sp.health = route_health(h);
     hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, sp);
     WQ_HIP(h, hipGetLastError());
 

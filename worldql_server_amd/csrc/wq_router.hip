@@ -34,6 +34,7 @@ using namespace wq;
 
 namespace {
 
+constexpr size_t kAutoShapeMinMsgs = 256;  // one route block
 thread_local std::string g_err;  // errors before a handle exists
 
 int check_device(int device, std::string* why) {
@@ -201,8 +202,34 @@ int wq_set_radius(wq_router* h, double radius) {
 
 int wq_set_fanout_hint(wq_router* h, double pairs_per_message) {
     if (!h) return WQ_E_INVALID;
-    h->heavy_fanout = pairs_per_message >= WQ_HEAVY_FANOUT;  // NaN compares false: single launch
+    if (!(pairs_per_message >= 0.0)) {  // negative or NaN: back to the automatic choice
+        h->fanout_auto = true;
+        return WQ_OK;
+    }
+    h->heavy_fanout = pairs_per_message >= WQ_HEAVY_FANOUT;
     h->fanout_auto = false;  // the caller decides from now on
+    return WQ_OK;
+}
+
+int wq_debug_route_shape(wq_router* h, int* heavy_fanout, int* fanout_auto) {
+    if (!h || !heavy_fanout || !fanout_auto) return WQ_E_INVALID;
+    *heavy_fanout = h->heavy_fanout ? 1 : 0;
+    *fanout_auto = h->fanout_auto ? 1 : 0;
+    return WQ_OK;
+}
+
+int wq_route_health(wq_router* h, uint32_t* error_bits, uint32_t* overflow) {
+    if (!h || !error_bits || !overflow) return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    *error_bits = 0;
+    *overflow = 0;
+    if (!h->rws.buf.p) return WQ_OK;  // no route call yet
+    uint32_t w[2];
+    WQ_HIP(h, hipMemcpyAsync(w, h->rws.buf.p, 8, hipMemcpyDeviceToHost, h->stream));
+    WQ_HIP(h, hipMemsetAsync(h->rws.buf.p, 0, 8, h->stream));
+    WQ_HIP(h, hipStreamSynchronize(h->stream));
+    *error_bits = w[0];
+    *overflow = w[1];
     return WQ_OK;
 }
 
@@ -335,7 +362,9 @@ int wq_route_tick(wq_router* h, const double* pos, const int64_t* keys, const ui
                           (msgs && cap) ? reinterpret_cast<uint32_t*>(dout + om) : nullptr, cap);
     if (rc) return rc;
     rc = read_back(h, M, dout, op, om, cap, capacity, offsets, peers, msgs, n_pairs);
-    if ((rc == WQ_OK || rc == WQ_E_CAPACITY) && h->fanout_auto && M)  // the next tick's shape
+    // the next tick's shape, from ticks of at least one block of messages (a single-message query
+    // such as AreaMap::get_subscribed_peers says nothing about a tick's fan-out)
+    if ((rc == WQ_OK || rc == WQ_E_CAPACITY) && h->fanout_auto && M >= kAutoShapeMinMsgs)
         h->heavy_fanout = (double)*n_pairs >= WQ_HEAVY_FANOUT * (double)M;
     return rc;
 }
@@ -363,6 +392,8 @@ int wq_route_global(wq_router* h, const uint32_t* world, const uint32_t* sender,
     if (!h || !offsets || !n_pairs || (M && (!world || !sender || !repl)) || (capacity && !peers))
         return WQ_E_INVALID;
     if (M >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
+    for (size_t i = 0; i < M; ++i)
+        if (world[i] == WQ_WORLD_INVALID) return set_error(h, WQ_E_INVALID, "reserved world id in a GlobalMessage");
     WQ_HIP(h, hipSetDevice(h->device));
     int rc0 = table_ensure_any(h);
     if (rc0) return rc0;

@@ -77,6 +77,8 @@ def load_library(build_if_missing: bool = True):
         "wq_set_peer_positions_device": ([vp, vp, sz], i32),
         "wq_set_radius": ([vp, ctypes.c_double], i32),
         "wq_set_fanout_hint": ([vp, ctypes.c_double], i32),
+        "wq_debug_route_shape": ([vp, ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
+        "wq_route_health": ([vp, ctypes.POINTER(u32), ctypes.POINTER(u32)], i32),
         "wq_shard_ops": ([vp, vp, sz, u32, vp], i32),
         "wq_shard_messages_device": ([vp, vp, vp, vp, vp, vp, sz, u32, vp, vp], i32),
         "wq_route_records_device": ([vp, vp, sz, vp, vp, vp, sz, vp], i32),
@@ -291,6 +293,27 @@ class Router:
         """Expected recipients per message (e.g. the previous tick's P / M): >= 16 selects the
         count / scan / emit tick shape (wq_set_fanout_hint)."""
         self._check(self.lib.wq_set_fanout_hint(self.h, float(pairs_per_message)))
+
+    def route_shape(self):
+        """(heavy_fanout, fanout_auto) of the next default-config tick (wq_debug_route_shape)."""
+        a, b = ctypes.c_int(), ctypes.c_int()
+        self._check(self.lib.wq_debug_route_shape(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return bool(a.value), bool(b.value)
+
+    def route_health(self):
+        """(error bits OR, overflow OR) over every route / global call since the last read
+        (wq_route_health; clears them)."""
+        e, o = ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self.lib.wq_route_health(self.h, ctypes.byref(e), ctypes.byref(o)))
+        return e.value, o.value
+
+    def check_health(self) -> None:
+        """Raises WQError when any tick since the last check reported an error or an overflow."""
+        e, o = self.route_health()
+        if e & 4:
+            raise WQError(abi.WQ_E_TIMEOUT, f"a route look-back spin gave up (error bits {e:#x})")
+        if e or o:
+            raise WQError(abi.WQ_E_CAPACITY, f"route error bits {e:#x}, overflow {o}")
 
     def set_stream(self, stream_ptr: int | None) -> None:
         self._check(self.lib.wq_set_stream(self.h, stream_ptr or None))

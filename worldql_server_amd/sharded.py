@@ -145,6 +145,19 @@ class DeviceShard:
                                  self.cap, self.counters.data_ptr(), keys_ptr=_ptr(keys))
         return offsets, self._peers
 
+    def counters_i64(self) -> torch.Tensor:
+        """The latest route call's wq_route_counters as 3 int64 words {P, F, overflow | error << 32}
+        (device), so a host sync the tick already makes can carry them."""
+        return self.counters.view(torch.int64)
+
+    @staticmethod
+    def check_counters(words) -> None:
+        """Raises when a route call reported an error (host copy of counters_i64)."""
+        err = (int(words[2]) >> 32) & 0xFFFFFFFF
+        if err:
+            code = abi.WQ_E_TIMEOUT if err & 4 else abi.WQ_E_CAPACITY
+            raise RuntimeError(f"wq error {code}: route counters report error bits {err:#x}")
+
     def read_counters(self):
         """(P, F) of the latest route call (synchronises the stream)."""
         self.stream.synchronize()
@@ -208,7 +221,11 @@ class ShardedRouter:
         if G == 1:
             self.last_recv = M
             offsets, peers = be.route_local(pos, keys, world, sender, repl)
-            P = int(offsets[M].item()) if M else 0
+            P = 0
+            if M:  # one host sync: P and the call's counters
+                h = torch.cat([offsets[M:M + 1].to(torch.int64), be.counters_i64()]).cpu().tolist()
+                be.check_counters(h[1:])
+                P = h[0]
             if P > be.cap:
                 offsets, peers = be.route_local(pos, keys, world, sender, repl, P_hint=P)
             return ShardedTick(torch.arange(M, device=dev), offsets.to(torch.int64), peers[:P])
@@ -232,8 +249,9 @@ class ShardedRouter:
         pair_send = (off_b[1:] - off_b[:-1]).to(torch.int64)
         pair_recv = torch.empty_like(pair_send)
         ex.all_to_all(pair_recv, pair_send, ones, ones)
-        ps_pr = torch.cat([pair_send, pair_recv]).cpu().tolist()  # host sync 2
-        ps, pr = ps_pr[:G], ps_pr[G:]
+        ps_pr = torch.cat([pair_send, pair_recv, be.counters_i64()]).cpu().tolist()  # host sync 2
+        be.check_counters(ps_pr[2 * G:])  # a route error must not hand back wrong pairs
+        ps, pr = ps_pr[:G], ps_pr[G:2 * G]
         P = sum(ps)
         if P > be.cap:  # the pair buffer was too small: offsets are right, re-run with room
             offsets, peers = be.route_records(recv, R, P_hint=P)

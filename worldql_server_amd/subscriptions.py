@@ -51,22 +51,49 @@ def _key_args(cube: ToCubeArea):
 
 
 class PeerIds:
-    """Uuid (any hashable) <-> dense u32 peer id."""
+    """Uuid (any hashable) <-> dense u32 peer id, with ids recycled after a disconnect.
+
+    The reference keys peers by Uuid and forgets a peer when it disconnects (PeerMap::remove,
+    worldql_server/src/transport/peer_map.rs:121-141, then WorldMap::remove_peer). `release` does
+    the same here: the id goes on a free list once the table no longer holds the peer, so per-peer
+    arrays on the device (F2 send lists, C5 positions) stay bounded by the peers connected at once
+    (`high_water`), not by every peer that ever connected."""
 
     def __init__(self):
         self._ids: dict = {}
         self._peers: list = []
+        self._free: list = []
 
     def id(self, peer: Hashable) -> int:
         pid = self._ids.get(peer)
         if pid is None:
-            pid = len(self._peers)
+            if self._free:
+                pid = self._free.pop()
+                self._peers[pid] = peer
+            else:
+                pid = len(self._peers)
+                self._peers.append(peer)
             self._ids[peer] = pid
-            self._peers.append(peer)
         return pid
 
     def lookup(self, peer: Hashable) -> Optional[int]:
         return self._ids.get(peer)
+
+    def release(self, peer: Hashable) -> Optional[int]:
+        """Forget `peer` (call after its REMOVE_PEER op is applied); returns its former id."""
+        pid = self._ids.pop(peer, None)
+        if pid is not None:
+            self._peers[pid] = None
+            self._free.append(pid)
+        return pid
+
+    @property
+    def high_water(self) -> int:
+        """Ids ever handed out at once: per-peer device arrays need this many entries."""
+        return len(self._peers)
+
+    def __len__(self) -> int:
+        return len(self._ids)
 
     def peer(self, pid: int) -> Hashable:
         return self._peers[pid]
@@ -98,11 +125,15 @@ class WorldMap:
 
     def remove_peer(self, uuid: Hashable) -> bool:  # world_map.rs:41-61
         pid = self.peer_ids.lookup(uuid)
-        if pid is None or not self._maps:
+        if pid is None:
+            return False
+        if not self._maps:
+            self.peer_ids.release(uuid)
             return False
         wids = np.array([am.world_id for am in self._maps.values()], dtype=np.uint32)
         removed = bool(self.router.is_subscribed_any(wids, np.full(len(wids), pid, np.uint32)).any())
         self.router.apply_ops(np.array([abi.make_op(abi.WORLD_INVALID, pid, abi.OP_REMOVE_PEER)], abi.OP_DTYPE))
+        self.peer_ids.release(uuid)  # the peer is gone (peer_map.rs:121-141): its id is free again
         return removed
 
 
