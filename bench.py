@@ -1,24 +1,23 @@
 #!/usr/bin/env python3
-"""Headline benchmark: routed message->peer pairs per second, one tick = one route launch.
+"""Headline benchmark: routed message->peer pairs per second per tick, % of the HBM roofline.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[1] = SURVEY.md §8(d) C2): 1 world, 100k peers each subscribed
-to a 3x3x3 cube neighbourhood (2.7M subscriptions), 1M LocalMessages per tick, positions
-U[-512,512)^3, cube_size 16, ExceptSelf, synthetic (splitmix64). The table is built once
-(AreaSubscribe ops through the GPU build path; its time is reported separately); every step is
-one full tick of the hot path on HBM-resident inputs: quantise -> probe -> filter -> compact into
-CSR offsets + (msg, peer) pairs, the launch that also resolves the tick's global output offsets.
-
-Multi-GPU (weak scaling, value = pairs of all ranks / max-over-ranks time):
-  --shard world (default)  every rank owns its own world (its own 100k peers and 1M messages per
-                           tick); no message crosses ranks, so no collective in the timed region.
-  --shard cube             one world G times the C2 volume (100k*G peers); every rank ingests 1M
-                           messages anywhere in it, and the tick runs the cube-hash sharded path
-                           (worldql_server_amd/sharded.py): owner grouping, RCCL all-to-all of the
-                           records, route on the owner, all-to-all of the pairs back.
+Headline workload: SURVEY.md §8(d) C3, the configuration north_star's target is quoted on — 1M peers
+each subscribed to a 3x3x3 neighbourhood (27M subscriptions), 10M LocalMessages per tick, 90% from
+256 Zipf-weighted Gaussian hotspots, cube_size 16, ExceptSelf, synthetic (splitmix64).
+  N = 1   the whole configuration on one GPU: every step is one full tick of the hot path on
+          HBM-resident inputs (quantise -> probe -> filter -> CSR offsets + (msg, peer) pairs), with
+          the C2 line (BASELINE.json configs[1]: 100k peers, 1M messages) nested under extra.c2.
+  N > 1   strong scaling by cube hash through the C ABI's sharded tick: every rank ingests M/N of
+          the messages; shard -> RCCL all-to-all of the records -> route on the owners -> RCCL
+          all-to-all of the pairs back to the ingesting GPU (wq_sharded_route_tick_device).
+The table is built once before timing. Every timed loop is checked afterwards through the
+routers' sticky health words (wq_route_health): no tick may have given up or overflowed.
+Other configs: --config c1 | c2 | c4 | c5 (bench_configs.py); --config c2 --shard cube = one world
+of N x the C2 volume over the same sharded tick (weak scaling).
 """
 from __future__ import annotations
 
@@ -345,52 +344,44 @@ def run_c2(a, rank, world_size, local_rank, dev) -> dict:
 
 
 def run_cube(a, rank, world_size, local_rank, dev):
-    """--shard cube: the cube-hash sharded tick, timed end to end (exchanges included)."""
+    """--shard cube: one world of N x the C2 volume sharded by cube hash through the C ABI's
+    sharded tick (wq_sharded_route_tick_device over RCCL), timed end to end, exchanges included."""
     import torch
-    import torch.distributed as dist
+    import bench_configs
     from worldql_server_amd.router import Router
-    from worldql_server_amd.sharded import DeviceShard, DistExchange, LocalExchange, ShardedRouter
 
     w, lo, hi = cube_workload(rank, world_size, a.scale)
+    M = hi - lo
     stream = torch.cuda.Stream(device=dev)
     r = Router(w.cube_size, local_rank)
-    be = DeviceShard(r, stream)
-    sr = ShardedRouter(be, DistExchange() if world_size > 1 else LocalExchange())
+    r.set_stream(stream.cuda_stream)
+    if world_size > 1:
+        bench_configs.attach_rccl(r, rank, world_size)
     t0 = time.perf_counter()
-    sr.apply_ops(w.ops)
+    r.sharded_apply_ops(w.ops)
     build_s = time.perf_counter() - t0
     st = r.stats()
-    M = hi - lo
-    with torch.cuda.stream(stream):
-        pos = torch.from_numpy(w.pos[lo:hi]).to(dev)
-        world = torch.from_numpy(w.world[lo:hi].view(np.int32)).to(dev)
-        sender = torch.from_numpy(w.sender[lo:hi].view(np.int32)).to(dev)
-        repl = torch.from_numpy(w.repl[lo:hi]).to(dev)
-        for _ in range(max(a.warmup, 1)):
-            res = sr.tick(world, sender, repl, pos=pos)
-        stream.synchronize()
-        P_in = int(res.peers.shape[0])  # pairs of the messages this rank ingested
-        P_own, F_own = be.read_counters()  # pairs / candidates routed on this shard
-        R = sr.last_recv
-        if world_size > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t_wall = time.perf_counter()
-        for _ in range(a.steps):
-            res = sr.tick(world, sender, repl, pos=pos)
-        torch.cuda.synchronize(dev)
-        t_ms = (time.perf_counter() - t_wall) * 1e3
-        if world_size > 1:
-            dist.barrier()
-        t_max_ms, pairs_all = reduce_over_ranks(t_ms, P_in, dev, world_size)
-        r.profile_enable(True)
-        for _ in range(a.steps):
-            sr.tick(world, sender, repl, pos=pos)
-        k_ms, launches = r.profile_read()
-        r.profile_enable(False)
-    k_avg_s = k_ms / launches / 1e3
-    B = algorithmic_bytes(R, F_own, P_own)
-    achieved = B / k_avg_s / 1e9
+    pos = torch.from_numpy(w.pos[lo:hi]).to(dev)
+    world = torch.from_numpy(w.world[lo:hi].view(np.int32)).to(dev)
+    sender = torch.from_numpy(w.sender[lo:hi].view(np.int32)).to(dev)
+    repl = torch.from_numpy(w.repl[lo:hi]).to(dev)
+    offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    cap = 24 * M + 1024
+    peers = torch.empty(cap, dtype=torch.int32, device=dev)
+    msgs = torch.empty(cap, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    state = {"P": 0}
+
+    def tick():
+        rc, P = r.sharded_route_device(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M,
+                                       offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap)
+        assert rc == 0, (rc, P)
+        state["P"] = P
+
+    for _ in range(max(a.warmup, 1)):
+        tick()
+    t_ms = timed_ticks(tick, a.steps, stream, dev, world_size, [r])
+    t_max_ms, pairs_all = reduce_over_ranks(t_ms, state["P"], dev, world_size)
     out = {
         "metric": METRIC,
         "value": pairs_all * a.steps / (t_max_ms / 1e3),
@@ -412,10 +403,9 @@ def run_cube(a, rank, world_size, local_rank, dev):
             "parallelism": f"cube-hash x{world_size}" + (" (RCCL all-to-all)" if world_size > 1 else ""),
             "table_build_s": round(build_s, 3),
         },
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "route tick on the owner shard (count + tile_scan + emit)",
-                     "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
+        "roofline": roofline(algorithmic_bytes(M, int(pairs_all) // world_size, int(pairs_all) // world_size),
+                             t_max_ms / a.steps / 1e3, "whole sharded tick per GPU (shard + exchanges + owner route "
+                             "+ unshard)"),
     }
     if rank == 0 and world_size == 1 and not a.no_cpu_baseline:
         w1 = shard_workload(0, a.scale)

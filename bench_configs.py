@@ -222,61 +222,69 @@ def run_c3(a, rank, world_size, local_rank, dev):
     return out
 
 
-def _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s):
-    import torch
+def attach_rccl(r, rank: int, world_size: int) -> None:
+    """This rank's router becomes shard `rank` of world_size over its own RCCL communicator (the id
+    travels over the bench's process group)."""
     import torch.distributed as dist
+    from worldql_server_amd.router import rccl_unique_id
+    uid = [rccl_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    r.attach_rccl(world_size, rank, uid[0])
+
+
+def _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s):
+    """C3 strong scaling through the C ABI's sharded tick (wq_sharded_route_tick_device over RCCL):
+    every rank ingests M/N of the 10M messages; each tick groups them by owner, exchanges the
+    records, routes on the owners and returns every (message, peer) pair to the ingesting GPU in
+    message order. value = all ranks' pairs / the max-over-ranks time of the timed ticks."""
+    import torch
     from worldql_server_amd.router import Router
-    from worldql_server_amd.sharded import DeviceShard, DistExchange, ShardedRouter
 
     M_all = len(w.world)
     lo, hi = rank * M_all // world_size, (rank + 1) * M_all // world_size
+    M = hi - lo
     stream = torch.cuda.Stream(device=dev)
     r = Router(w.cube_size, local_rank)
-    be = DeviceShard(r, stream)
-    sr = ShardedRouter(be, DistExchange())
+    r.set_stream(stream.cuda_stream)
+    attach_rccl(r, rank, world_size)
     t0 = time.perf_counter()
-    sr.apply_ops(w.ops)
+    r.sharded_apply_ops(w.ops)
     build_s = time.perf_counter() - t0
     st = r.stats()
-    with torch.cuda.stream(stream):
-        pos = torch.from_numpy(w.pos[lo:hi]).to(dev)
-        world = torch.from_numpy(w.world[lo:hi].view(np.int32)).to(dev)
-        sender = torch.from_numpy(w.sender[lo:hi].view(np.int32)).to(dev)
-        repl = torch.from_numpy(w.repl[lo:hi]).to(dev)
-        for _ in range(max(a.warmup, 1)):
-            res = sr.tick(world, sender, repl, pos=pos)
-        stream.synchronize()
-        P_in = int(res.peers.shape[0])
-        P_own, F_own = be.read_counters()
-        R = sr.last_recv
-        r.set_fanout_hint(P_own / max(R, 1))  # the owner's tick shape from its warm-up fan-out
-        dist.barrier()
-        torch.cuda.synchronize(dev)
-        t_wall = time.perf_counter()
-        for _ in range(a.steps):
-            res = sr.tick(world, sender, repl, pos=pos)
-        torch.cuda.synchronize(dev)
-        t_ms = (time.perf_counter() - t_wall) * 1e3
-        dist.barrier()
-        t_max_ms, pairs_all = reduce_over_ranks(t_ms, P_in, dev, world_size)
-        r.profile_enable(True)
-        for _ in range(a.steps):
-            sr.tick(world, sender, repl, pos=pos)
-        k_ms, launches = r.profile_read()
-        r.profile_enable(False)
-    k_avg_s = k_ms / launches / 1e3
-    B = algorithmic_bytes(R, F_own, P_own)
+    pos = torch.from_numpy(w.pos[lo:hi]).to(dev)
+    world = torch.from_numpy(w.world[lo:hi].view(np.int32)).to(dev)
+    sender = torch.from_numpy(w.sender[lo:hi].view(np.int32)).to(dev)
+    repl = torch.from_numpy(w.repl[lo:hi]).to(dev)
+    offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    r.set_fanout_hint(40.0)  # C3's fan-out: the owners route with count / scan / emit
+    cap = 64 * M + 1024
+    peers = torch.empty(cap, dtype=torch.int32, device=dev)
+    msgs = torch.empty(cap, dtype=torch.int32, device=dev)
+    state = {"P": 0}
+
+    def tick():
+        rc, P = r.sharded_route_device(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M,
+                                       offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap)
+        assert rc == 0, (rc, P)
+        state["P"] = P
+
+    for _ in range(max(a.warmup, 1)):
+        tick()
+    t_ms = timed_ticks(tick, a.steps, stream, dev, world_size, [r])
+    t_max_ms, pairs_all = reduce_over_ranks(t_ms, state["P"], dev, world_size)
     out = _line(a, world_size, pairs_all * a.steps / (t_max_ms / 1e3), t_max_ms / a.steps, "strong",
                 f"C3 over {world_size} GPUs by cube hash: 1M peers x 3x3x3, 10M LocalMessages/tick in total, "
                 "256 Zipf(1) Gaussian hotspots + 10% uniform, cube_size 16, ExceptSelf"
                 + ("" if a.scale == 1.0 else f" (scaled {a.scale})"),
-                {"messages_per_tick": M_all, "messages_per_gpu": hi - lo, "peers": w.n_peers,
+                {"messages_per_tick": M_all, "messages_per_gpu": M, "peers": w.n_peers,
                  "subscriptions_this_shard": int(st["n_entries"]), "pairs_per_tick": int(pairs_all),
-                 "parallelism": f"cube-hash x{world_size} (RCCL all-to-all)", "table_build_s": round(build_s, 3),
-                 "generate_s": round(gen_s, 1)},
-                {"bound": "hbm", "achieved": B / k_avg_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                 "frac": B / k_avg_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                 "kernel": "route tick on rank 0's shard", "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
+                 "parallelism": f"cube-hash x{world_size} (wq_sharded_route_tick_device, RCCL all-to-all: records "
+                                "out, pairs back)",
+                 "table_build_s": round(build_s, 3), "generate_s": round(gen_s, 1)},
+                roofline(algorithmic_bytes(M_all, int(pairs_all), int(pairs_all)) // world_size, t_max_ms / a.steps / 1e3,
+                         "whole sharded tick per GPU (shard + exchanges + owner route + unshard); bytes = the "
+                         "tick's SURVEY §8(d) bytes / N"),
                 "synthetic (splitmix64, SURVEY.md §8(d) C3 generator)")
     r.close()
     return out
@@ -544,14 +552,13 @@ def _cpu_c5_sample(init, tick_ops, pos_after, radius, seconds):
 
 
 def _run_c5_sharded(a, rank, world_size, local_rank, dev):
-    """C5 over G GPUs by cube hash (strong scaling): every rank applies the churn ops it owns and
-    holds every entity's position; it ingests 1/G of the messages, whose records carry their
-    positions to the owners (RCCL all-to-all), which route them with the radius filter."""
+    """C5 over G GPUs by cube hash (strong scaling) through the C ABI's sharded tick: every rank
+    applies the churn ops of the cubes it owns (wq_apply_ops_device on its slice of the op stream)
+    and holds every entity's position; it ingests 1/G of the messages, whose records carry their
+    positions to the owners (RCCL), which route them with the radius filter; pairs come back."""
     import torch
-    import torch.distributed as dist
     from worldql_server_amd import synth_ext
     from worldql_server_amd.router import Router
-    from worldql_server_amd.sharded import DeviceShard, DistExchange, ShardedRouter
 
     c5 = synth_ext.config_c5(scale=a.scale)
     t0 = time.perf_counter()
@@ -564,99 +571,54 @@ def _run_c5_sharded(a, rank, world_size, local_rank, dev):
     gen_s = time.perf_counter() - t0
     N = c5.n
     lo, hi = rank * N // world_size, (rank + 1) * N // world_size
+    M = hi - lo
     stream = torch.cuda.Stream(device=dev)
     r = Router(16, local_rank)
-    be = DeviceShard(r, stream)
-    sr = ShardedRouter(be, DistExchange())
-    sr.apply_ops(init)
-    be.set_radius(c5.radius, init_pos)
+    r.set_stream(stream.cuda_stream)
+    attach_rccl(r, rank, world_size)
+    r.sharded_apply_ops(init)
+    r.set_peer_positions(init_pos)
+    r.set_radius(c5.radius)
     own_ops = []
-    for ops, _ in ticks:  # host-partitioned churn: the ops of the cubes this rank owns
+    for ops, _ in ticks:  # the churn of the cubes this rank owns (host-partitioned on ingest)
         owner = r.shard_ops(ops, world_size)
         own_ops.append(_ops_tensor(ops[owner == rank], dev))
     pos_d = [torch.from_numpy(p_).to(dev) for _, p_ in ticks]
-    world = torch.zeros(hi - lo, dtype=torch.int32, device=dev)
+    world = torch.zeros(M, dtype=torch.int32, device=dev)
     sender = torch.arange(lo, hi, dtype=torch.int32, device=dev)
-    repl = torch.zeros(hi - lo, dtype=torch.uint8, device=dev)
+    repl = torch.zeros(M, dtype=torch.uint8, device=dev)
+    offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    cap = 16 * M + 1024
+    peers = torch.empty(cap, dtype=torch.int32, device=dev)
+    msgs = torch.empty(cap, dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
+    state = {"i": 0, "P": 0}
 
-    def one(i):
+    def one():
+        i = state["i"]
         r.apply_ops_device(own_ops[i].data_ptr(), int(own_ops[i].shape[0]) // 40)
         r.set_peer_positions_device(pos_d[i].data_ptr(), N)
-        return sr.tick(world, sender, repl, pos=pos_d[i][lo:hi])
+        p = pos_d[i][lo:hi]
+        rc, P = r.sharded_route_device(p.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M,
+                                       offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap)
+        assert rc == 0, (rc, P)
+        state["P"] += P
+        state["i"] = i + 1
 
-    with torch.cuda.stream(stream):
-        for i in range(a.warmup):
-            one(i)
-        stream.synchronize()
-        dist.barrier()
-        P_in = 0
-        t_wall = time.perf_counter()
-        for i in range(a.warmup, a.warmup + a.steps):
-            res = one(i)
-            P_in += int(res.peers.shape[0])
-        torch.cuda.synchronize(dev)
-        t_ms = (time.perf_counter() - t_wall) * 1e3
-        dist.barrier()
-    t_max_ms, pairs_all = reduce_over_ranks(t_ms, P_in, dev, world_size)
+    for _ in range(a.warmup):
+        one()
+    state["P"] = 0
+    t_ms = timed_ticks(one, a.steps, stream, dev, world_size, [r])
+    t_max_ms, pairs_all = reduce_over_ranks(t_ms, state["P"], dev, world_size)
     out = _line(a, world_size, pairs_all / (t_max_ms / 1e3), t_max_ms / a.steps, "strong",
                 f"C5 over {world_size} GPUs by cube hash: 1M entities, incremental churn on the owners, "
-                "message positions to the owners by RCCL all-to-all, exact radius filter r=16"
+                "message positions to the owners by RCCL (wq_sharded_route_tick_device), exact radius filter r=16"
                 + ("" if a.scale == 1.0 else f" (scaled {a.scale})"),
-                {"messages_per_tick": N, "messages_per_gpu": hi - lo, "entities": N,
+                {"messages_per_tick": N, "messages_per_gpu": M, "entities": N,
                  "pairs_per_tick": int(pairs_all) // a.steps,
                  "parallelism": f"cube-hash x{world_size} (RCCL all-to-all)", "generate_s": round(gen_s, 1)},
                 {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                  "traffic": None, "kernel": "whole sharded tick (update + exchange + radius route)"},
                 "synthetic (splitmix64, SURVEY.md §8(d) C5 generator)")
     r.close()
-    if not a.no_cpu_baseline:
-        out["cpu_baseline"] = _cpu_c5_sample(init, [t[0] for t in ticks[:a.warmup + 1]], ticks[a.warmup][1],
-                                             c5.radius, a.cpu_seconds)
     return out
-
-
-def _cpu_c5_sample(init, tick_ops, pos_after, radius, seconds):
-    """C5 on 1 host thread by the C restatement, one whole tick estimated from two timed parts:
-      route  the tick's 1M messages with the radius filter (wqo_route_radius), on a table brought
-             to the tick's state in checker mode (wqo_set_fast; the route itself is the same code);
-      churn  a strided sample of the tick's ops applied to a FAITHFUL table (the reference's
-             O(#cubes) scan per unsubscribe, area_map.rs:113-116), scaled to all of the tick's ops.
-    value = pairs of the tick / (t_route + n_ops * t_per_op). The tables are built untimed."""
-    import ctypes
-    from oracle import oracle as orc
-    vp = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
-    M = len(pos_after)
-    fast = orc.COracle(16)
-    fast.set_fast(True)
-    fast.apply_ops(init)
-    for ops in tick_ops:  # the table as the first timed tick sees it
-        fast.apply_ops(ops)
-    world = np.zeros(M, np.uint32)
-    sender = np.arange(M, dtype=np.uint32)
-    repl = np.zeros(M, np.uint8)
-    offs = np.empty(M + 1, np.uint32)
-    t0 = time.perf_counter()
-    P = fast.lib.wqo_route_radius(fast.h, vp(np.ascontiguousarray(pos_after)), vp(world), vp(sender), vp(repl), M,
-                                  vp(np.ascontiguousarray(pos_after)), M, float(radius), vp(offs), None, 0, None)
-    t_route = time.perf_counter() - t0
-    fast.close()
-    faith = orc.COracle(16)
-    faith.apply_ops(init)
-    n_ops = len(ops)
-    stride = max(1, n_ops // 4096)
-    sample = np.ascontiguousarray(ops[::stride])
-    done, t_ops = 0, 0.0
-    while done < len(sample) and t_ops < seconds / 2:
-        chunk = sample[done:done + 64]
-        t0 = time.perf_counter()
-        faith.apply_ops(chunk)
-        t_ops += time.perf_counter() - t0
-        done += len(chunk)
-    faith.close()
-    t_tick = t_route + n_ops * (t_ops / done)
-    return {"value": P / t_tick, "unit": "pairs/s", "cores": 1, "kind": "port",
-            "sample": f"C5 tick estimate: {M} messages routed with the radius filter in {t_route:.2f} s "
-                      f"({P} pairs) + {done} of the tick's {n_ops} churn ops (every {stride}th) applied with the "
-                      f"reference's O(#cubes) unsubscribe scan in {t_ops:.2f} s, scaled to all {n_ops} ops: "
-                      f"{t_tick:.1f} s per tick, oracle/wq_oracle.c on 1 host thread"}

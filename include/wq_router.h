@@ -35,7 +35,7 @@ extern "C" {
 #define WQ_E_INVALID (-1)  /* bad argument (null handle, cube_size 0, reserved world id ...) */
 #define WQ_E_OOM (-2)      /* device allocation failed */
 #define WQ_E_HIP (-3)      /* HIP runtime error (message in wq_last_error) */
-#define WQ_E_RCCL (-4)     /* reserved for the multi-GPU exchange */
+#define WQ_E_RCCL (-4)     /* the multi-GPU exchange failed (RCCL, hub timeout, caller callback) */
 #define WQ_E_CAPACITY (-5) /* caller's output buffer too small; required size reported */
 #define WQ_E_NODEV (-6)    /* no usable gfx950 device: the path never falls back to the CPU */
 #define WQ_E_TIMEOUT (-7)  /* a bounded in-kernel spin gave up (must never happen) */
@@ -198,7 +198,8 @@ int wq_quantize_device(wq_router* h, const double* d_coords, size_t n, int64_t* 
  * holds every subscription a message to that cube can reach. A sharded tick is
  *   wq_shard_messages_device -> all-to-all of the records (RCCL) -> wq_route_records_device on
  *   the owner -> all-to-all of per-message counts and peers back to the ingesting GPU.
- * worldql_server_amd/sharded.py drives it over torch.distributed. */
+ * worldql_server_amd/sharded.py drives these over torch.distributed; the whole tick behind one
+ * call is wq_sharded_route_tick_device (below). */
 #define WQ_MAX_SHARDS 64
 #define WQ_SHARD_ALL 0xFFFFFFFFu /* owner of a REMOVE_PEER op: every shard */
 
@@ -232,6 +233,47 @@ int wq_shard_messages_device(wq_router* h, const double* d_pos, const int64_t* d
 int wq_route_records_device(wq_router* h, const wq_msg_rec* d_recs, size_t n_msgs, uint32_t* d_offsets,
                             uint32_t* d_peers, uint32_t* d_msgs, size_t capacity,
                             wq_route_counters* d_counters);
+
+/* ---- multi-GPU: sharded ticks behind the ABI ----
+ * A handle becomes shard `rank` of G by attaching an exchange; afterwards
+ *   wq_sharded_apply_ops            every shard is given the SAME op stream (the reference's one
+ *                                   subscription task, thread.rs:122-146) and keeps the ops of the
+ *                                   buckets it owns plus every REMOVE_PEER;
+ *   wq_sharded_route_tick_device    every shard is given its OWN ingested messages; the call runs
+ *                                   shard -> exchange -> route on the owners -> exchange back and
+ *                                   returns, on each shard, exactly the CSR wq_route_tick_device would
+ *                                   return for those messages on one GPU holding the whole table
+ *                                   (offsets[M+1] and peers[P] in message order, msgs[P] optional).
+ * The tick is collective: all G shards call it (M may be 0), each on its own thread or process.
+ * It reads two small count vectors back to the host (the exchange sizes) and is synchronous on
+ * return; *n_pairs = P. If P > capacity the tick still completes (its peers are not left waiting),
+ * returns WQ_E_CAPACITY with offsets written, and wq_sharded_copy_out re-copies the kept result
+ * into a larger buffer without another exchange. Exchange failures return WQ_E_RCCL.
+ * Exchanges: RCCL (one process per GPU, or several handles of one process), an in-process hub
+ * (G handles of one process, peer copies over xGMI), or the caller's own all-to-all. */
+#define WQ_RCCL_ID_BYTES 128
+/* The caller's all-to-all: send_bytes[d] bytes to shard d from d_send (segments contiguous in
+ * shard order), recv_bytes[s] bytes from shard s into d_recv (likewise); device pointers, ordered
+ * after the work already queued on hip_stream. Returns 0 on success. */
+typedef int (*wq_exchange_fn)(void* ctx, const void* d_send, const size_t* send_bytes, void* d_recv,
+                              const size_t* recv_bytes, void* hip_stream);
+typedef struct wq_hub wq_hub;
+int wq_hub_create(uint32_t n_shards, wq_hub** out);
+int wq_hub_destroy(wq_hub* hub);
+int wq_shard_attach_hub(wq_router* h, wq_hub* hub, uint32_t rank);
+/* RCCL: rank 0 makes the id (wq_rccl_unique_id), the caller distributes the 128 bytes, every rank
+ * attaches (collective, blocks until all G have joined). librccl is loaded at run time. */
+int wq_rccl_unique_id(uint8_t* id_out);
+int wq_shard_attach_rccl(wq_router* h, uint32_t n_shards, uint32_t rank, const uint8_t* id);
+int wq_shard_attach_exchange(wq_router* h, uint32_t n_shards, uint32_t rank, wq_exchange_fn fn, void* ctx);
+int wq_shard_detach(wq_router* h);
+int wq_shard_info(wq_router* h, uint32_t* n_shards, uint32_t* rank);
+int wq_sharded_apply_ops(wq_router* h, const wq_op* ops, size_t n);
+int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_keys,
+                                 const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
+                                 size_t n_msgs, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs,
+                                 size_t capacity, size_t* n_pairs);
+int wq_sharded_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity);
 
 /* ---- F2: per-peer send lists (PeerMap::broadcast_to, worldql_server/src/transport/peer_map.rs:151-163)
  * The transpose of a tick's message-major CSR for a transport that batches per peer: for every

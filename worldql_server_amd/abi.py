@@ -76,6 +76,7 @@ def concat_ops(parts) -> np.ndarray:
 
 # ---- multi-GPU (include/wq_router.h, "cube-hash ownership") ----
 MAX_SHARDS = 64
+RCCL_ID_BYTES = 128  # WQ_RCCL_ID_BYTES
 SHARD_ALL = 0xFFFFFFFF  # owner of a REMOVE_PEER op
 
 # struct wq_msg_rec: 40 bytes on the wire between GPUs

@@ -17,7 +17,7 @@ BUILD = os.path.join(PKG, "_build")
 LIB = os.path.join(PKG, "libwq_router.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["wq_route.hip", "wq_global.hip", "wq_query.hip", "wq_table.hip", "wq_delta.hip", "wq_shard.hip", "wq_peers.hip", "wq_router.hip"]
+SOURCES = ["wq_route.hip", "wq_global.hip", "wq_query.hip", "wq_table.hip", "wq_delta.hip", "wq_shard.hip", "wq_sharded.hip", "wq_peers.hip", "wq_router.hip"]
 HOST_SOURCES = ["wq_codec.cpp"]
 CXX = os.environ.get("CXX", "g++")
 HOST_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-pthread", "-Wall"]
@@ -60,7 +60,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
             subprocess.check_call(cmd)
             relink = True
     if relink or any(_mtime(o) > _mtime(LIB) for o in objs):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-pthread", "-o", LIB, *objs]
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-pthread", "-o", LIB, *objs, "-ldl"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)

@@ -97,6 +97,8 @@ struct ProfileEvents {
     bool enabled = false;
 };
 
+struct ShardCtx;  // wq_sharded.hip: the exchange a sharded tick uses, and its workspace
+
 }  // namespace wq
 
 struct wq_router {
@@ -137,6 +139,7 @@ struct wq_router {
     uint64_t n_ppos = 0;
     double radius = 0.0;
     wq::ProfileEvents prof;
+    wq::ShardCtx* shard = nullptr;  // wq_shard_attach_*: this handle is one shard of G
 };
 
 namespace wq {
@@ -185,6 +188,8 @@ int table_materialize(wq_router* h);
 // Rebuilds the any-keys if incremental updates left them stale.
 int table_ensure_any(wq_router* h);
 int set_error(wq_router* h, int code, const char* what, hipError_t e = hipSuccess);
+// wq_sharded.hip: frees the exchange and its workspace (destroys an RCCL communicator).
+void shard_release(wq_router* h);
 }  // namespace wq
 
 #define WQ_HIP(h, call)                                                    \

@@ -130,6 +130,7 @@ int wq_router_destroy(wq_router* h) {
     if (!h) return WQ_E_INVALID;
     (void)hipSetDevice(h->device);
     (void)hipStreamSynchronize(h->stream);
+    shard_release(h);
     for (auto e : h->prof.start) (void)hipEventDestroy(e);
     for (auto e : h->prof.stop) (void)hipEventDestroy(e);
     DevBuf* bufs[] = {&h->st.h, &h->st.w, &h->st.kx, &h->st.ky, &h->st.kz, &h->st.p,

@@ -18,6 +18,11 @@ LIB_PATH = os.path.join(PKG, "libwq_router.so")
 
 _lib = None
 
+# typedef int (*wq_exchange_fn)(void* ctx, const void* d_send, const size_t* send_bytes, void* d_recv,
+#                               const size_t* recv_bytes, void* hip_stream)
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
+                               ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p)
+
 
 class WQError(RuntimeError):
     def __init__(self, code: int, msg: str):
@@ -82,6 +87,17 @@ def load_library(build_if_missing: bool = True):
         "wq_shard_ops": ([vp, vp, sz, u32, vp], i32),
         "wq_shard_messages_device": ([vp, vp, vp, vp, vp, vp, sz, u32, vp, vp], i32),
         "wq_route_records_device": ([vp, vp, sz, vp, vp, vp, sz, vp], i32),
+        "wq_hub_create": ([u32, ctypes.POINTER(vp)], i32),
+        "wq_hub_destroy": ([vp], i32),
+        "wq_shard_attach_hub": ([vp, vp, u32], i32),
+        "wq_rccl_unique_id": ([vp], i32),
+        "wq_shard_attach_rccl": ([vp, u32, u32, vp], i32),
+        "wq_shard_attach_exchange": ([vp, u32, u32, EXCHANGE_FN, vp], i32),
+        "wq_shard_detach": ([vp], i32),
+        "wq_shard_info": ([vp, ctypes.POINTER(u32), ctypes.POINTER(u32)], i32),
+        "wq_sharded_apply_ops": ([vp, vp, sz], i32),
+        "wq_sharded_route_tick_device": ([vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, ctypes.POINTER(sz)], i32),
+        "wq_sharded_copy_out": ([vp, vp, vp, vp, sz], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -278,6 +294,60 @@ class Router:
                                                      peers_ptr or None, msgs_ptr or None, capacity,
                                                      counters_ptr or None))
 
+    # ---- multi-GPU behind the ABI: this handle as one shard of G (include/wq_router.h) ----
+    def attach_hub(self, hub: "Hub", rank: int) -> None:
+        self._check(self.lib.wq_shard_attach_hub(self.h, hub.h, rank))
+        self._hub = hub  # keep it alive while attached
+
+    def attach_rccl(self, n_shards: int, rank: int, uid: bytes) -> None:
+        assert len(uid) == abi.RCCL_ID_BYTES
+        buf = ctypes.create_string_buffer(bytes(uid), abi.RCCL_ID_BYTES)
+        self._check(self.lib.wq_shard_attach_rccl(self.h, n_shards, rank, buf))
+
+    def attach_exchange(self, n_shards: int, rank: int, fn) -> None:
+        """fn(d_send, send_bytes[G], d_recv, recv_bytes[G], stream) -> None: the caller's all-to-all
+        (device pointers as ints, byte counts as lists). Exceptions count as failures."""
+        G = n_shards
+
+        def tramp(_ctx, send, sb, recv, rb, stream):
+            try:
+                fn(send or 0, [sb[i] for i in range(G)], recv or 0, [rb[i] for i in range(G)], stream or 0)
+                return 0
+            except Exception:  # noqa: BLE001 — reported through the C status
+                import traceback
+                traceback.print_exc()
+                return 1
+        self._xfn = EXCHANGE_FN(tramp)  # keep the trampoline alive
+        self._check(self.lib.wq_shard_attach_exchange(self.h, n_shards, rank, self._xfn, None))
+
+    def detach_shard(self) -> None:
+        self._check(self.lib.wq_shard_detach(self.h))
+
+    def shard_info(self):
+        g, r = ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self.lib.wq_shard_info(self.h, ctypes.byref(g), ctypes.byref(r)))
+        return g.value, r.value
+
+    def sharded_apply_ops(self, ops: np.ndarray) -> None:
+        """The tick's whole op stream (every shard gets the same); this shard keeps what it owns."""
+        ops = np.ascontiguousarray(ops, dtype=abi.OP_DTYPE)
+        self._check(self.lib.wq_sharded_apply_ops(self.h, _p(ops), len(ops)))
+
+    def sharded_route_device(self, pos_ptr, world_ptr, sender_ptr, repl_ptr, n_msgs, offsets_ptr, peers_ptr,
+                             msgs_ptr, capacity, keys_ptr=None):
+        """One collective sharded tick on this shard's ingested messages (device pointers).
+        Returns (rc, P): rc is WQ_OK or WQ_E_CAPACITY (then sharded_copy_out with room for P)."""
+        n = ctypes.c_size_t()
+        rc = self.lib.wq_sharded_route_tick_device(self.h, pos_ptr or None, keys_ptr or None, world_ptr or None,
+                                                   sender_ptr or None, repl_ptr or None, n_msgs, offsets_ptr,
+                                                   peers_ptr or None, msgs_ptr or None, capacity, ctypes.byref(n))
+        if rc not in (0, abi.WQ_E_CAPACITY):
+            self._check(rc)
+        return rc, n.value
+
+    def sharded_copy_out(self, offsets_ptr, peers_ptr, msgs_ptr, capacity) -> None:
+        self._check(self.lib.wq_sharded_copy_out(self.h, offsets_ptr, peers_ptr or None, msgs_ptr or None, capacity))
+
     # ---- C5 radius filter (include/wq_router.h) ----
     def set_peer_positions(self, pos) -> None:
         p = np.ascontiguousarray(pos, dtype=np.float64).reshape(-1, 3)
@@ -369,3 +439,37 @@ class Router:
         n = ctypes.c_uint64()
         self._check(self.lib.wq_profile_read(self.h, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
+
+
+class Hub:
+    """An in-process exchange for G router handles of one process (wq_hub_create)."""
+
+    def __init__(self, n_shards: int):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        rc = self.lib.wq_hub_create(n_shards, ctypes.byref(h))
+        if rc != 0:
+            raise WQError(rc, "wq_hub_create")
+        self.h = h
+        self.n_shards = n_shards
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.wq_hub_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def rccl_unique_id() -> bytes:
+    """wq_rccl_unique_id: the 128-byte communicator id rank 0 hands to every rank."""
+    lib = load_library()
+    buf = ctypes.create_string_buffer(abi.RCCL_ID_BYTES)
+    rc = lib.wq_rccl_unique_id(buf)
+    if rc != 0:
+        raise WQError(rc, "wq_rccl_unique_id (librccl not loadable?)")
+    return buf.raw
