@@ -41,7 +41,8 @@ def main():
         print(k)
         for c, v in sorted(means.items()):
             print(f"    {c:28s} {v:16.1f}   (n={len(cs[c])})")
-        if any(s in k for s in ("count_kernel", "tile_scan_kernel", "emit_kernel", "tick_kernel")) and not (
+        if any(s in k for s in ("count_kernel", "tile_scan_kernel", "tile_finish_kernel", "emit_kernel",
+                                "emit_heavy_kernel", "tick_kernel")) and not (
                 a.exclude and a.exclude in k):
             route[k] = means
     if a.json and route:

@@ -127,6 +127,9 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
         }
     }
 
+    // per-peer boxes (PeerBox) on and still valid: skip long-list searches they rule out
+    const bool boxes = !(DBG & 4) && tv.pbox && *tv.pbox_valid;
+
     // ---- B: rounds of two 16-byte loads per pending message ----
     const uint4* recs4 = reinterpret_cast<const uint4*>(tv.recs);
     uint4 c0[IPT], c1[IPT];
@@ -180,11 +183,12 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
                             } else if (cnt[i] <= (uint32_t)kInline) {  // inline peers from chunk 2 on
                                 st[i] = kStVerify;
                                 vc[i] = 2;
-                            } else {  // > kInline peers: binary search of the full list (rare in C2)
+                            } else if (!boxes || box_may_hold(tv, me, pk[i])) {
+                                // > kInline peers, the sender's box holds the cube: binary search
                                 const uint32_t* lp = tv.list + loff[i] + 1;
                                 lt[i] = lower_bound_dev(lp, cnt[i], me);
                                 has[i] = lt[i] < cnt[i] && lp[lt[i]] == me;
-                            }
+                            }  // else: outside the sender's box, certainly not subscribed
                         }
                     }
                 } else {

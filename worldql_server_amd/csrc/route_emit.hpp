@@ -277,10 +277,16 @@ __device__ __forceinline__ void emit_row(EmitRowSmem<STAGE>& sm, const TableView
 // descriptors: op[0..255] st, op[256..511] source, op[512..767] skipped index, om[0..255] kind.
 constexpr uint8_t kDirNone = 0, kDirInline = 1, kDirList = 2, kDirSelf = 3;
 
-template <int STAGE>
-__device__ __forceinline__ void direct_meta(EmitRowSmem<STAGE>& es, const EmitOut& out, uint32_t m, uint32_t e,
-                                            uint2 inf, uint32_t st) {
-    static_assert(STAGE >= 3 * kBlock, "the descriptors live in the image's LDS");
+// The descriptors' LDS on its own (the heavy-row emit kernel needs nothing else): 4 KB per block.
+struct DirectSmem {
+    alignas(16) uint32_t op[3 * kBlock];
+    uint8_t om[kBlock];
+};
+
+template <class SM>
+__device__ __forceinline__ void direct_meta(SM& es, const EmitOut& out, uint32_t m, uint32_t e, uint2 inf,
+                                            uint32_t st) {
+    static_assert(sizeof(es.op) >= 3 * kBlock * sizeof(uint32_t), "room for three descriptor arrays");
     const int tid = threadIdx.x;
     uint8_t kind = kDirNone;
     uint32_t src = 0, skip = kNone;
@@ -305,35 +311,43 @@ __device__ __forceinline__ void direct_meta(EmitRowSmem<STAGE>& es, const EmitOu
     es.om[tid] = kind;
 }
 
-template <int STAGE, int R>
-__device__ __forceinline__ void emit_direct(const EmitRowSmem<STAGE>& es, const TableView& tv, const EmitOut& out,
-                                            uint32_t m0, uint64_t g0, uint32_t T) {
-    // R: outputs per thread per pass, R loads in flight before the stores. 16 in the emit pass
-    // (C3: 2.0 -> 1.76 ms); the single-launch tick takes 4, since the kernel's register count,
-    // and so its residency, is set by its largest path (16 there costs C2 4 us)
+template <int R, class SM>
+__device__ __forceinline__ void emit_direct(const SM& es, const TableView& tv, const EmitOut& out, uint32_t m0,
+                                            uint64_t g0, uint32_t T) {
+    // R: outputs per thread per pass. The R binary searches run in lockstep (each of the 8 rounds
+    // issues R LDS reads, then waits once) and the peer loads are branch-free (one address select,
+    // R loads in flight): written as R independent loops with per-output branches, the compiler
+    // serialised them — 8 dependent LDS round trips per output, the emit's main cost on C3.
     const uint32_t* recs32 = reinterpret_cast<const uint32_t*>(tv.recs);
     for (uint32_t r0 = threadIdx.x; r0 < T; r0 += R * kBlock) {
-        uint32_t peer[R], msg[R];
+        uint32_t rr[R], lo[R];
 #pragma unroll
         for (int u = 0; u < R; ++u) {
             const uint32_t r = r0 + u * kBlock;
-            peer[u] = 0;
-            msg[u] = 0;
-            if (r >= T) continue;
-            uint32_t lo = 0, n = kBlock;  // last j with st[j] <= r (st[0] = 0)
+            rr[u] = r < T ? r : T - 1;  // clamped: a valid output, its store is masked below
+            lo[u] = 0;                  // last j with st[j] <= r (st[0] = 0)
+        }
 #pragma unroll
-            for (int it = 0; it < 8; ++it) {
-                const uint32_t half = n >> 1;
-                if (es.op[lo + half] <= r) lo += half;
-                n -= half;
-            }
-            const uint32_t k = r - es.op[lo], src = es.op[kBlock + lo], sk = es.op[2 * kBlock + lo];
+        for (int it = 0; it < 8; ++it) {
+            const uint32_t half = 128u >> it;
+            uint32_t t[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u) t[u] = es.op[lo[u] + half];
+#pragma unroll
+            for (int u = 0; u < R; ++u) lo[u] += t[u] <= rr[u] ? half : 0u;
+        }
+        uint32_t peer[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            const uint32_t j = lo[u];
+            const uint32_t k = rr[u] - es.op[j], src = es.op[kBlock + j], sk = es.op[2 * kBlock + j];
             const uint32_t idx = k + (k >= sk ? 1u : 0u);
-            const uint8_t kind = es.om[lo];
-            peer[u] = kind == kDirSelf ? src
-                      : kind == kDirList ? tv.list[(uint64_t)src + idx]
-                                         : recs32[(uint64_t)src * 32 + kInlineWord0 + idx];
-            msg[u] = m0 + lo;
+            const uint8_t kind = es.om[j];
+            const uint32_t* a = kind == kDirList     ? tv.list + ((uint64_t)src + idx)
+                                : kind == kDirInline ? recs32 + ((uint64_t)src * 32 + kInlineWord0 + idx)
+                                                     : tv.list;  // OnlySelf / none: a safe dummy load
+            peer[u] = *a;
+            if (kind == kDirSelf) peer[u] = src;
         }
 #pragma unroll
         for (int u = 0; u < R; ++u) {
@@ -341,7 +355,7 @@ __device__ __forceinline__ void emit_direct(const EmitRowSmem<STAGE>& es, const 
             const uint64_t o = g0 + r;
             if (r < T && o < out.capacity) {
                 out.peers[o] = peer[u];
-                if (out.msgs) out.msgs[o] = msg[u];
+                if (out.msgs) out.msgs[o] = m0 + lo[u];
             }
         }
     }
@@ -373,13 +387,44 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(EmitParams p) {
     if (m < p.M) p.offsets[m] = g + st;
     if (!p.peers) return;  // counts-only call: offsets are all that is asked for
     if (!RADIUS && T > (uint32_t)STAGE) {  // block-uniform: heavy fan-out, no windows
-        direct_meta<STAGE>(sm, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl}, m, e, inf, st);
+        direct_meta(sm, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl}, m, e, inf, st);
         lds_barrier();
-        emit_direct<STAGE, 16>(sm, p.t, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl}, m0, g, T);
+        emit_direct<16>(sm, p.t, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl}, m0, g, T);
         return;
     }
     emit_row<STAGE, U, RADIUS>(sm, p.t, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl}, m0, e, inf,
                                st, g, T);
+}
+
+// Pass 3 for heavy fan-out (wq_set_fanout_hint, C3): every row through emit_direct, whatever its
+// size, so the block needs only the 4 KB of descriptors instead of emit_kernel's 27 KB image — 8
+// blocks (32 waves) per CU instead of 5, i.e. more peer loads in flight. Offsets as emit_kernel.
+template <int R>
+__global__ __launch_bounds__(kBlock) void emit_heavy_kernel(EmitParams p) {
+    __shared__ DirectSmem sm;
+    __shared__ uint32_t wave_tot[kWaves];
+    __shared__ uint32_t part_tot[kWaves];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t m0 = blockIdx.x * kBlock;
+    const uint32_t m = m0 + tid;
+    const uint32_t e = m < p.M ? p.e[m] : 0u;
+    const uint2 inf = (p.peers && m < p.M) ? p.info[m] : make_uint2(0, kNone);
+    const uint32_t ct0 = (m0 / p.count_tile) * p.count_tile;
+    uint32_t g = p.tile_prefix[m0 / p.count_tile];
+    uint32_t part = 0;
+    for (uint32_t k = ct0 + tid; k < m0; k += kBlock) part += p.e[k];
+    part = (uint32_t)wave_sum_u64(part);
+    if (lane == 0) part_tot[wave] = part;
+    uint32_t T;
+    const uint32_t st = row_scan(e, wave_tot, &T);
+#pragma unroll
+    for (int u = 0; u < kWaves; ++u) g += part_tot[u];
+    if (m < p.M) p.offsets[m] = g + st;
+    if (!p.peers) return;
+    const EmitOut out{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl};
+    direct_meta(sm, out, m, e, inf, st);
+    lds_barrier();
+    emit_direct<R>(sm, p.t, out, m0, g, T);
 }
 
 }  // namespace wq

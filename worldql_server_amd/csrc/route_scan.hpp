@@ -1,10 +1,14 @@
 // route_scan.hpp — pass 2 of the tick: exclusive scan of the count pass's per-block totals.
 //
 // The count pass reduces e_m per block of 256*IPT messages; this single 1024-thread block scans
-// those few thousand totals (C2: 1,954) into tile_prefix[], writes offsets[M] = P and the
+// those few thousand totals (C2: 3,907; C3: 39,063) into tile_prefix[], writes offsets[M] = P and the
 // counters. The emit pass turns tile_prefix + a block-local scan into every CSR offset, so no
 // 1M-element global scan and no inter-block look-back is needed anywhere in the tick.
 #pragma once
+#include <cstring>  // rocPRIM's host code needs memset declared first
+
+#include <rocprim/rocprim.hpp>
+
 #include "route_common.hpp"
 
 namespace wq {
@@ -33,19 +37,38 @@ __device__ __forceinline__ uint64_t wave_incl_scan_add64(uint64_t v, int lane) {
     return v;
 }
 
+// One pass of the block covers 16,384 tiles (C3's 39,063 take three): wave w scans its 1,024-tile
+// chunk as 16 coalesced rows of 64 (row k = tiles chunk + 64k + lane) with a running carry, the
+// chunk totals are scanned across the 16 waves in LDS, and the rows are written with the wave's
+// offset. Every load and store is one contiguous 256-byte wave access (a per-thread run of 16
+// tiles instead made each load touch 64 separate segments: ~58 us on C3; one tile per thread and
+// pass took 39 passes: ~70 us).
+constexpr int kScanRows = 16;
+
 static __global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScanParams p) {
     __shared__ uint64_t s_wave[kScanWaves];
     __shared__ uint64_t s_F[kScanWaves];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint64_t carry = 0, F = 0;
-    for (uint32_t i = tid; i < p.n_tiles; i += kScanThreads) F += p.tile_F[i];
-    F = wave_sum_u64(F);
-    if (lane == 0) s_F[wave] = F;
-    for (uint32_t b = 0; b < p.n_tiles; b += kScanThreads) {
-        const uint32_t i = b + tid;
-        const uint64_t x = i < p.n_tiles ? p.tile_total[i] : 0u;
-        const uint64_t incl = wave_incl_scan_add64(x, lane);
-        if (lane == 63) s_wave[wave] = incl;
+    for (uint32_t base = 0; base < p.n_tiles; base += kScanThreads * kScanRows) {
+        const uint32_t c0 = base + (uint32_t)wave * (64 * kScanRows) + lane;
+        uint32_t v[kScanRows];
+#pragma unroll
+        for (int k = 0; k < kScanRows; ++k) {
+            const uint32_t i = c0 + 64u * k;
+            const bool in = i < p.n_tiles;
+            v[k] = in ? p.tile_total[i] : 0u;
+            F += in ? p.tile_F[i] : 0u;
+        }
+        uint64_t run = 0;  // wave-local exclusive prefix of each row element
+        uint64_t ex[kScanRows];
+#pragma unroll
+        for (int k = 0; k < kScanRows; ++k) {
+            const uint64_t incl = wave_incl_scan_add64(v[k], lane);
+            ex[k] = run + incl - v[k];
+            run += __shfl(incl, 63, 64);
+        }
+        if (lane == 0) s_wave[wave] = run;
         __syncthreads();
         uint64_t before = carry, tot = 0;
 #pragma unroll
@@ -54,10 +77,17 @@ static __global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScan
             if (u < wave) before += t;
             tot += t;
         }
-        if (i < p.n_tiles) p.tile_prefix[i] = (uint32_t)(before + incl - x);
+#pragma unroll
+        for (int k = 0; k < kScanRows; ++k) {
+            const uint32_t i = c0 + 64u * k;
+            if (i < p.n_tiles) p.tile_prefix[i] = (uint32_t)(before + ex[k]);
+        }
         carry += tot;
         __syncthreads();
     }
+    F = wave_sum_u64(F);
+    if (lane == 0) s_F[wave] = F;
+    __syncthreads();
     if (tid == 0) {
         uint64_t Ft = 0;
 #pragma unroll
@@ -69,6 +99,57 @@ static __global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScan
         // u32 CSR offsets cannot hold more than 2^32-1 pairs: error bit 2
         flag_route(p.cnt, p.health, P > 0xFFFFFFFFull ? 2u : 0u, P > p.capacity ? 1u : 0u);
     }
+}
+
+// Many tiles (C3: 39,063): one block cannot keep up (the single-block scan above took ~60-76 us
+// there whatever its load pattern), so the prefix is rocPRIM's single-pass decoupled look-back
+// scan over every CU and this kernel adds what tile_scan_kernel adds: F (candidates) by block
+// partial sums into the call's counters, P from the last tile, the overflow / error flags.
+static __global__ __launch_bounds__(kBlock) void tile_finish_kernel(TileScanParams p) {
+    __shared__ uint64_t s_F[kWaves];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint64_t F = 0;
+    for (uint32_t i = blockIdx.x * kBlock + tid; i < p.n_tiles; i += gridDim.x * kBlock) F += p.tile_F[i];
+    F = wave_sum_u64(F);
+    if (lane == 0) s_F[wave] = F;
+    lds_barrier();
+    if (tid == 0) {
+        uint64_t Fb = 0;
+#pragma unroll
+        for (int u = 0; u < kWaves; ++u) Fb += s_F[u];
+        atomicAdd(reinterpret_cast<unsigned long long*>(&p.cnt->n_candidates), (unsigned long long)Fb);
+    }
+    if (blockIdx.x == 0 && tid == 0) {
+        const uint32_t last = p.n_tiles - 1;
+        const uint64_t P = (uint64_t)p.tile_prefix[last] + p.tile_total[last];  // no u32 wrap below 2^32
+        p.offsets[p.M] = (uint32_t)P;
+        p.cnt->n_pairs = P;
+        flag_route(p.cnt, p.health, P > 0xFFFFFFFFull ? 2u : 0u, P > p.capacity ? 1u : 0u);
+    }
+}
+
+constexpr uint32_t kScanOneBlockMax = 8192;  // tiles: up to here the one-block scan is the faster
+
+// The tick's tile scan (n_tiles >= 1): one block for a few thousand tiles (C2: 3,907, ~5 us),
+// rocPRIM + tile_finish_kernel beyond. P must fit the u32 offsets either way (error bit 2 if not);
+// a tick of > 2^32 pairs wraps the prefix, which the error bit already reports.
+inline int launch_tile_scan(wq_router* h, const TileScanParams& sp) {
+    hipStream_t s = h->stream;
+    if (sp.n_tiles <= kScanOneBlockMax) {
+        hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, sp);
+        WQ_HIP(h, hipGetLastError());
+        return WQ_OK;
+    }
+    size_t bytes = 0;
+    WQ_HIP(h, rocprim::exclusive_scan(nullptr, bytes, sp.tile_total, sp.tile_prefix, 0u, (size_t)sp.n_tiles,
+                                      rocprim::plus<uint32_t>(), s));
+    WQ_ALLOC(h, h->rws.scan_tmp, bytes);
+    WQ_HIP(h, rocprim::exclusive_scan(h->rws.scan_tmp.p, bytes, sp.tile_total, sp.tile_prefix, 0u,
+                                      (size_t)sp.n_tiles, rocprim::plus<uint32_t>(), s));
+    const unsigned g = std::min<unsigned>(256u, (sp.n_tiles + kBlock * 8 - 1) / (kBlock * 8));
+    hipLaunchKernelGGL(tile_finish_kernel, dim3(g), dim3(kBlock), 0, s, sp);
+    WQ_HIP(h, hipGetLastError());
+    return WQ_OK;
 }
 
 }  // namespace wq

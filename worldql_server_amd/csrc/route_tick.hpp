@@ -238,7 +238,7 @@ __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
     // ---- 3. stage the block's outputs in LDS (if they fit) ----
     const bool fits = T <= (uint32_t)STAGE && p.out.peers;  // block-uniform
     if (fits) stage_image<STAGE>(sm.es, tv, p.out, m, e, inf, st, pc[0]);
-    else if (p.out.peers) direct_meta<STAGE>(sm.es, p.out, m, e, inf, st);
+    else if (p.out.peers) direct_meta(sm.es, p.out, m, e, inf, st);
 
     // ---- 4. look-back (wave 0), publish the inclusive prefix ----
     if (wave == 0) {
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
     if (m < p.in.M) p.offsets[m] = (uint32_t)(g0 + st);
     if (p.out.peers) {
         if (fits) copy_image_out<STAGE>(sm.es, p.out, m0, g0, T);
-        else emit_direct<STAGE, 4>(sm.es, tv, p.out, m0, g0, T);
+        else emit_direct<4>(sm.es, tv, p.out, m0, g0, T);
     }
     if (stamp) p.stamps[4 * b + 3] = __builtin_amdgcn_s_memrealtime();
 }

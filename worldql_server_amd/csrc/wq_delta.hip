@@ -66,7 +66,8 @@ __device__ __forceinline__ void op_key(const wq_op& o, double sf, int64_t si, in
 // be grouped by slot with a short radix sort. The caller guarantees free slots (load <= 1/2).
 __global__ void k_delta_events(const wq_op* __restrict__ ops, uint32_t n, double sf, int64_t si, Record* recs,
                                uint64_t rmask, int rshift, uint64_t hmask, uint64_t* pk, uint32_t* slot,
-                               uint32_t* peer, uint8_t* kind, uint64_t* sv, DeltaSummary* sum) {
+                               uint32_t* peer, uint8_t* kind, uint64_t* sv, DeltaSummary* sum, uint32_t* pbox,
+                               uint32_t n_pbox) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const wq_op o = ops[i];
@@ -91,6 +92,12 @@ __global__ void k_delta_events(const wq_op* __restrict__ ops, uint32_t n, double
             j = (j + 1) & rmask;
         }
         sl = (uint32_t)j;
+        // a subscribe widens its peer's box (PeerBox); a peer beyond the boxes switches them off
+        // until the next full build (the count pass then searches every long list)
+        if (pbox && o.kind == WQ_OP_SUBSCRIBE) {
+            if (o.peer < n_pbox) box_add(pbox + (uint64_t)kBoxWords * o.peer, p);
+            else atomicExch(pbox + (uint64_t)kBoxWords * n_pbox, 0u);
+        }
     }
     const uint32_t kd = o.kind == WQ_OP_SUBSCRIBE ? 1u : 0u;
     pk[i] = p;
@@ -832,7 +839,7 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     hipLaunchKernelGGL(k_delta_events, dim3(nb), dim3(kBlock), 0, s, h->cur_ops, n, (double)h->cube_size,
                        (int64_t)h->cube_size, t.recs.as<Record>(), t.rec_cap - 1, t.rec_shift, h->hash_mask,
                        d.pk.as<uint64_t>(), d.slot.as<uint32_t>(), d.peer.as<uint32_t>(), d.kind.as<uint8_t>(),
-                       d.sv.as<uint64_t>(), sum);
+                       d.sv.as<uint64_t>(), sum, t.n_pbox ? t.pbox.as<uint32_t>() : nullptr, t.n_pbox);
     DeltaTable tb{t.recs.as<Record>(), t.rclaim.as<uint32_t>(), t.rec_cap - 1, t.rec_shift, h->hash_mask,
                   t.list.as<uint32_t>()};
     int rc = delta_plan_groups(h, n, sum);

@@ -193,7 +193,50 @@ struct TableView {
     const double* ppos;
     uint32_t n_ppos;
     double r2;
+    // per-peer boxes of the record cubes each peer is subscribed to (PeerBox); nullptr: none
+    const uint32_t* pbox;
+    uint32_t n_pbox;            // peers [0, n_pbox) have a box; others hold no record cube
+    const uint32_t* pbox_valid; // device word: 0 once an update could not keep the boxes
 };
+
+// ---- per-peer boxes: a fast "certainly not subscribed" for long lists ---------------------
+// For every peer, the world and the per-axis [min, max] of the packed axes (pack_key) of the
+// record cubes it is subscribed to: 8 words {world, ax_min, ay_min, az_min, ax_max, ay_max,
+// az_max, -}. A message whose cube lies outside its sender's box cannot have the sender among
+// the cube's peers, so the count pass skips the binary search of a long list (C3: random senders
+// in hotspot cubes of ~500 peers — ~0.8 extra line per message). Boxes only grow: subscribes
+// widen them (builds and incremental updates); unsubscribes and disconnects leave them wider
+// than needed, which is still exact ("maybe" -> the search decides). kBoxMulti: the peer holds
+// record cubes in more than one world -> always search.
+constexpr uint32_t kBoxEmpty = 0xFFFFFFFFu;
+constexpr uint32_t kBoxMulti = 0xFFFFFFFEu;  // never a packed world (those are < 1023)
+constexpr int kBoxWords = 8;
+
+__device__ __forceinline__ void box_add(uint32_t* box, uint64_t pk) {
+    const uint32_t w = (uint32_t)(pk >> 54) - 1u;
+    const uint32_t ax = (uint32_t)(pk >> 36) & 0x3FFFFu, ay = (uint32_t)(pk >> 18) & 0x3FFFFu,
+                   az = (uint32_t)pk & 0x3FFFFu;
+    const uint32_t w0 = atomicCAS(&box[0], kBoxEmpty, w);
+    if (w0 != kBoxEmpty && w0 != w) atomicExch(&box[0], kBoxMulti);
+    atomicMin(&box[1], ax);
+    atomicMin(&box[2], ay);
+    atomicMin(&box[3], az);
+    atomicMax(&box[4], ax);
+    atomicMax(&box[5], ay);
+    atomicMax(&box[6], az);
+}
+
+// false: `peer` is certainly not subscribed to the record cube pk.
+__device__ __forceinline__ bool box_may_hold(const TableView& t, uint32_t peer, uint64_t pk) {
+    if (peer >= t.n_pbox) return false;
+    const uint4 a = *reinterpret_cast<const uint4*>(t.pbox + (uint64_t)kBoxWords * peer);
+    const uint4 b = *reinterpret_cast<const uint4*>(t.pbox + (uint64_t)kBoxWords * peer + 4);
+    if (a.x == kBoxMulti) return true;
+    const uint32_t w = (uint32_t)(pk >> 54) - 1u;
+    const uint32_t ax = (uint32_t)(pk >> 36) & 0x3FFFFu, ay = (uint32_t)(pk >> 18) & 0x3FFFFu,
+                   az = (uint32_t)pk & 0x3FFFFu;
+    return a.x == w && ax >= a.y && ay >= a.z && az >= a.w && ax <= b.x && ay <= b.y && az <= b.z;
+}
 
 // C5: is peer p within the radius of message position (mx, my, mz)? f64, left to right, no FMA
 // (this file is compiled with contraction off), a peer without a position never is.

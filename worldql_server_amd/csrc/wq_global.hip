@@ -204,8 +204,7 @@ int launch_route_global(wq_router* h, const uint32_t* d_world, const uint32_t* d
     sp.capacity = capacity;
     sp.cnt = cur;
     sp.health = route_health(h);
-    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, sp);
-    WQ_HIP(h, hipGetLastError());
+    if ((rc = launch_tile_scan(h, sp))) return rc;
     hipLaunchKernelGGL(global_offsets_kernel, dim3(n_tiles), dim3(kBlock), 0, s, gp);
     if (gp.peers) hipLaunchKernelGGL(global_copy_kernel, dim3(kCopyGrid), dim3(kBlock), 0, s, gp);
     WQ_HIP(h, hipGetLastError());

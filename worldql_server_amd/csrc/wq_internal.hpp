@@ -61,6 +61,9 @@ struct Table {
     // build's dense region when they outgrow their capacity) and record slots in use (including
     // records whose cube emptied: they keep their key, count 0)
     uint64_t list_used = 0, list_cap = 0, n_recs = 0;
+    // per-peer boxes (wq_device.hpp PeerBox): kBoxWords words per peer, then the valid word
+    DevBuf pbox;
+    uint32_t n_pbox = 0;
 };
 
 // Scratch of the incremental update (wq_delta.hip).
@@ -85,6 +88,7 @@ struct RouteWs {
     DevBuf tiles;  // u32[2 * n_count_blocks]: block totals, then their exclusive prefix
     DevBuf spill;  // per-block output images of the count+spill tick (route config 7)
     DevBuf agg;    // u64[2 * blocks]: look-back and candidate granules of the single-launch tick
+    DevBuf scan_tmp;  // rocPRIM temporary storage of the many-tile scan (launch_tile_scan)
     uint64_t agg_zeroed = 0;
     uint64_t* stamps = nullptr;  // wq_debug_set_timeline
     uint64_t calls = 0;
@@ -157,6 +161,9 @@ inline TableView table_view(const wq_router* h) {
     v.ppos = h->ppos.as<double>();
     v.n_ppos = (uint32_t)h->n_ppos;
     v.r2 = h->radius > 0.0 ? h->radius * h->radius : -1.0;
+    v.n_pbox = h->tab.n_pbox;
+    v.pbox = h->tab.n_pbox ? h->tab.pbox.as<uint32_t>() : nullptr;
+    v.pbox_valid = h->tab.n_pbox ? h->tab.pbox.as<uint32_t>() + (uint64_t)kBoxWords * h->tab.n_pbox : nullptr;
     return v;
 }
 // Sticky {error OR, overflow OR} words of every route / global call since the last

@@ -38,6 +38,9 @@ struct Cfg {
     void (*tick)(const TickParams&, hipStream_t, unsigned);
     // count+spill / tile_scan / copy (route_spill.hpp): image positions per block, or 0
     int spill_stage;
+    // three launches: 0 = emit_kernel (windowed image, heavy rows through emit_direct), or the
+    // outputs in flight per thread of emit_heavy_kernel (every row through emit_direct, 4 KB LDS)
+    int emit_heavy;
 };
 
 template <int IPT, int MINW, bool FULL = false>
@@ -56,9 +59,10 @@ void launch_tick(const TickParams& p, hipStream_t s, unsigned grid) {
         hipLaunchKernelGGL((tick_kernel<false, STAGE, U>), dim3(grid), dim3(kBlock), 0, s, p);
 }
 
-#define WQ_CFG3(cipt, minw, stage) {kBlock * cipt, &launch_count<cipt, minw>, stage, 0, nullptr, 0}
-#define WQ_CFG1(stage, u) {kBlock, &launch_count<1, 8>, 4096, stage, &launch_tick<stage, u>, 0}
-#define WQ_CFGS(stage) {kBlock, &launch_count<1, 8>, 4096, 0, nullptr, stage}
+#define WQ_CFG3(cipt, minw, stage) {kBlock * cipt, &launch_count<cipt, minw>, stage, 0, nullptr, 0, 0}
+#define WQ_CFG3H(r) {kBlock, &launch_count<1, 8>, 4096 + 2, 0, nullptr, 0, r}
+#define WQ_CFG1(stage, u) {kBlock, &launch_count<1, 8>, 4096, stage, &launch_tick<stage, u>, 0, 0}
+#define WQ_CFGS(stage) {kBlock, &launch_count<1, 8>, 4096, 0, nullptr, stage, 0}
 // Three launches: count (messages per lane, min waves per SIMD) / tile_scan / emit. One launch:
 // messages per block; its three-launch fallback (too many blocks to be resident) is count 4/2.
 const Cfg kCfgs[] = {
@@ -70,12 +74,15 @@ const Cfg kCfgs[] = {
     WQ_CFG1(3072, 2),         // 5: 21.6 KB LDS -> 7 blocks per CU (65.6 us)
     WQ_CFG1(2560, 2),         // 6: C2 blocks overflow the image (78 us)
     WQ_CFGS(kSpillStage),     // 7: count+spill / tile_scan / copy, no block waits on another
+    WQ_CFG3H(16),             // 8: three launches, emit_heavy_kernel (16 outputs in flight per thread)
+    WQ_CFG3H(8),              // 9: ... 8 in flight
 };
 #undef WQ_CFG1
 #undef WQ_CFGS
 #undef WQ_CFG3
+#undef WQ_CFG3H
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
-constexpr int kCfgHeavy = 1;  // the default shape under wq_set_fanout_hint >= WQ_HEAVY_FANOUT
+constexpr int kCfgHeavy = 8;  // the default shape under wq_set_fanout_hint >= WQ_HEAVY_FANOUT (emit_heavy_kernel)
 
 }  // namespace
 
@@ -198,8 +205,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         tsp.capacity = capacity;
         tsp.cnt = cur;
         tsp.health = route_health(h);
-        hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, tsp);
-        WQ_HIP(h, hipGetLastError());
+        if (int rc = launch_tile_scan(h, tsp)) return rc;
         hipLaunchKernelGGL((spill_copy_kernel<kSpillStage, 2>), dim3(nb), dim3(kBlock), 0, s, sp);
         WQ_HIP(h, hipGetLastError());
         if (pr.enabled) {
@@ -245,8 +251,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     sp.capacity = capacity;
     sp.cnt = cur;
     sp.health = route_health(h);
-    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, sp);
-    WQ_HIP(h, hipGetLastError());
+    if (int rc = launch_tile_scan(h, sp)) return rc;
 
     EmitParams ep;
     ep.sender = d_sender;
@@ -265,6 +270,10 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     const dim3 eg((unsigned)((M + kBlock - 1) / kBlock));
     if (radius)
         hipLaunchKernelGGL((emit_kernel<4096, 2, true>), eg, dim3(kBlock), 0, s, ep);
+    else if (cfg.emit_heavy == 16)
+        hipLaunchKernelGGL((emit_heavy_kernel<16>), eg, dim3(kBlock), 0, s, ep);
+    else if (cfg.emit_heavy == 8)
+        hipLaunchKernelGGL((emit_heavy_kernel<8>), eg, dim3(kBlock), 0, s, ep);
     else if (cfg.emit_stage == 4096 + 2)
         hipLaunchKernelGGL((emit_kernel<4096, 2>), eg, dim3(kBlock), 0, s, ep);
     else if (cfg.emit_stage == 4096 + 4)

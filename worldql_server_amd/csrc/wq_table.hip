@@ -182,6 +182,31 @@ __global__ void k_insert_cubes(EvView st, const uint32_t* __restrict__ cube_star
     slots[s] = r;
 }
 
+__global__ void k_max_peer(const uint32_t* __restrict__ p, uint64_t n, uint32_t* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) atomicMax(out, p[i]);
+}
+
+__global__ void k_box_init(uint32_t* box, uint32_t n_peers) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n_peers) {
+        uint32_t* b = box + (uint64_t)kBoxWords * i;
+        b[0] = kBoxEmpty;
+        b[1] = b[2] = b[3] = 0xFFFFFFFFu;
+        b[4] = b[5] = b[6] = 0u;
+        b[7] = 0u;
+    }
+    if (i == 0) box[(uint64_t)kBoxWords * n_peers] = 1u;  // valid
+}
+
+// Every live entry of a record cube widens its peer's box.
+__global__ void k_box_build(EvView st, uint64_t n, double sf, uint32_t* box) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    uint64_t pk;
+    if (pack_key(st.w[i], st.kx[i], st.ky[i], st.kz[i], sf, &pk)) box_add(box + (uint64_t)kBoxWords * st.p[i], pk);
+}
+
 __global__ void k_any_keys(const uint32_t* __restrict__ w, const uint32_t* __restrict__ p, uint64_t n,
                            uint64_t* out) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -429,6 +454,25 @@ int table_rebuild_derived(wq_router* h) {
                            t.rclaim.as<uint32_t>(), t.recs.as<Record>(),
                            rcap - 1, t.rec_shift, t.claim.as<uint32_t>(), t.slots.as<Slot>(), cap - 1, t.shift,
                            h->hash_mask, (double)h->cube_size);
+    // per-peer boxes (PeerBox, wq_device.hpp): room for 25% more peer ids than the build has, so
+    // incremental subscribes of new peers keep them; one beyond that switches them off
+    t.n_pbox = 0;
+    if (S) {
+        uint32_t* mx = h->small.as<uint32_t>();
+        WQ_HIP(h, hipMemsetAsync(mx, 0, 4, s));
+        hipLaunchKernelGGL(k_max_peer, dim3(grid_for(S)), dim3(kBlock), 0, s, h->st.p.as<uint32_t>(), S, mx);
+        uint32_t max_peer = 0;
+        if ((rc = read_u32(h, mx, 0, &max_peer))) return rc;
+        const uint64_t np = (uint64_t)max_peer + 1, cap = np + np / 4 + 1024;
+        if (cap < 0xFFFFFFF0ull) {
+            WQ_ALLOC(h, t.pbox, (cap * kBoxWords + 1) * 4);
+            hipLaunchKernelGGL(k_box_init, dim3(grid_for(cap)), dim3(kBlock), 0, s, t.pbox.as<uint32_t>(),
+                               (uint32_t)cap);
+            hipLaunchKernelGGL(k_box_build, dim3(grid_for(S)), dim3(kBlock), 0, s, st, S, (double)h->cube_size,
+                               t.pbox.as<uint32_t>());
+            t.n_pbox = (uint32_t)cap;
+        }
+    }
     t.n_cubes = n_cubes;
     t.n_recs = n_cubes;
     t.list_used = list_words;
