@@ -43,6 +43,9 @@ def parse():
                     help="default: the headline, C3 (north_star's 1M peers / 10M messages per tick) with the C2 "
                          "line nested under extra.c2 at N = 1; c1..c5 = one SURVEY.md §8(d) config alone")
     ap.add_argument("--no-extra", action="store_true", help="headline only (skip the nested C2 line)")
+    ap.add_argument("--c2-world", type=int, default=0, help="C2 in this world id (>= 1023: the wide-key path)")
+    ap.add_argument("--c2-shift", type=float, default=0.0,
+                    help="C2 translated by this much on every axis (e.g. 2.5e7: Minecraft-scale coordinates)")
     ap.add_argument("--steps", type=int, default=None, help="timed ticks (default c3/c5 10, c4 20, c1/c2 50)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed ticks (default 10; c3/c4/c5 2)")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink C2 (tests only; 1.0 = the headline)")
@@ -111,11 +114,16 @@ def roofline(B: int, tick_s: float, kernel: str, traffic=None, event_us=None) ->
     return out
 
 
-def shard_workload(rank: int, scale: float = 1.0):
+def shard_workload(rank: int, scale: float = 1.0, world: int = 0, shift: float = 0.0):
     """World-sharded weak scaling: rank r owns world r (its own peers and its own tick of
-    messages); no message crosses ranks, so there is no exchange step."""
+    messages); no message crosses ranks, so there is no exchange step.
+    world / shift move the C2 box to another world id / far from the origin (same fan-out)."""
     from worldql_server_amd import synth
-    return synth.config_c2(scale=scale, world_offset=rank)
+    w = synth.config_c2(scale=scale, world_offset=world + rank)
+    if shift:
+        w.pos += shift
+        w.ops["pos"] += shift
+    return w
 
 
 def cube_workload(rank: int, world_size: int, scale: float = 1.0):
@@ -250,7 +258,7 @@ def run_c2(a, rank, world_size, local_rank, dev) -> dict:
     from worldql_server_amd import abi
     from worldql_server_amd.router import Router
 
-    w = shard_workload(rank, a.scale)
+    w = shard_workload(rank, a.scale, a.c2_world, a.c2_shift)
     M = len(w.world)
     r = Router(w.cube_size, local_rank)
     stream = torch.cuda.Stream(device=dev)  # a real stream object: its handle is never the NULL stream
@@ -326,7 +334,9 @@ def run_c2(a, rank, world_size, local_rank, dev) -> dict:
         "data": "synthetic (splitmix64, SURVEY.md §8(d) C2 generator)",
         "config": {
             "workload": "C2: 1 world/GPU, 100k peers x 3x3x3 cubes, 1M LocalMessages/tick, U[-512,512)^3, "
-                        "cube_size 16, ExceptSelf" + ("" if a.scale == 1.0 else f" (scaled {a.scale})"),
+                        "cube_size 16, ExceptSelf" + ("" if a.scale == 1.0 else f" (scaled {a.scale})")
+                        + (f", world id {a.c2_world}" if a.c2_world else "")
+                        + (f", box translated by {a.c2_shift:g} per axis" if a.c2_shift else ""),
             "messages_per_tick": M, "peers": w.n_peers, "subscriptions": int(st["n_entries"]),
             "cubes": int(st["n_cubes"]), "pairs_per_tick": P, "candidates_per_tick": F,
             "parallelism": f"world-sharded x{world_size}", "table_build_s": round(build_s, 3),

@@ -119,15 +119,17 @@ def test_c5_full_tick_radius_exact_vs_oracle():
 def test_large_worlds_and_minecraft_scale_coordinates():
     """World ids >= 1023 (up to 2^32 - 2) and coordinates out to +-3e7 (cube_area.rs:23-44 takes
     any f64; world_map.rs:31-36 creates worlds without bound), mixed with small keys, raw keys at
-    the i64 limits and the 2^17-cube boundary of the packed record key."""
+    the i64 limits and the boundaries of the 96-bit packed record key (2^23 cubes per axis, world
+    ids below 2^24 - 1; beyond them the slot table)."""
     rng = np.random.default_rng(5)
-    worlds = np.array([0, 1022, 1023, 4096, 0x7FFFFFFF, 0xFFFFFFFE], np.uint32)
+    worlds = np.array([0, 1022, 1023, 4096, 0xFFFFFD, 0xFFFFFE, 0xFFFFFF, 0x7FFFFFFF, 0xFFFFFFFE], np.uint32)
     n_peers = 3000
     peer_w = worlds[rng.integers(0, len(worlds), n_peers)]
     scale = np.where(rng.random(n_peers) < 0.5, 3e7, 64.0)
     ppos = rng.uniform(-1, 1, (n_peers, 3)) * scale[:, None]
-    edge = 131072.0 * 16.0  # 2^17 cubes of 16
-    ppos[:200] = rng.choice([edge - 8, edge + 8, -edge - 8, -edge + 8, edge, -edge], (200, 3))
+    edge = 8388608.0 * 16.0  # 2^23 cubes of 16: the packed axis range
+    small = 131072.0 * 16.0  # 2^17 cubes: round 1's packed range
+    ppos[:200] = rng.choice([edge - 8, edge + 8, -edge - 8, -edge + 8, edge, -edge, small, -small - 8], (200, 3))
     ops = synth_ext._neighbourhood_ops(peer_w, ppos, 16)
     raw = abi.ops_array(np.full(4, 4096, np.uint32), np.arange(4), np.zeros(4, np.uint8),
                         key=[[2**63 - 1, 0, 16], [-2**63, -2**63, -2**63], [edge, edge, edge], [5, 6, 7]])
@@ -135,6 +137,27 @@ def test_large_worlds_and_minecraft_scale_coordinates():
     r, o = _router(), orc.COracle(16)
     r.apply_ops(ops)
     o.apply_ops(ops)
+    assert r.stats()["n_entries"] == o.counts()[0]
+    # an incremental batch on the wide keys (new cubes claimed by the delta path, moves out of old
+    # ones) and a REMOVE_PEER, before routing
+    def move(mv):
+        ppos_new = ppos[mv] + rng.uniform(-400, 400, (len(mv), 3))
+        delta = abi.concat_ops([
+            synth_ext._neighbourhood_ops(peer_w[mv], ppos[mv], 16, peers=mv, kind=abi.OP_UNSUBSCRIBE),
+            synth_ext._neighbourhood_ops(peer_w[mv], ppos_new, 16, peers=mv)])
+        ppos[mv] = ppos_new
+        r.apply_ops(delta)
+        o.apply_ops(delta)
+        assert r.stats()["n_entries"] == o.counts()[0]
+
+    packed = (peer_w < 0xFFFFFF) & (np.abs(ppos).max(1) < edge - 1000)
+    inc, fb = r.update_counts()
+    move(np.flatnonzero(packed)[:300].astype(np.uint32))  # packed keys only: the delta path
+    assert r.update_counts() == (inc + 1, fb)
+    move(np.arange(0, 300, dtype=np.uint32))  # keys beyond the packed range: the rebuild
+    assert r.update_counts() == (inc + 1, fb + 1)
+    r.remove_peers([7])
+    o.remove_peer(7)
     assert r.stats()["n_entries"] == o.counts()[0]
     M = 60_000
     src = rng.integers(0, n_peers, M)

@@ -81,7 +81,7 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
         in_c[i][2] = src[3ull * mm + 2];
     }
     uint64_t pk[IPT];
-    uint32_t sl[IPT], st[IPT];
+    uint32_t ext[IPT], sl[IPT], st[IPT];
     bool via_rec[IPT];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
@@ -99,10 +99,11 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
             z = coord_clamp_dev(__longlong_as_double((long long)in_c[i][2]), tv.sf, in.si);
         }
         pk[i] = 0;
-        const bool reg = pack_key(w, x, y, z, tv.sf, &pk[i]);
+        ext[i] = 0;
+        const bool reg = pack_key(w, x, y, z, tv.sf, &pk[i], &ext[i]);
         // lanes with nothing to probe read a dummy line spread by message index (never one shared
         // line: a chip-wide hot line serialises on its L2 channel)
-        sl[i] = reg ? (uint32_t)slot_of(rec_hash(pk[i]) & tv.hash_mask, tv.rec_shift)
+        sl[i] = reg ? (uint32_t)slot_of(rec_hash(pk[i], ext[i]) & tv.hash_mask, tv.rec_shift)
                     : (m & (uint32_t)tv.rec_mask);
         via_rec[i] = valid && reg;
         st[i] = via_rec[i] ? kStProbe : kStDone;
@@ -143,7 +144,7 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
             for (int q = 0; q < 6; ++q) pc[i][q] = recs4[(uint64_t)sl[i] * 8 + 2 + q];
     }
     uint32_t cnt[IPT], loff[IPT], lt[IPT], vc[IPT];
-    bool has[IPT];
+    bool has[IPT], srch[IPT];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
         cnt[i] = 0;
@@ -151,6 +152,7 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
         lt[i] = 0;
         vc[i] = 0;
         has[i] = false;
+        srch[i] = false;
     }
     for (;;) {
         bool pending = false;
@@ -159,8 +161,9 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
             const uint32_t me = in_me[i];
             if (st[i] == kStProbe) {
                 const uint64_t key = ((uint64_t)c0[i].y << 32) | c0[i].x;
-                if (key == pk[i] || key == 0) {  // found, or an empty slot: the cube has no peers
-                    cnt[i] = key ? c0[i].z : 0u;
+                const bool empty = c1[i].w == 0;  // ext == 0: an empty slot, the cube has no peers
+                if (empty || (key == pk[i] && c1[i].w == ext[i])) {
+                    cnt[i] = empty ? 0u : c0[i].z;
                     loff[i] = c0[i].w;
                     st[i] = kStDone;
                     if (cnt[i] && in_rp[i] != WQ_REPL_INCLUDING_SELF) {
@@ -183,12 +186,9 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
                             } else if (cnt[i] <= (uint32_t)kInline) {  // inline peers from chunk 2 on
                                 st[i] = kStVerify;
                                 vc[i] = 2;
-                            } else if (!boxes || box_may_hold(tv, me, pk[i])) {
-                                // > kInline peers, the sender's box holds the cube: binary search
-                                const uint32_t* lp = tv.list + loff[i] + 1;
-                                lt[i] = lower_bound_dev(lp, cnt[i], me);
-                                has[i] = lt[i] < cnt[i] && lp[lt[i]] == me;
-                            }  // else: outside the sender's box, certainly not subscribed
+                            } else {
+                                srch[i] = true;  // > kInline peers: after the probe loop
+                            }
                         }
                     }
                 } else {
@@ -222,6 +222,17 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
             if (FULL && st[i] == kStProbe)
 #pragma unroll
                 for (int c = 0; c < 6; ++c) pc[i][c] = recs4[(uint64_t)sl[i] * 8 + 2 + c];
+        }
+    }
+    // long lists (> kInline peers) whose signature admits the sender: unless the sender's box
+    // rules the cube out, a binary search — outside the probe loop, whose record lines are dead
+    // by now (fewer live registers there)
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+        if (srch[i] && (!boxes || box_may_hold(tv, in_me[i], pk[i], ext[i]))) {
+            const uint32_t* lp = tv.list + loff[i] + 1;
+            lt[i] = lower_bound_dev(lp, cnt[i], in_me[i]);
+            has[i] = lt[i] < cnt[i] && lp[lt[i]] == in_me[i];
         }
     }
 

@@ -49,7 +49,8 @@ __global__ __launch_bounds__(kBlock) void count_radius_kernel(CountParams p) {
     const int64_t ky = coord_clamp_dev(my, tv.sf, p.in.si);
     const int64_t kz = coord_clamp_dev(mz, tv.sf, p.in.si);
     uint64_t pk = 0;
-    const bool reg = pack_key(w, kx, ky, kz, tv.sf, &pk);
+    uint32_t ext = 0;
+    const bool reg = pack_key(w, kx, ky, kz, tv.sf, &pk, &ext);
     uint32_t e = 0, cnt = 0;
     uint2 info = make_uint2(0, kNone);
     if (valid && !reg) {  // full-key slot table: the list is walked from `list`
@@ -63,26 +64,27 @@ __global__ __launch_bounds__(kBlock) void count_radius_kernel(CountParams p) {
     }
     // the whole record line: header, signature, 24 inline peers
     const uint4* recs4 = reinterpret_cast<const uint4*>(tv.recs);
-    uint32_t sl = reg ? (uint32_t)slot_of(rec_hash(pk) & tv.hash_mask, tv.rec_shift) : (m & (uint32_t)tv.rec_mask);
-    uint4 c0, pc[6];
+    uint32_t sl = reg ? (uint32_t)slot_of(rec_hash(pk, ext) & tv.hash_mask, tv.rec_shift) : (m & (uint32_t)tv.rec_mask);
+    uint4 c0, c1, pc[6];
     c0 = recs4[(uint64_t)sl * 8];
+    c1 = recs4[(uint64_t)sl * 8 + 1];
 #pragma unroll
     for (int k = 0; k < 6; ++k) pc[k] = recs4[(uint64_t)sl * 8 + 2 + k];
     bool pend = valid && reg;
     for (;;) {
         const uint64_t key = ((uint64_t)c0.y << 32) | c0.x;
-        const bool coll = pend && key != 0 && key != pk;
+        const bool coll = pend && c1.w != 0 && (key != pk || c1.w != ext);  // another cube's record
         if (!__any(coll)) break;
         if (coll) {
             sl = (sl + 1) & (uint32_t)tv.rec_mask;
             c0 = recs4[(uint64_t)sl * 8];
+            c1 = recs4[(uint64_t)sl * 8 + 1];
 #pragma unroll
             for (int k = 0; k < 6; ++k) pc[k] = recs4[(uint64_t)sl * 8 + 2 + k];
         }
     }
     if (pend) {
-        const uint64_t key = ((uint64_t)c0.y << 32) | c0.x;
-        cnt = key ? c0.z : 0u;
+        cnt = c1.w ? c0.z : 0u;  // ext == 0: empty, no peers
         const uint32_t loff = c0.w;
         if (cnt > (uint32_t)kInline) {
             e = count_list_radius(tv, tv.list + loff + 1, cnt, mx, my, mz, rp, me);

@@ -16,7 +16,7 @@
 //            (in place, or relocated past the used part of `list` with 50% headroom) and the whole
 //            record line (count, offset, capacity, Bloom signature, inline peers)
 // Cubes beyond the group bounds (old count + ops > 128) send the batch to the per-lane path:
-// sort by (pk, peer), one lane per cube, in-place forward compaction then backward merge.
+// sort by (slot, peer), one lane per cube, in-place forward compaction then backward merge.
 // A cube that empties keeps its record (count 0, key kept), so every probe sequence stays intact.
 // The sorted state `st` and the any-keys are left stale and regenerated from the records only
 // when something needs them (table_materialize / table_ensure_any). A batch falls back to the full
@@ -64,43 +64,61 @@ __device__ __forceinline__ void op_key(const wq_op& o, double sf, int64_t si, in
 // Per op: packed key, and the record slot of its cube — a cube the table does not hold yet gets
 // its record here (key claimed by compare-and-swap on the probe path, count 0), so the batch can
 // be grouped by slot with a short radix sort. The caller guarantees free slots (load <= 1/2).
+// Claim words (rclaim, one per record slot): 0 free, kClaiming while an op writes a new cube's key,
+// otherwise the slot holds a key — builds write the cube index + 2 (< 2^31), a delta batch writes
+// its tag (kBatchTag | batch number). The 96-bit key spans two words of the record, so a slot is
+// claimed through its claim word: the winner writes the key, then publishes the tag (release). A
+// key published before this launch is read with plain loads; only a slot tagged by this very
+// batch takes an acquire fence first (the one case where the key may still be in flight). An op
+// that finds a slot being claimed looks again (the winner's wave progresses meanwhile).
+constexpr uint32_t kClaiming = 1u, kBatchTag = 0x80000000u;
+
 __global__ void k_delta_events(const wq_op* __restrict__ ops, uint32_t n, double sf, int64_t si, Record* recs,
-                               uint64_t rmask, int rshift, uint64_t hmask, uint64_t* pk, uint32_t* slot,
-                               uint32_t* peer, uint8_t* kind, uint64_t* sv, DeltaSummary* sum, uint32_t* pbox,
-                               uint32_t n_pbox) {
+                               uint32_t* rclaim, uint32_t tag, uint64_t rmask, int rshift, uint64_t hmask,
+                               uint32_t* slot, uint32_t* peer, uint8_t* kind, uint64_t* sv, DeltaSummary* sum) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const wq_op o = ops[i];
     int64_t k[3];
     op_key(o, sf, si, k);
     uint64_t p = 0;
+    uint32_t x = 0;
     uint32_t sl = 0;  // ops without a record (the batch then falls back): slot 0, an in-bounds dummy
     if (o.kind > WQ_OP_UNSUBSCRIBE || o.world == WQ_WORLD_INVALID) {
         atomicOr(&sum->irregular, 2u);  // bad op
-    } else if (!pack_key(o.world, k[0], k[1], k[2], sf, &p)) {
+    } else if (!pack_key(o.world, k[0], k[1], k[2], sf, &p, &x)) {
         atomicOr(&sum->irregular, 1u);
     } else {
-        uint64_t j = slot_of(rec_hash(p) & hmask, rshift);
+        uint64_t j = slot_of(rec_hash(p, x) & hmask, rshift);
         for (;;) {
-            unsigned long long* kp = reinterpret_cast<unsigned long long*>(&recs[j].pk);
-            unsigned long long cur = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (cur == 0) {
-                cur = atomicCAS(kp, 0ull, (unsigned long long)p);
-                if (cur == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&sum->new_recs), 1ull);
+            uint32_t c = __hip_atomic_load(&rclaim[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c == 0) {
+                c = atomicCAS(&rclaim[j], 0u, kClaiming);
+                if (c == 0) {  // won: a new cube (count 0) with this key
+                    recs[j].pk = p;
+                    recs[j].ext = x;
+                    __hip_atomic_store(&rclaim[j], tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&sum->new_recs), 1ull);
+                    break;
+                }
             }
-            if (cur == 0 || cur == p) break;
+            if (c == kClaiming) continue;  // being claimed: look again
+            uint64_t rp;
+            uint32_t rx;
+            if (c == tag) {  // claimed by this batch: order the key loads after the tag
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                rp = __hip_atomic_load(&recs[j].pk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                rx = __hip_atomic_load(&recs[j].ext, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                rp = recs[j].pk;
+                rx = recs[j].ext;
+            }
+            if (rp == p && rx == x) break;
             j = (j + 1) & rmask;
         }
         sl = (uint32_t)j;
-        // a subscribe widens its peer's box (PeerBox); a peer beyond the boxes switches them off
-        // until the next full build (the count pass then searches every long list)
-        if (pbox && o.kind == WQ_OP_SUBSCRIBE) {
-            if (o.peer < n_pbox) box_add(pbox + (uint64_t)kBoxWords * o.peer, p);
-            else atomicExch(pbox + (uint64_t)kBoxWords * n_pbox, 0u);
-        }
     }
     const uint32_t kd = o.kind == WQ_OP_SUBSCRIBE ? 1u : 0u;
-    pk[i] = p;
     slot[i] = sl;
     peer[i] = o.peer;
     kind[i] = (uint8_t)kd;
@@ -108,7 +126,7 @@ __global__ void k_delta_events(const wq_op* __restrict__ ops, uint32_t n, double
 }
 
 // Sorted order -> peer / kind columns and cube heads.
-__global__ void k_delta_mark(const uint32_t* __restrict__ order, const uint64_t* __restrict__ spk,
+__global__ void k_delta_mark(const uint32_t* __restrict__ order, const uint32_t* __restrict__ spk,
                              const uint32_t* __restrict__ peer, const uint8_t* __restrict__ kind, uint32_t n,
                              uint32_t* sp, uint8_t* skd, uint32_t* head) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -136,20 +154,10 @@ __device__ __forceinline__ uint32_t run_last(const uint32_t* sp, uint32_t t, uin
     return t;
 }
 
-__device__ __forceinline__ uint32_t find_rec(const DeltaTable& tb, uint64_t pk) {
-    uint64_t i = slot_of(rec_hash(pk) & tb.hmask, tb.rshift);
-    for (;;) {
-        const uint64_t k = tb.recs[i].pk;
-        if (k == pk) return (uint32_t)i;
-        if (k == 0) return kNone;
-        i = (i + 1) & tb.rmask;
-    }
-}
-
 __device__ __forceinline__ uint32_t grown(uint32_t n) { return n + n / 2 + 4; }
 
 __global__ __launch_bounds__(kBlock) void k_delta_plan(DeltaTable tb, const uint32_t* __restrict__ cube_start,
-                                                       const uint64_t* __restrict__ spk,
+                                                       const uint32_t* __restrict__ sslot,
                                                        const uint32_t* __restrict__ sp,
                                                        const uint8_t* __restrict__ skd, const DeltaSummary* sum,
                                                        uint32_t n, uint4* plan, uint32_t* reloc, uint64_t* part) {
@@ -161,15 +169,9 @@ __global__ __launch_bounds__(kBlock) void k_delta_plan(DeltaTable tb, const uint
     uint32_t rw = 0;
     if (c < n_dc) {
         const uint32_t s0 = cube_start[c], s1 = cube_start[c + 1];
-        const uint64_t pk = spk[s0];
-        const uint32_t slot = find_rec(tb, pk);
-        uint32_t oc = 0, off = 0, cap = 0;
-        if (slot != kNone) {
-            const Record& r = tb.recs[slot];
-            oc = r.count;
-            off = r.list_off;
-            cap = r.unused[0];
-        }
+        const uint32_t slot = sslot[s0];  // k_delta_events gave every cube of the batch its record
+        const Record& r = tb.recs[slot];
+        const uint32_t oc = r.count, off = r.list_off, cap = r.cap;
         const uint32_t* old = tb.list + off + 1;
         uint32_t adds = 0, rms = 0, j = 0;
         for (uint32_t t = s0; t < s1;) {
@@ -220,7 +222,6 @@ __global__ __launch_bounds__(kBlock) void k_delta_reduce(const uint64_t* __restr
 }
 
 __global__ __launch_bounds__(kBlock) void k_delta_apply(DeltaTable tb, const uint32_t* __restrict__ cube_start,
-                                                        const uint64_t* __restrict__ spk,
                                                         const uint32_t* __restrict__ sp,
                                                         const uint8_t* __restrict__ skd, const DeltaSummary* sum,
                                                         const uint4* __restrict__ plan,
@@ -231,13 +232,12 @@ __global__ __launch_bounds__(kBlock) void k_delta_apply(DeltaTable tb, const uin
     const uint4 pl = plan[c];
     if (!pl.z) return;
     const uint32_t s0 = cube_start[c], s1 = cube_start[c + 1];
-    const uint64_t pk = spk[s0];
     const uint32_t nc = pl.y, oc = pl.w;
     uint64_t slot = pl.x;
     uint32_t off = 0, cap = 0;
     if (pl.x == kNone) return;  // unreachable: k_delta_events gave every cube of the batch a record
     off = tb.recs[slot].list_off;
-    cap = tb.recs[slot].unused[0];
+    cap = tb.recs[slot].cap;
     uint32_t* L = tb.list;
     if (reloc[c]) {  // forward merge of the old list and the changes into new space
         const uint32_t dst = (uint32_t)(list_base + reloc_off[c]);
@@ -285,13 +285,11 @@ __global__ __launch_bounds__(kBlock) void k_delta_apply(DeltaTable tb, const uin
     const uint32_t* a = L + off + 1;
     uint64_t sig = 0;
     for (uint32_t j = 0; j < nc; ++j) sig |= peer_sig(a[j]);
-    Record& r = tb.recs[slot];
-    r.pk = pk;
+    Record& r = tb.recs[slot];  // the key (pk, ext) stays as claimed
     r.count = nc;
     r.list_off = off;
     r.sig = sig;
-    r.unused[0] = cap;
-    r.unused[1] = kNone;
+    r.cap = cap;
 #pragma unroll 4
     for (int j = 0; j < kInline; ++j) r.peers[j] = (uint32_t)j < nc ? a[j] : kNone;
 }
@@ -516,7 +514,7 @@ __global__ __launch_bounds__(kBlock) void k_delta_apply_group(DeltaTable tb, con
                 case 4: v = (uint32_t)sig; break;
                 case 5: v = (uint32_t)(sig >> 32); break;
                 case 6: v = cap; break;
-                case 7: v = kNone; break;
+                case 7: v = h1.w; break;  // ext: the key's high word
                 default: v = (uint32_t)(w - kInlineWord0) < n ? cur[w - kInlineWord0] : kNone; break;
             }
             rw[w] = v;
@@ -603,9 +601,9 @@ __global__ __launch_bounds__(kBlock) void k_remove_peers(DeltaTable tb, const Sl
         uint32_t w, off, n;
         if (is_rec) {
             const uint4 h0 = reinterpret_cast<const uint4*>(tb.recs + e)[0];
-            const uint64_t pk = ((uint64_t)h0.y << 32) | h0.x;
-            if (!pk || !h0.z) continue;
-            w = (uint32_t)(pk >> 54) - 1u;
+            const uint32_t ext = reinterpret_cast<const uint32_t*>(tb.recs + e)[7];
+            if (!ext || !h0.z) continue;
+            w = (ext >> 8) - 1u;
             n = h0.z;
             off = h0.w;
         } else {
@@ -659,19 +657,18 @@ __global__ __launch_bounds__(kBlock) void k_remove_peers(DeltaTable tb, const Sl
 
 // ---- materialize: the sorted-state arrays from the records and slots ---------------------------
 
-__device__ __forceinline__ void unpack_key(uint64_t pk, int64_t s, uint32_t* w, int64_t* k) {
-    *w = (uint32_t)(pk >> 54) - 1u;
-    k[0] = ((int64_t)((pk >> 36) & 0x3FFFFull) - (int64_t)kAxisBias) * s;
-    k[1] = ((int64_t)((pk >> 18) & 0x3FFFFull) - (int64_t)kAxisBias) * s;
-    k[2] = ((int64_t)(pk & 0x3FFFFull) - (int64_t)kAxisBias) * s;
+__device__ __forceinline__ void record_key(const Record& r, int64_t s, uint32_t* w, int64_t* k) {
+    uint32_t a[3];
+    unpack_key(r.pk, r.ext, w, a);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) k[d] = ((int64_t)a[d] - (int64_t)kAxisBias) * s;
 }
 
 __global__ void k_mat_count(const Record* __restrict__ recs, uint64_t rcap, const Slot* __restrict__ slots,
                             uint64_t scap, const uint32_t* __restrict__ list, uint32_t* cnt) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i < rcap) {
-        const uint4 h = *reinterpret_cast<const uint4*>(recs + i);
-        cnt[i] = (h.x | h.y) ? h.z : 0u;
+        cnt[i] = recs[i].ext ? recs[i].count : 0u;
     } else if (i < rcap + scap) {
         const SlotView s = load_slot(slots, i - rcap);
         cnt[i] = s.world == kWorldEmpty ? 0u : list[s.off];
@@ -690,7 +687,7 @@ __global__ void k_mat_write(const Record* __restrict__ recs, uint64_t rcap, cons
     int64_t k[3];
     if (i < rcap) {
         const Record& r = recs[i];
-        unpack_key(r.pk, s, &w, k);
+        record_key(r, s, &w, k);
         off = r.list_off;
     } else {
         const SlotView v = load_slot(slots, i - rcap);
@@ -731,21 +728,24 @@ int table_sync_delta_stats(wq_router* h) {
 
 namespace {
 
-// The per-lane path (any cube size): sort by (pk, peer), one lane per touched cube.
+// The per-lane path (any cube size): sort by (slot, peer), one lane per touched cube.
 int delta_plan_lanes(wq_router* h, uint32_t n, DeltaTable tb, DeltaSummary* sum) {
     DeltaWs& d = h->dws;
     hipStream_t s = h->stream;
     const uint32_t nb = grid_for(n);
+    int bits = 1;
+    while ((1ull << bits) < h->tab.rec_cap) bits++;
     uint32_t* idx_a = h->idx_a.as<uint32_t>();
     uint32_t* idx_b = h->idx_b.as<uint32_t>();
     hipLaunchKernelGGL(k_iota, dim3(nb), dim3(kBlock), 0, s, idx_a, (uint64_t)n);
     int rc = sort_pairs<uint32_t>(h, d.peer.as<uint32_t>(), h->key32_a.as<uint32_t>(), idx_a, idx_b, n, 32);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_gather<uint64_t>, dim3(nb), dim3(kBlock), 0, s, d.pk.as<uint64_t>(), idx_b,
-                       h->key64_a.as<uint64_t>(), (uint64_t)n);
-    if ((rc = sort_pairs<uint64_t>(h, h->key64_a.as<uint64_t>(), h->key64_b.as<uint64_t>(), idx_b, idx_a, n, 64)))
-        return rc;
-    const uint64_t* spk = h->key64_b.as<uint64_t>();
+    uint32_t* key_a = h->key64_a.as<uint32_t>();  // 32-bit slot columns in the 64-bit scratch
+    uint32_t* key_b = h->key64_b.as<uint32_t>();
+    hipLaunchKernelGGL(k_gather<uint32_t>, dim3(nb), dim3(kBlock), 0, s, d.slot.as<uint32_t>(), idx_b, key_a,
+                       (uint64_t)n);
+    if ((rc = sort_pairs<uint32_t>(h, key_a, key_b, idx_b, idx_a, n, bits))) return rc;
+    const uint32_t* spk = key_b;
     uint32_t* head = h->flags.as<uint32_t>();
     uint32_t* cid = h->scan.as<uint32_t>();
     hipLaunchKernelGGL(k_delta_mark, dim3(nb), dim3(kBlock), 0, s, idx_a, spk, d.peer.as<uint32_t>(),
@@ -809,7 +809,6 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
         return WQ_OK;
     }
     const uint32_t nb = grid_for(n);
-    WQ_ALLOC(h, d.pk, (uint64_t)n * 8);
     WQ_ALLOC(h, d.slot, (uint64_t)n * 4);
     WQ_ALLOC(h, d.peer, (uint64_t)n * 4);
     WQ_ALLOC(h, d.kind, n);
@@ -837,9 +836,10 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     DeltaSummary* sum = d.summ.as<DeltaSummary>();
     WQ_HIP(h, hipMemsetAsync(sum, 0, sizeof(DeltaSummary), s));
     hipLaunchKernelGGL(k_delta_events, dim3(nb), dim3(kBlock), 0, s, h->cur_ops, n, (double)h->cube_size,
-                       (int64_t)h->cube_size, t.recs.as<Record>(), t.rec_cap - 1, t.rec_shift, h->hash_mask,
-                       d.pk.as<uint64_t>(), d.slot.as<uint32_t>(), d.peer.as<uint32_t>(), d.kind.as<uint8_t>(),
-                       d.sv.as<uint64_t>(), sum, t.n_pbox ? t.pbox.as<uint32_t>() : nullptr, t.n_pbox);
+                       (int64_t)h->cube_size, t.recs.as<Record>(), t.rclaim.as<uint32_t>(),
+                       kBatchTag | (uint32_t)(++h->n_delta_batches & 0x7FFFFFFFu), t.rec_cap - 1,
+                       t.rec_shift, h->hash_mask, d.slot.as<uint32_t>(), d.peer.as<uint32_t>(),
+                       d.kind.as<uint8_t>(), d.sv.as<uint64_t>(), sum);
     DeltaTable tb{t.recs.as<Record>(), t.rclaim.as<uint32_t>(), t.rec_cap - 1, t.rec_shift, h->hash_mask,
                   t.list.as<uint32_t>()};
     int rc = delta_plan_groups(h, n, sum);
@@ -871,12 +871,15 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
         h->dstat_pending = true;
     } else {
         hipLaunchKernelGGL(k_delta_apply, dim3(nb), dim3(kBlock), 0, s, tb, h->cube_start.as<uint32_t>(),
-                           h->key64_b.as<uint64_t>(), d.sp.as<uint32_t>(), d.skd.as<uint8_t>(), sum,
+                           d.sp.as<uint32_t>(), d.skd.as<uint8_t>(), sum,
                            d.plan.as<uint4>(), d.reloc.as<uint32_t>(), d.reloc_off.as<uint32_t>(), t.list_used);
         h->st.n = (uint64_t)((int64_t)h->st.n + (int64_t)hs.d_entries);
         t.n_cubes = (uint64_t)((int64_t)t.n_cubes + (int64_t)hs.d_live);
     }
     WQ_HIP(h, hipGetLastError());
+    // subscribes may widen peer boxes: switch the boxes off until the next full build (the count
+    // pass then searches every long list); per-op box atomics here cost more than they save
+    if (t.n_pbox) WQ_HIP(h, hipMemsetAsync(t.pbox.as<uint32_t>() + (uint64_t)kBoxWords * t.n_pbox, 0, 4, s));
     t.list_used += hs.reloc_words;
     h->st_stale = true;
     h->any_stale = true;

@@ -83,29 +83,37 @@ __host__ __device__ __forceinline__ uint32_t shard_of(uint32_t w, int64_t x, int
 }
 
 // ---- bucket records (the table the hot path probes) --------------------------------------
-// A "regular" cube — world < 1023 and every key coordinate an exact multiple k = a*s of the cube
-// size with a in [-2^17, 2^17) — has an exact 64-bit packed key
-//   pk = (world + 1) << 54 | (ax + 2^17) << 36 | (ay + 2^17) << 18 | (az + 2^17)   (pk != 0).
-// Every key a Vector3 can produce for coordinates within +-2^17 cubes of the origin is regular.
+// A "regular" cube — world < 2^24 - 1 and every key coordinate an exact multiple k = a*s of the
+// cube size with a in [-2^23, 2^23) — has an exact 96-bit packed key
+//   V = (world + 1) << 72 | (ax + 2^23) << 48 | (ay + 2^23) << 24 | (az + 2^23)
+// held as pk = V mod 2^64 (header words 0-1) and ext = V >> 64 (word 7). ext is never 0 for a key
+// (world + 1 >= 1), so ext == 0 marks an empty record. Every key a Vector3 can produce within
+// +-2^23 cubes of the origin (+-134M units at the default cube_size 16, far past Minecraft's
+// +-3e7) in any of 16M worlds is regular.
 // Regular cubes live in 128-byte records (one cache line: one fabric request per lookup):
 //   chunk 0 (bytes 0-15)   pk, peer count, offset of the cube's full list in `list`
-//   chunk 1 (16-31)        sig: 64-bit Bloom signature of the cube's peers (peer_sig), 8 B unused
+//   chunk 1 (16-31)        sig: 64-bit Bloom signature of the cube's peers (peer_sig), the list
+//                          block's capacity, ext
 //   chunks 2-7 (32-127)    p0 .. p23, four per chunk
 // so peer i sits in word 8 + i: output quad q of a message without a skipped sender is chunk
-// 2 + q verbatim (route_emit.hpp). The count pass reads chunks 0-1 only unless the signature says
-// the sender may be subscribed (route_count.hpp).
-// Everything else (raw off-grid keys, NaN/inf/huge coordinates, world ids >= 1023) lives in the
-// 32-byte full-key Slot table. Both tables are exact; a key is in exactly one of them.
+// 2 + q verbatim (route_emit.hpp). The count pass reads chunks 0-1 (key, count, signature) in its
+// first round (route_count.hpp).
+// Everything else (raw off-grid keys, NaN/inf/saturated coordinates, the last world ids) lives in
+// the 32-byte full-key Slot table. Both tables are exact; a key is in exactly one of them.
 constexpr int kInline = 24;
 constexpr int kInlineWord0 = 8;
-constexpr uint32_t kAxisBias = 1u << 17;
+constexpr int kAxisBits = 24;
+constexpr uint32_t kAxisBias = 1u << (kAxisBits - 1);
+constexpr uint32_t kAxisMask = (1u << kAxisBits) - 1u;
+constexpr uint32_t kMaxPackedWorld = (1u << 24) - 2u;  // world + 1 must fit 24 bits
 
 struct __attribute__((aligned(128))) Record {
-    uint64_t pk;       // 0 = empty
+    uint64_t pk;       // low 64 bits of the packed key
     uint32_t count;    // peers subscribed to the cube
     uint32_t list_off; // list[list_off] = count, list[list_off+1 ..] = ascending peers
     uint64_t sig;      // OR of peer_sig over the cube's peers
-    uint32_t unused[2];
+    uint32_t cap;      // capacity (peers) of the cube's list block
+    uint32_t ext;      // high 32 bits of the packed key; 0 = empty record
     uint32_t peers[kInline];  // the first min(count, kInline) peers, ascending; rest 0xFFFFFFFF
 };
 // Two of the 64 signature bits per peer (one multiply): with ~10 peers per cube about 7% of
@@ -120,24 +128,36 @@ static_assert(sizeof(Record) == 128, "Record must be one 128-byte line");
 __host__ __device__ __forceinline__ uint32_t list_capacity(uint32_t count) { return count + count / 4 + 2; }
 
 __host__ __device__ __forceinline__ bool pack_key(uint32_t w, int64_t x, int64_t y, int64_t z, double sf,
-                                                  uint64_t* pk) {
-    if (w >= 1023u) return false;
+                                                  uint64_t* pk, uint32_t* ext) {
+    if (w > kMaxPackedWorld) return false;
     const int64_t k[3] = {x, y, z};
     uint64_t a[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
-        // |k| < 2^33: exact in f64, and k/s is an integer iff the quotient is
-        if (k[d] <= -(1ll << 33) || k[d] >= (1ll << 33)) return false;
+        // |k| < 2^40: exact in f64; with |k/s| < 2^23 the quotient's ulp is <= 2^-29, far below the
+        // >= 2^-16 distance of a non-multiple's k/s from an integer, so k/s is an integer iff the
+        // rounded quotient is
+        if (k[d] <= -(1ll << 40) || k[d] >= (1ll << 40)) return false;
         const double q = (double)k[d] / sf;
-        if (q != trunc(q) || q < -131072.0 || q >= 131072.0) return false;
+        if (q != trunc(q) || q < -(double)kAxisBias || q >= (double)kAxisBias) return false;
         a[d] = (uint64_t)((int64_t)q + (int64_t)kAxisBias);
     }
-    *pk = ((uint64_t)(w + 1) << 54) | (a[0] << 36) | (a[1] << 18) | a[2];
+    *pk = (a[0] << 48) | (a[1] << 24) | a[2];
+    *ext = ((w + 1u) << 8) | (uint32_t)(a[0] >> 16);
     return true;
 }
 
-__host__ __device__ __forceinline__ uint64_t rec_hash(uint64_t pk) {
-    uint64_t h = pk ^ (pk >> 31);
+// The packed key's world and biased axes (a_d = k_d / s + 2^23).
+__host__ __device__ __forceinline__ void unpack_key(uint64_t pk, uint32_t ext, uint32_t* w, uint32_t* a) {
+    *w = (ext >> 8) - 1u;
+    a[0] = ((ext & 0xFFu) << 16) | (uint32_t)(pk >> 48);
+    a[1] = (uint32_t)(pk >> 24) & kAxisMask;
+    a[2] = (uint32_t)pk & kAxisMask;
+}
+
+__host__ __device__ __forceinline__ uint64_t rec_hash(uint64_t pk, uint32_t ext) {
+    uint64_t h = pk ^ ((uint64_t)ext * 0xD6E8FEB86659FD93ull);
+    h ^= h >> 31;
     h *= 0x9E3779B97F4A7C15ull;
     h ^= h >> 29;
     h *= 0xBF58476D1CE4E5B9ull;
@@ -200,42 +220,43 @@ struct TableView {
 };
 
 // ---- per-peer boxes: a fast "certainly not subscribed" for long lists ---------------------
-// For every peer, the world and the per-axis [min, max] of the packed axes (pack_key) of the
-// record cubes it is subscribed to: 8 words {world, ax_min, ay_min, az_min, ax_max, ay_max,
-// az_max, -}. A message whose cube lies outside its sender's box cannot have the sender among
-// the cube's peers, so the count pass skips the binary search of a long list (C3: random senders
-// in hotspot cubes of ~500 peers — ~0.8 extra line per message). Boxes only grow: subscribes
-// widen them (builds and incremental updates); unsubscribes and disconnects leave them wider
-// than needed, which is still exact ("maybe" -> the search decides). kBoxMulti: the peer holds
-// record cubes in more than one world -> always search.
-constexpr uint32_t kBoxEmpty = 0xFFFFFFFFu;
-constexpr uint32_t kBoxMulti = 0xFFFFFFFEu;  // never a packed world (those are < 1023)
+// For every peer, the [min, max] world and the per-axis [min, max] of the packed axes (pack_key)
+// of the record cubes it is subscribed to: 8 words {world_min, world_max, a0_min, a0_max | a1_min,
+// a1_max, a2_min, a2_max} (empty: every min 0xFFFFFFFF, every max 0). A message whose cube lies
+// outside its sender's box cannot have the sender among the cube's peers, so the count pass skips
+// the binary search of a long list (C3: random senders in hotspot cubes of ~500 peers — ~0.8
+// extra line per message). Built with the table; unsubscribes and disconnects leave boxes wider
+// than needed, which is still exact ("maybe" -> the search decides); an incremental batch turns
+// them off (valid word 0) until the next build. A peer with record cubes in several worlds gets
+// the world-range test only. The test reads the box's first half (world, axis 0) and only then
+// the second: few registers live in the count pass's probe loop.
 constexpr int kBoxWords = 8;
 
-__device__ __forceinline__ void box_add(uint32_t* box, uint64_t pk) {
-    const uint32_t w = (uint32_t)(pk >> 54) - 1u;
-    const uint32_t ax = (uint32_t)(pk >> 36) & 0x3FFFFu, ay = (uint32_t)(pk >> 18) & 0x3FFFFu,
-                   az = (uint32_t)pk & 0x3FFFFu;
-    const uint32_t w0 = atomicCAS(&box[0], kBoxEmpty, w);
-    if (w0 != kBoxEmpty && w0 != w) atomicExch(&box[0], kBoxMulti);
-    atomicMin(&box[1], ax);
-    atomicMin(&box[2], ay);
-    atomicMin(&box[3], az);
-    atomicMax(&box[4], ax);
-    atomicMax(&box[5], ay);
-    atomicMax(&box[6], az);
+__device__ __forceinline__ void box_add(uint32_t* box, uint64_t pk, uint32_t ext) {
+    uint32_t w, a[3];
+    unpack_key(pk, ext, &w, a);
+    atomicMin(&box[0], w);
+    atomicMax(&box[1], w);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        atomicMin(&box[2 + 2 * d], a[d]);
+        atomicMax(&box[3 + 2 * d], a[d]);
+    }
 }
 
-// false: `peer` is certainly not subscribed to the record cube pk.
-__device__ __forceinline__ bool box_may_hold(const TableView& t, uint32_t peer, uint64_t pk) {
+// false: `peer` is certainly not subscribed to the record cube (pk, ext).
+__device__ __forceinline__ bool box_may_hold(const TableView& t, uint32_t peer, uint64_t pk, uint32_t ext) {
     if (peer >= t.n_pbox) return false;
-    const uint4 a = *reinterpret_cast<const uint4*>(t.pbox + (uint64_t)kBoxWords * peer);
-    const uint4 b = *reinterpret_cast<const uint4*>(t.pbox + (uint64_t)kBoxWords * peer + 4);
-    if (a.x == kBoxMulti) return true;
-    const uint32_t w = (uint32_t)(pk >> 54) - 1u;
-    const uint32_t ax = (uint32_t)(pk >> 36) & 0x3FFFFu, ay = (uint32_t)(pk >> 18) & 0x3FFFFu,
-                   az = (uint32_t)pk & 0x3FFFFu;
-    return a.x == w && ax >= a.y && ay >= a.z && az >= a.w && ax <= b.x && ay <= b.y && az <= b.z;
+    const uint4* b = reinterpret_cast<const uint4*>(t.pbox + (uint64_t)kBoxWords * peer);
+    const uint4 lo = b[0];
+    const uint32_t w = (ext >> 8) - 1u;
+    if (w < lo.x || w > lo.y) return false;  // also: no record cube at all (min > max)
+    if (lo.x != lo.y) return true;            // several worlds: the world range is all we know
+    const uint32_t a0 = ((ext & 0xFFu) << 16) | (uint32_t)(pk >> 48);
+    if (a0 < lo.z || a0 > lo.w) return false;
+    const uint4 hi = b[1];
+    const uint32_t a1 = (uint32_t)(pk >> 24) & kAxisMask, a2 = (uint32_t)pk & kAxisMask;
+    return a1 >= hi.x && a1 <= hi.y && a2 >= hi.z && a2 <= hi.w;
 }
 
 // C5: is peer p within the radius of message position (mx, my, mz)? f64, left to right, no FMA
@@ -250,14 +271,17 @@ __device__ __forceinline__ bool within_radius(const TableView& t, double mx, dou
     return d2 <= t.r2;
 }
 
-// Header of the record probe sequence for pk: walks while the slot holds another key.
-__device__ __forceinline__ uint64_t find_record(const TableView& t, uint64_t pk, uint4* hdr) {
-    uint64_t i = slot_of(rec_hash(pk) & t.hash_mask, t.rec_shift);
+// Header (chunks 0-1) of the record probe sequence for (pk, ext): walks while the slot holds
+// another key; an empty record (ext == 0) ends it.
+__device__ __forceinline__ uint64_t find_record(const TableView& t, uint64_t pk, uint32_t ext, uint4* h0, uint4* h1) {
+    uint64_t i = slot_of(rec_hash(pk, ext) & t.hash_mask, t.rec_shift);
     for (;;) {
-        const uint4 h = *reinterpret_cast<const uint4*>(t.recs + i);
-        const uint64_t k = ((uint64_t)h.y << 32) | h.x;
-        if (k == 0 || k == pk) {
-            *hdr = h;
+        const uint4 a = *reinterpret_cast<const uint4*>(t.recs + i);
+        const uint4 b = *(reinterpret_cast<const uint4*>(t.recs + i) + 1);
+        const uint64_t k = ((uint64_t)a.y << 32) | a.x;
+        if (b.w == 0 || (k == pk && b.w == ext)) {
+            *h0 = a;
+            *h1 = b;
             return i;
         }
         i = (i + 1) & t.rec_mask;
@@ -267,10 +291,11 @@ __device__ __forceinline__ uint64_t find_record(const TableView& t, uint64_t pk,
 // Offset of the cube's list in t.list, or kNone (both tables).
 __device__ __forceinline__ uint32_t find_list(const TableView& t, uint32_t w, int64_t x, int64_t y, int64_t z) {
     uint64_t pk;
-    if (pack_key(w, x, y, z, t.sf, &pk)) {
-        uint4 h;
-        find_record(t, pk, &h);
-        return (h.x | h.y) ? h.w : kNone;
+    uint32_t ext;
+    if (pack_key(w, x, y, z, t.sf, &pk, &ext)) {
+        uint4 h0, h1;
+        find_record(t, pk, ext, &h0, &h1);
+        return h1.w ? h0.w : kNone;
     }
     return probe(t.slots, t.slot_mask, t.slot_shift, cube_hash(w, x, y, z) & t.hash_mask, w, x, y, z);
 }

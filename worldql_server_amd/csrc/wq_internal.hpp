@@ -68,8 +68,8 @@ struct Table {
 
 // Scratch of the incremental update (wq_delta.hip).
 struct DeltaWs {
-    DevBuf pk, slot, peer, kind;  // per op (u64, u32, u32, u8)
-    DevBuf sp, skd;         // per op in (pk, peer, op) order: peer, kind (per-lane path)
+    DevBuf slot, peer, kind;      // per op (u32, u32, u8)
+    DevBuf sp, skd;         // per op in (slot, peer, op) order: peer, kind (per-lane path)
     DevBuf sv, svs;         // per op: kind << 32 | peer, and the same sorted by record slot (group path)
     DevBuf plan;            // uint4 per delta cube {record slot, new count, changed, -}
     DevBuf reloc, reloc_off;  // u32 per delta cube: words of a relocated list, their exclusive scan
@@ -122,6 +122,7 @@ struct wq_router {
     bool st_stale = false, any_stale = false;
     wq::DeltaWs dws;
     uint64_t n_delta_applies = 0, n_delta_fallbacks = 0, n_delta_lane_batches = 0;
+    uint64_t n_delta_batches = 0;  // batch tags of the record claims (wq_delta.hip)
     bool dstat_pending = false;
 
     // build scratch

@@ -142,7 +142,7 @@ int wq_router_destroy(wq_router* h) {
                       &h->cube_start, &h->rws.buf, &h->rws.info, &h->rws.e, &h->rws.tiles,
                       &h->h_in, &h->h_out, &h->tab.recs, &h->tab.rclaim, &h->tab.pbox, &h->shard_hist,
                       &h->rec_keys, &h->rec_w, &h->rec_s, &h->rec_r, &h->ppos, &h->rws.agg, &h->rws.spill, &h->rws.scan_tmp,
-                      &h->dws.pk, &h->dws.slot, &h->dws.peer, &h->dws.kind, &h->dws.sp, &h->dws.skd, &h->dws.plan,
+                      &h->dws.slot, &h->dws.peer, &h->dws.kind, &h->dws.sp, &h->dws.skd, &h->dws.plan,
                       &h->dws.reloc, &h->dws.reloc_off, &h->dws.part, &h->dws.summ, &h->dws.dstat,
                       &h->dws.rm_bits, &h->dws.sv, &h->dws.svs};
     for (DevBuf* b : bufs) b->release();

@@ -20,6 +20,8 @@
 // kernel in this file.
 #include <cstring>
 
+#include <algorithm>
+
 #include "table_prims.hpp"
 
 namespace wq {
@@ -155,18 +157,21 @@ __global__ void k_insert_cubes(EvView st, const uint32_t* __restrict__ cube_star
     const uint32_t j = cube_start[c];
     const uint32_t cnt = cube_start[c + 1] - j;
     uint64_t pk;
-    if (pack_key(st.w[j], st.kx[j], st.ky[j], st.kz[j], sf, &pk)) {
-        uint64_t s = slot_of(rec_hash(pk) & hmask, rshift);
-        while (atomicCAS(&rclaim[s], 0u, c + 1) != 0u) s = (s + 1) & rmask;
+    uint32_t ext;
+    if (pack_key(st.w[j], st.kx[j], st.ky[j], st.kz[j], sf, &pk, &ext)) {
+        uint64_t s = slot_of(rec_hash(pk, ext) & hmask, rshift);
+        // claim words: 0 free, 1 being claimed, >= 2 holds a key (wq_delta.hip); c + 2 < 2^31, as
+        // 2^31 records would take 256 GiB
+        while (atomicCAS(&rclaim[s], 0u, c + 2) != 0u) s = (s + 1) & rmask;
         Record& r = recs[s];
         r.pk = pk;
+        r.ext = ext;
         r.count = cnt;
         r.list_off = loff[c];
         uint64_t sig = 0;
         for (uint32_t i = 0; i < cnt; ++i) sig |= peer_sig(st.p[j + i]);
         r.sig = sig;
-        r.unused[0] = list_capacity(cnt);
-        r.unused[1] = 0xFFFFFFFFu;
+        r.cap = list_capacity(cnt);
 #pragma unroll 2
         for (int i = 0; i < kInline; ++i) r.peers[i] = (uint32_t)i < cnt ? st.p[j + i] : 0xFFFFFFFFu;
         return;
@@ -183,18 +188,27 @@ __global__ void k_insert_cubes(EvView st, const uint32_t* __restrict__ cube_star
 }
 
 __global__ void k_max_peer(const uint32_t* __restrict__ p, uint64_t n, uint32_t* out) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) atomicMax(out, p[i]);
+    __shared__ uint32_t wmax[kBlock / 64];
+    uint32_t v = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+        v = max(v, p[i]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 1; k < kBlock / 64; ++k) v = max(v, wmax[k]);
+        atomicMax(out, v);  // one atomic per block
+    }
 }
 
 __global__ void k_box_init(uint32_t* box, uint32_t n_peers) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i < n_peers) {
         uint32_t* b = box + (uint64_t)kBoxWords * i;
-        b[0] = kBoxEmpty;
-        b[1] = b[2] = b[3] = 0xFFFFFFFFu;
-        b[4] = b[5] = b[6] = 0u;
-        b[7] = 0u;
+        b[0] = b[2] = b[4] = b[6] = 0xFFFFFFFFu;  // minima
+        b[1] = b[3] = b[5] = b[7] = 0u;           // maxima
     }
     if (i == 0) box[(uint64_t)kBoxWords * n_peers] = 1u;  // valid
 }
@@ -204,7 +218,9 @@ __global__ void k_box_build(EvView st, uint64_t n, double sf, uint32_t* box) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     uint64_t pk;
-    if (pack_key(st.w[i], st.kx[i], st.ky[i], st.kz[i], sf, &pk)) box_add(box + (uint64_t)kBoxWords * st.p[i], pk);
+    uint32_t ext;
+    if (pack_key(st.w[i], st.kx[i], st.ky[i], st.kz[i], sf, &pk, &ext))
+        box_add(box + (uint64_t)kBoxWords * st.p[i], pk, ext);
 }
 
 __global__ void k_any_keys(const uint32_t* __restrict__ w, const uint32_t* __restrict__ p, uint64_t n,
@@ -454,16 +470,17 @@ int table_rebuild_derived(wq_router* h) {
                            t.rclaim.as<uint32_t>(), t.recs.as<Record>(),
                            rcap - 1, t.rec_shift, t.claim.as<uint32_t>(), t.slots.as<Slot>(), cap - 1, t.shift,
                            h->hash_mask, (double)h->cube_size);
-    // per-peer boxes (PeerBox, wq_device.hpp): room for 25% more peer ids than the build has, so
-    // incremental subscribes of new peers keep them; one beyond that switches them off
+    // per-peer boxes (PeerBox, wq_device.hpp) for the peers the build holds; an incremental batch
+    // switches them off until the next build (wq_delta.hip)
     t.n_pbox = 0;
     if (S) {
         uint32_t* mx = h->small.as<uint32_t>();
         WQ_HIP(h, hipMemsetAsync(mx, 0, 4, s));
-        hipLaunchKernelGGL(k_max_peer, dim3(grid_for(S)), dim3(kBlock), 0, s, h->st.p.as<uint32_t>(), S, mx);
+        hipLaunchKernelGGL(k_max_peer, dim3(std::min<unsigned>(grid_for(S), 2048u)), dim3(kBlock), 0, s,
+                           h->st.p.as<uint32_t>(), S, mx);
         uint32_t max_peer = 0;
         if ((rc = read_u32(h, mx, 0, &max_peer))) return rc;
-        const uint64_t np = (uint64_t)max_peer + 1, cap = np + np / 4 + 1024;
+        const uint64_t cap = (uint64_t)max_peer + 1;
         if (cap < 0xFFFFFFF0ull) {
             WQ_ALLOC(h, t.pbox, (cap * kBoxWords + 1) * 4);
             hipLaunchKernelGGL(k_box_init, dim3(grid_for(cap)), dim3(kBlock), 0, s, t.pbox.as<uint32_t>(),
