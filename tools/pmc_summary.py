@@ -42,7 +42,7 @@ def main():
         for c, v in sorted(means.items()):
             print(f"    {c:28s} {v:16.1f}   (n={len(cs[c])})")
         if any(s in k for s in ("count_kernel", "tile_scan_kernel", "tile_finish_kernel", "emit_kernel",
-                                "emit_heavy_kernel", "tick_kernel")) and not (
+                                "emit_heavy_kernel", "emit_map_kernel", "tick_kernel")) and not (
                 a.exclude and a.exclude in k):
             route[k] = means
     if a.json and route:

@@ -38,8 +38,9 @@ struct Cfg {
     void (*tick)(const TickParams&, hipStream_t, unsigned);
     // count+spill / tile_scan / copy (route_spill.hpp): image positions per block, or 0
     int spill_stage;
-    // three launches: 0 = emit_kernel (windowed image, heavy rows through emit_direct), or the
-    // outputs in flight per thread of emit_heavy_kernel (every row through emit_direct, 4 KB LDS)
+    // three launches: 0 = emit_kernel (windowed image, heavy rows through emit_direct), the
+    // outputs in flight per thread of emit_heavy_kernel (every row through emit_direct, 4 KB LDS),
+    // or 100 + outputs per thread per window of emit_map_kernel (owner map)
     int emit_heavy;
 };
 
@@ -76,13 +77,18 @@ const Cfg kCfgs[] = {
     WQ_CFGS(kSpillStage),     // 7: count+spill / tile_scan / copy, no block waits on another
     WQ_CFG3H(16),             // 8: three launches, emit_heavy_kernel (16 outputs in flight per thread)
     WQ_CFG3H(8),              // 9: ... 8 in flight
+    // 10: three launches, emit_map_kernel (owner map, 16 outputs per thread per window): C3 1288 us
+    //     against cfg 8's 1472 us on one box (R = 8: 1366, R = 32: 1412; storing the message index
+    //     before the peer loads land: 1467)
+    WQ_CFG3H(116),
+    WQ_CFG3H(108),            // 11: ... 8 per window
 };
 #undef WQ_CFG1
 #undef WQ_CFGS
 #undef WQ_CFG3
 #undef WQ_CFG3H
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
-constexpr int kCfgHeavy = 8;  // the default shape under wq_set_fanout_hint >= WQ_HEAVY_FANOUT (emit_heavy_kernel)
+constexpr int kCfgHeavy = 10;  // the default shape under wq_set_fanout_hint >= WQ_HEAVY_FANOUT (emit_map_kernel)
 
 }  // namespace
 
@@ -274,6 +280,10 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         hipLaunchKernelGGL((emit_heavy_kernel<16>), eg, dim3(kBlock), 0, s, ep);
     else if (cfg.emit_heavy == 8)
         hipLaunchKernelGGL((emit_heavy_kernel<8>), eg, dim3(kBlock), 0, s, ep);
+    else if (cfg.emit_heavy == 116)
+        hipLaunchKernelGGL((emit_map_kernel<16>), eg, dim3(kBlock), 0, s, ep);
+    else if (cfg.emit_heavy == 108)
+        hipLaunchKernelGGL((emit_map_kernel<8>), eg, dim3(kBlock), 0, s, ep);
     else if (cfg.emit_stage == 4096 + 2)
         hipLaunchKernelGGL((emit_kernel<4096, 2>), eg, dim3(kBlock), 0, s, ep);
     else if (cfg.emit_stage == 4096 + 4)
