@@ -307,9 +307,10 @@ int wq_debug_set_hash_bits(wq_router* h, int bits);
 int wq_debug_set_record_slack(wq_router* h, uint32_t slots_per_cube);
 /* ---- test hook: how many op batches took the incremental update (wq_delta.hip), how many
  * tried it but fell back to the full rebuild (irregular keys, list space, record load), and how
- * many incremental batches needed the per-lane path (a cube with > 256 peers or > 64 changes). */
+ * many incremental batches had a cube go through the wave path (a list longer than 48 peers;
+ * shorter lists are merged one lane per cube). */
 int wq_debug_update_counts(wq_router* h, uint64_t* incremental, uint64_t* rebuild_fallbacks,
-                           uint64_t* lane_batches);
+                           uint64_t* wave_batches);
 /* ---- tuning hook: select a compiled route-kernel shape (messages per thread, expansion chunk);
  * 0 is the default. Results are identical for every shape. */
 int wq_debug_set_route_config(wq_router* h, int cfg);

@@ -48,9 +48,15 @@ def test_delta_random_churn_vs_oracle(hash_bits, f):
     for tick in range(8):
         # concentrated batches: a few hot cubes gain many peers (relocation), others churn
         ops = _random_ops(rng, int(4000 * f), 3, 4500, half, 0.55)
-        nh = int(600 * f) if tick % 2 else 0  # odd ticks: one hot cube (> 64 changes: per-lane path)
+        nh = int(600 * f) if tick % 2 else 0  # odd ticks: one new hot cube (a lane merges 600 ops)
         hot = abi.ops_array(np.zeros(nh, np.uint32), rng.integers(0, 4500, nh).astype(np.uint32),
                             np.zeros(nh, np.uint8), pos=np.tile([[8.0 + 16 * tick, 8.0, 8.0]], (nh, 1)))
+        if tick % 2 == 0 and tick:  # even ticks: churn on the previous tick's hot cube (wave path)
+            nw = int(300 * f)
+            warm = abi.ops_array(np.zeros(nw, np.uint32), rng.integers(0, 4500, nw).astype(np.uint32),
+                                 rng.integers(0, 2, nw).astype(np.uint8),
+                                 pos=np.tile([[8.0 + 16 * (tick - 1), 8.0, 8.0]], (nw, 1)))
+            hot = abi.concat_ops([hot, warm])
         # re-issue some ops of this batch in reverse kind: last op wins per triple
         nf = int(500 * f)
         flip = ops[:nf].copy()
@@ -64,8 +70,8 @@ def test_delta_random_churn_vs_oracle(hash_bits, f):
         sender = rng.integers(0, 4500, M).astype(np.uint32)
         repl = rng.integers(0, 3, M).astype(np.uint8)
         assert _check(r, o, pos, world, sender, repl) > 0
-    inc, fb, lanes = r.update_counts(lanes=True)
-    assert inc == 8 and fb == 0 and ((4 <= lanes < 8) or f < 1)  # a tick touching an old hot cube goes per lane
+    inc, fb, wave = r.update_counts(lanes=True)
+    assert inc == 8 and fb == 0 and (wave >= 3 or f < 1)  # ticks touching an old hot cube: its list > kLaneList
     # membership and any-sets after churn (regenerated from the records)
     for w in range(4):
         assert (r.world_peers(w) == o.world_peers(w)).all()
@@ -180,7 +186,7 @@ def test_c4_scaled_churn_is_incremental():
         o.apply_ops(ops)
         rp = synth.stream(4, 3).below(3, len(w)).astype(np.uint8)
         assert _check(r, o, pos, w, s, rp) > 0
-    assert r.update_counts(lanes=True) == (5, 0, 0)  # C4 churn: the wave path throughout
+    assert r.update_counts() == (5, 0)  # C4 churn: incremental throughout
     for wid in (0, 8, 56):
         assert (r.world_peers(wid) == o.world_peers(wid)).all()
 

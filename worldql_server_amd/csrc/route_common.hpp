@@ -68,6 +68,13 @@ __device__ __forceinline__ void flag_route(wq_route_counters* c, uint32_t* healt
     }
 }
 
+// Error bit 8: the table is missing an incremental batch the device could not apply (keys without
+// a packed form, list space); the next host call on the handle re-applies it (wq_delta.hip).
+constexpr uint32_t kErrStale = 8u;
+__device__ __forceinline__ void check_stale(const TableView& t, wq_route_counters* c, uint32_t* health) {
+    if (t.stale && *t.stale) flag_route(c, health, kErrStale, 0u);
+}
+
 struct RouteIn {
     const double* pos;
     const int64_t* keys;

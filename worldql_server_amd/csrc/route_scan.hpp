@@ -26,6 +26,7 @@ struct TileScanParams {
     uint64_t capacity;
     wq_route_counters* cnt;
     uint32_t* health;  // sticky {error, overflow} words (flag_route)
+    const uint32_t* stale = nullptr;  // the table's stale word (check_stale)
 };
 
 __device__ __forceinline__ uint64_t wave_incl_scan_add64(uint64_t v, int lane) {
@@ -98,6 +99,7 @@ static __global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScan
         p.cnt->n_pairs = P;
         // u32 CSR offsets cannot hold more than 2^32-1 pairs: error bit 2
         flag_route(p.cnt, p.health, P > 0xFFFFFFFFull ? 2u : 0u, P > p.capacity ? 1u : 0u);
+        if (p.stale && *p.stale) flag_route(p.cnt, p.health, kErrStale, 0u);
     }
 }
 
@@ -125,6 +127,7 @@ static __global__ __launch_bounds__(kBlock) void tile_finish_kernel(TileScanPara
         p.offsets[p.M] = (uint32_t)P;
         p.cnt->n_pairs = P;
         flag_route(p.cnt, p.health, P > 0xFFFFFFFFull ? 2u : 0u, P > p.capacity ? 1u : 0u);
+        if (p.stale && *p.stale) flag_route(p.cnt, p.health, kErrStale, 0u);
     }
 }
 

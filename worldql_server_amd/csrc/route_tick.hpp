@@ -257,6 +257,7 @@ __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
             p.cnt->n_pairs = P;
             // u32 CSR offsets cannot hold more than 2^32-1 pairs: error bit 2
             flag_route(p.cnt, p.health, P > 0xFFFFFFFFull ? 2u : 0u, P > p.out.capacity ? 1u : 0u);
+            check_stale(tv, p.cnt, p.health);
         }
         if (__any(gave_up) && lane == 0) flag_route(p.cnt, p.health, kErrSpin, 0u);
         if (lane == 0) sm.pre = pre;

@@ -4,25 +4,27 @@
 // Same semantics as the full rebuild in wq_table.hip — per (world, cube, peer) the last op of the
 // batch wins (AreaMap::add_subscription / remove_subscription, area_map.rs:72-119, applied in
 // order by thread.rs:122-146) — but the work is proportional to the batch and the cubes it
-// touches, not to the whole table. The group path (default):
-//   events   each op -> packed cube key and its record slot (a new cube claims its record here by
-//            CAS on the probe path, count 0), and a value kind << 32 | peer
-//   sort     one stable radix sort of the values by slot over log2(capacity) bits: every cube's
-//            ops are contiguous and in op order
-//   plan     one lane per touched cube reads the record header and reserves relocation space for
-//            old count + subscribes beyond the list's capacity (one host read-back of the totals)
-//   apply    16 lanes per cube merge the cube's ops (16 at a time, sorted by (peer, op) in
-//            registers, last op of a peer wins) into its list staged in LDS, then write the list
-//            (in place, or relocated past the used part of `list` with 50% headroom) and the whole
-//            record line (count, offset, capacity, Bloom signature, inline peers)
-// Cubes beyond the group bounds (old count + ops > 128) send the batch to the per-lane path:
-// sort by (slot, peer), one lane per cube, in-place forward compaction then backward merge.
+// touches, not to the whole table. Three steps, no host read-back between them:
+//   events   each op -> packed cube key and its record slot (a new cube claims its record here,
+//            count 0); the op becomes one u64 sort key  slot << 33 | kind << 32 | peer
+//   bucket   one stable rocPRIM radix sort over the slot's high 16 bits: a bucket (2^lowbits
+//            adjacent slots, ~100-200 ops at C5) is contiguous, in op order
+//   apply    one wave per bucket: the bucket's ops (windows of 256) sorted in registers by (slot,
+//            peer, op) with a bitonic network, then one LANE per touched cube: it stages the cube's
+//            list in LDS, counts adds / removes (the last op of a peer wins), merges straight into
+//            the list (in place, or relocated to bump-allocated space when it outgrows its
+//            capacity) and rewrites the record's count, signature, capacity and inline peers.
+//            Cubes with more than kLaneList peers go to the whole wave (ranks by binary search).
 // A cube that empties keeps its record (count 0, key kept), so every probe sequence stays intact.
 // The sorted state `st` and the any-keys are left stale and regenerated from the records only
-// when something needs them (table_materialize / table_ensure_any). A batch falls back to the full
-// rebuild (no list changed) when an op is not regular, relocations would overflow `list`, or the
-// record table would pass load 1/4.
+// when something needs them (table_materialize / table_ensure_any). A batch holding an op without
+// a packed key is not applied (the caller rebuilds); one whose relocations would overflow `list`
+// is applied except for the cubes that did not fit — re-applying the whole batch in the rebuild
+// is exact, since a batch fixes the final state of every (cube, peer) it touches.
 #include <algorithm>
+#include <cstdlib>
+#include <cstdio>
+#include <vector>
 
 #include "table_prims.hpp"
 
@@ -30,14 +32,13 @@ namespace wq {
 
 namespace {
 
-struct DeltaSummary {
-    uint64_t d_entries;    // two's complement: adds - removes
-    uint64_t d_live;       // two's complement: cubes that became non-empty - cubes that emptied
-    uint64_t n_big;        // touched cubes too large for the wave path (lists > kWaveOld, > kWaveCh changes)
-    uint64_t reloc_words;  // list words to bump-allocate
-    uint64_t new_recs;     // records claimed by this batch's new cubes
-    uint32_t irregular;    // 1: an op without a packed key; 2: an invalid op (device batches)
-    uint32_t n_dc;         // touched cubes
+// Device-side status of one batch (read back once, after the apply).
+struct DeltaStatus {
+    uint32_t flags;     // 1: an op without a packed key; 2: an invalid op; 4: relocations overflowed `list`
+    uint32_t n_wave;    // cubes the wave path took
+    uint64_t new_recs;  // records claimed by this batch's new cubes
+    uint64_t bump;      // list words bump-allocated past t.list_used
+    uint64_t pad;
 };
 
 struct DeltaTable {
@@ -61,21 +62,21 @@ __device__ __forceinline__ void op_key(const wq_op& o, double sf, int64_t si, in
     }
 }
 
-// Per op: packed key, and the record slot of its cube — a cube the table does not hold yet gets
-// its record here (key claimed by compare-and-swap on the probe path, count 0), so the batch can
-// be grouped by slot with a short radix sort. The caller guarantees free slots (load <= 1/2).
+// Per op: packed key and the record slot of its cube — a cube the table does not hold yet gets
+// its record here, count 0 (the caller guarantees free slots: load <= 1/2).
 // Claim words (rclaim, one per record slot): 0 free, kClaiming while an op writes a new cube's key,
 // otherwise the slot holds a key — builds write the cube index + 2 (< 2^31), a delta batch writes
-// its tag (kBatchTag | batch number). The 96-bit key spans two words of the record, so a slot is
-// claimed through its claim word: the winner writes the key, then publishes the tag (release). A
-// key published before this launch is read with plain loads; only a slot tagged by this very
-// batch takes an acquire fence first (the one case where the key may still be in flight). An op
-// that finds a slot being claimed looks again (the winner's wave progresses meanwhile).
+// its tag (kBatchTag | batch number). The 96-bit key spans two words of the record: the claimer
+// writes both, then publishes its tag (release). A reader takes the record line first (one line
+// per op in the common case): its own key -> found; a visible other key -> the next slot, unless
+// this very batch is claiming or has claimed the slot (then the claim word decides, after an
+// acquire fence); ext == 0 -> the slot looks free, and the claim word is the arbiter.
 constexpr uint32_t kClaiming = 1u, kBatchTag = 0x80000000u;
+constexpr uint64_t kNoKey = ~0ull;  // an op without a record: sorts after every real slot
 
 __global__ void k_delta_events(const wq_op* __restrict__ ops, uint32_t n, double sf, int64_t si, Record* recs,
                                uint32_t* rclaim, uint32_t tag, uint64_t rmask, int rshift, uint64_t hmask,
-                               uint32_t* slot, uint32_t* peer, uint8_t* kind, uint64_t* sv, DeltaSummary* sum) {
+                               uint64_t* keys, DeltaStatus* status) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const wq_op o = ops[i];
@@ -83,229 +84,87 @@ __global__ void k_delta_events(const wq_op* __restrict__ ops, uint32_t n, double
     op_key(o, sf, si, k);
     uint64_t p = 0;
     uint32_t x = 0;
-    uint32_t sl = 0;  // ops without a record (the batch then falls back): slot 0, an in-bounds dummy
+    uint64_t key = kNoKey;
     if (o.kind > WQ_OP_UNSUBSCRIBE || o.world == WQ_WORLD_INVALID) {
-        atomicOr(&sum->irregular, 2u);  // bad op
+        atomicOr(&status->flags, 2u);  // bad op
     } else if (!pack_key(o.world, k[0], k[1], k[2], sf, &p, &x)) {
-        atomicOr(&sum->irregular, 1u);
+        atomicOr(&status->flags, 1u);
     } else {
         uint64_t j = slot_of(rec_hash(p, x) & hmask, rshift);
         for (;;) {
-            uint32_t c = __hip_atomic_load(&rclaim[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (c == 0) {
-                c = atomicCAS(&rclaim[j], 0u, kClaiming);
+            const uint32_t* line = reinterpret_cast<const uint32_t*>(recs + j);
+            uint64_t rp = *reinterpret_cast<const uint64_t*>(line);
+            uint32_t rx = line[7];
+            if (rp == p && rx == x) break;
+            uint32_t c;
+            if (rx == 0) {  // looks free: claim it (or learn who did)
+                c = __hip_atomic_load(&rclaim[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (c == 0) c = atomicCAS(&rclaim[j], 0u, kClaiming);
                 if (c == 0) {  // won: a new cube (count 0) with this key
                     recs[j].pk = p;
                     recs[j].ext = x;
                     __hip_atomic_store(&rclaim[j], tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    atomicAdd(reinterpret_cast<unsigned long long*>(&sum->new_recs), 1ull);
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&status->new_recs), 1ull);
                     break;
                 }
+            } else {  // another key is visible: final unless this batch is claiming the slot
+                c = __hip_atomic_load(&rclaim[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             if (c == kClaiming) continue;  // being claimed: look again
-            uint64_t rp;
-            uint32_t rx;
-            if (c == tag) {  // claimed by this batch: order the key loads after the tag
+            if (c == tag) {                // claimed by this batch: order the key loads after the tag
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 rp = __hip_atomic_load(&recs[j].pk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 rx = __hip_atomic_load(&recs[j].ext, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                rp = recs[j].pk;
-                rx = recs[j].ext;
+                if (rp == p && rx == x) break;
             }
-            if (rp == p && rx == x) break;
             j = (j + 1) & rmask;
         }
-        sl = (uint32_t)j;
+        key = (j << 33) | ((uint64_t)(o.kind == WQ_OP_SUBSCRIBE ? 1u : 0u) << 32) | o.peer;
     }
-    const uint32_t kd = o.kind == WQ_OP_SUBSCRIBE ? 1u : 0u;
-    slot[i] = sl;
-    peer[i] = o.peer;
-    kind[i] = (uint8_t)kd;
-    sv[i] = ((uint64_t)kd << 32) | o.peer;  // sorted along with the slot: no gather afterwards
+    keys[i] = key;
 }
 
-// Sorted order -> peer / kind columns and cube heads.
-__global__ void k_delta_mark(const uint32_t* __restrict__ order, const uint32_t* __restrict__ spk,
-                             const uint32_t* __restrict__ peer, const uint8_t* __restrict__ kind, uint32_t n,
-                             uint32_t* sp, uint8_t* skd, uint32_t* head) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t a = order[i];
-    sp[i] = peer[a];
-    skd[i] = kind[a];
-    head[i] = (i == 0 || spk[i] != spk[i - 1]) ? 1u : 0u;
-}
-
-__global__ void k_delta_cubes(const uint32_t* __restrict__ head, const uint32_t* __restrict__ cid, uint32_t n,
-                              uint32_t* cube_start, DeltaSummary* sum) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    if (head[i]) cube_start[cid[i] - 1] = i;
-    if (i == n - 1) {
-        sum->n_dc = cid[i];
-        cube_start[cid[i]] = n;
+// Bucket b = sorted keys whose slot >> lowbits is b: bstart[b] = first such index (b <= NBr;
+// bstart[NBr] ends the real slots, kNoKey ops follow).
+__global__ void k_bucket_bounds(const uint64_t* __restrict__ keys, uint32_t n, int lowbits, uint32_t NBr,
+                                uint32_t* bstart) {
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    if (b > NBr) return;
+    const int sh = 33 + lowbits;
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint64_t kb = keys[mid] >> sh;
+        if ((kb < NBr ? (uint32_t)kb : NBr) < b)
+            lo = mid + 1;
+        else
+            hi = mid;
     }
+    bstart[b] = lo;
 }
 
-// Last index of the (cube, peer) run starting at t.
-__device__ __forceinline__ uint32_t run_last(const uint32_t* sp, uint32_t t, uint32_t s1) {
-    while (t + 1 < s1 && sp[t + 1] == sp[t]) ++t;
-    return t;
-}
-
-__device__ __forceinline__ uint32_t grown(uint32_t n) { return n + n / 2 + 4; }
-
-__global__ __launch_bounds__(kBlock) void k_delta_plan(DeltaTable tb, const uint32_t* __restrict__ cube_start,
-                                                       const uint32_t* __restrict__ sslot,
-                                                       const uint32_t* __restrict__ sp,
-                                                       const uint8_t* __restrict__ skd, const DeltaSummary* sum,
-                                                       uint32_t n, uint4* plan, uint32_t* reloc, uint64_t* part) {
-    __shared__ unsigned long long acc[4];
-    if (threadIdx.x < 4) acc[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t n_dc = sum->n_dc;
-    uint32_t rw = 0;
-    if (c < n_dc) {
-        const uint32_t s0 = cube_start[c], s1 = cube_start[c + 1];
-        const uint32_t slot = sslot[s0];  // k_delta_events gave every cube of the batch its record
-        const Record& r = tb.recs[slot];
-        const uint32_t oc = r.count, off = r.list_off, cap = r.cap;
-        const uint32_t* old = tb.list + off + 1;
-        uint32_t adds = 0, rms = 0, j = 0;
-        for (uint32_t t = s0; t < s1;) {
-            const uint32_t l = run_last(sp, t, s1);
-            const uint32_t q = sp[l];
-            while (j < oc && old[j] < q) ++j;
-            const bool present = j < oc && old[j] == q;
-            if (skd[l])
-                adds += present ? 0u : 1u;
-            else
-                rms += present ? 1u : 0u;
-            t = l + 1;
-        }
-        const uint32_t nc = oc + adds - rms;
-        const bool changed = (adds | rms) != 0;
-        if (changed && nc > cap) rw = 1 + grown(nc);
-        plan[c] = make_uint4(slot, nc, changed ? 1u : 0u, oc);
-        const int64_t de = (int64_t)adds - (int64_t)rms;
-        const int64_t dl = (int64_t)(oc == 0 && nc > 0) - (int64_t)(oc > 0 && nc == 0);
-        if (de) atomicAdd(&acc[0], (unsigned long long)de);
-        if (dl) atomicAdd(&acc[1], (unsigned long long)dl);
-        if (rw) atomicAdd(&acc[3], (unsigned long long)rw);
-    }
-    if (c < n) reloc[c] = rw;
-    __syncthreads();
-    if (threadIdx.x < 4) part[4ull * blockIdx.x + threadIdx.x] = acc[threadIdx.x];
-}
-
-__global__ __launch_bounds__(kBlock) void k_delta_reduce(const uint64_t* __restrict__ part, uint32_t nb,
-                                                         DeltaSummary* sum) {
-    __shared__ unsigned long long acc[4];
-    if (threadIdx.x < 4) acc[threadIdx.x] = 0;
-    __syncthreads();
-    unsigned long long v[4] = {0, 0, 0, 0};
-    for (uint32_t b = threadIdx.x; b < nb; b += kBlock)
+// End of a batch, one thread: snapshot {status, stat deltas} for the host (one copy to pinned
+// memory), zero both for the next batch, mark the table stale if the batch was not fully applied
+// (the host re-applies it), and switch the peer boxes off (subscribes may widen them; per-op box
+// atomics cost more than they save, so the count pass searches every long list until the next
+// build).
+__global__ void k_delta_finish(DeltaStatus* status, int64_t* dstat, uint64_t* snap, uint32_t* stale,
+                               uint32_t* pbox_valid) {
+    const uint64_t* sw = reinterpret_cast<const uint64_t*>(status);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] += part[4ull * b + k];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (v[k]) atomicAdd(&acc[k], v[k]);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        sum->d_entries = acc[0];
-        sum->d_live = acc[1];
-        sum->n_big = acc[2];
-        sum->reloc_words = acc[3];
-    }
+    for (int i = 0; i < 4; ++i) snap[i] = sw[i];
+    snap[4] = (uint64_t)dstat[0];
+    snap[5] = (uint64_t)dstat[1];
+    if (status->flags) *stale = 1u;
+    if (pbox_valid) *pbox_valid = 0u;
+    *status = DeltaStatus{};
+    dstat[0] = 0;
+    dstat[1] = 0;
 }
 
-__global__ __launch_bounds__(kBlock) void k_delta_apply(DeltaTable tb, const uint32_t* __restrict__ cube_start,
-                                                        const uint32_t* __restrict__ sp,
-                                                        const uint8_t* __restrict__ skd, const DeltaSummary* sum,
-                                                        const uint4* __restrict__ plan,
-                                                        const uint32_t* __restrict__ reloc,
-                                                        const uint32_t* __restrict__ reloc_off, uint64_t list_base) {
-    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
-    if (c >= sum->n_dc) return;
-    const uint4 pl = plan[c];
-    if (!pl.z) return;
-    const uint32_t s0 = cube_start[c], s1 = cube_start[c + 1];
-    const uint32_t nc = pl.y, oc = pl.w;
-    uint64_t slot = pl.x;
-    uint32_t off = 0, cap = 0;
-    if (pl.x == kNone) return;  // unreachable: k_delta_events gave every cube of the batch a record
-    off = tb.recs[slot].list_off;
-    cap = tb.recs[slot].cap;
-    uint32_t* L = tb.list;
-    if (reloc[c]) {  // forward merge of the old list and the changes into new space
-        const uint32_t dst = (uint32_t)(list_base + reloc_off[c]);
-        const uint32_t* old = L + off + 1;
-        uint32_t* out = L + dst + 1;
-        uint32_t i = 0, w = 0, t = s0;
-        while (i < oc || t < s1) {
-            if (t < s1) {
-                const uint32_t l = run_last(sp, t, s1);
-                const uint32_t q = sp[l];
-                while (i < oc && old[i] < q) out[w++] = old[i++];
-                const bool present = i < oc && old[i] == q;
-                if (present) ++i;
-                if (skd[l]) out[w++] = q;  // subscribed after the batch (kept or added)
-                t = l + 1;
-            } else {
-                out[w++] = old[i++];
-            }
-        }
-        off = dst;
-        cap = reloc[c] - 1;
-    } else {  // in place: compact the removals forward, then merge the adds backward
-        uint32_t* a = L + off + 1;
-        uint32_t w = 0, t = s0;
-        for (uint32_t i = 0; i < oc; ++i) {
-            const uint32_t x = a[i];
-            while (t < s1 && sp[t] < x) t = run_last(sp, t, s1) + 1;
-            bool rm = false;
-            if (t < s1 && sp[t] == x) rm = skd[run_last(sp, t, s1)] == 0;
-            if (!rm) a[w++] = x;
-        }
-        int64_t i = (int64_t)w - 1;
-        uint32_t k = nc;
-        for (int64_t u = (int64_t)s1 - 1; u >= (int64_t)s0;) {
-            const uint32_t q = sp[u];
-            const bool sub = skd[u] != 0;  // u is the last op of its run
-            while (u >= (int64_t)s0 && sp[u] == q) --u;
-            if (!sub) continue;
-            while (i >= 0 && a[i] > q) a[--k] = a[i--];
-            if (i >= 0 && a[i] == q) continue;  // already subscribed
-            a[--k] = q;
-        }
-    }
-    L[off] = nc;
-    const uint32_t* a = L + off + 1;
-    uint64_t sig = 0;
-    for (uint32_t j = 0; j < nc; ++j) sig |= peer_sig(a[j]);
-    Record& r = tb.recs[slot];  // the key (pk, ext) stays as claimed
-    r.count = nc;
-    r.list_off = off;
-    r.sig = sig;
-    r.cap = cap;
-#pragma unroll 4
-    for (int j = 0; j < kInline; ++j) r.peers[j] = (uint32_t)j < nc ? a[j] : kNone;
-}
-
-// ---- the group path: 16 lanes per touched cube ------------------------------------------------
-// The batch is grouped by record slot (one radix sort over log2(capacity) bits). A light plan reads
-// only each touched cube's record header and reserves relocation space for an upper bound (old
-// count + changes). Then a group of 16 lanes per cube stages the list in LDS (old count + changes
-// <= kGroupList), takes the cube's changes in op order 16 at a time, sorts each chunk by (peer, op)
-// with a bitonic network in registers (the last op of a peer wins within the chunk, chunks apply in
-// order), merges adds and removes into the other LDS buffer by rank, and finally writes the list
-// and the record line with coalesced stores. A batch holding a cube beyond the bound takes the
-// per-lane path above.
+// ---- shared helpers (bucket apply, REMOVE_PEER) ---------------------------------------------
 constexpr int kG = 16;
 constexpr int kGroups = kBlock / kG;
-constexpr uint32_t kGroupList = 128;
 constexpr uint32_t kGroupGrid = 2048;
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -326,218 +185,7 @@ __device__ __forceinline__ uint32_t lds_lower_bound(const uint32_t* a, uint32_t 
     return lo;
 }
 
-__global__ void k_slot_heads(const uint32_t* __restrict__ sslot, uint32_t n, uint32_t* head) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) head[i] = (i == 0 || sslot[i] != sslot[i - 1]) ? 1u : 0u;
-}
-
-// One lane per touched cube: {slot, first op, ops, old count} and the relocation reserve.
-__global__ __launch_bounds__(kBlock) void k_delta_plan_light(const Record* __restrict__ recs,
-                                                             const uint32_t* __restrict__ cube_start,
-                                                             const uint32_t* __restrict__ sslot,
-                                                             const uint64_t* __restrict__ svs,
-                                                             const DeltaSummary* sum, uint32_t n, uint4* cinfo,
-                                                             uint32_t* reloc, uint64_t* part) {
-    __shared__ unsigned long long acc[4];
-    if (threadIdx.x < 4) acc[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
-    uint32_t rw = 0;
-    if (c < sum->n_dc) {
-        const uint32_t s0 = cube_start[c], nch = cube_start[c + 1] - s0;
-        const uint32_t slot = sslot[s0];
-        const uint4* line = reinterpret_cast<const uint4*>(recs + slot);
-        const uint32_t oc = line[0].z, cap = line[1].z;
-        uint32_t subs = 0;  // only subscribes can grow the list
-        for (uint32_t t = s0; t < s0 + nch; ++t) subs += (uint32_t)(svs[t] >> 32);
-        if ((uint64_t)oc + nch > kGroupList) atomicAdd(&acc[2], 1ull);
-        const uint64_t ub = (uint64_t)oc + subs;
-        if (ub > cap) rw = 1 + grown((uint32_t)std::min<uint64_t>(ub, 0x7FFFFFFFull));
-        cinfo[c] = make_uint4(slot, s0, nch, oc);
-        if (rw) atomicAdd(&acc[3], (unsigned long long)rw);
-    }
-    if (c < n) reloc[c] = rw;
-    __syncthreads();
-    if (threadIdx.x < 4) part[4ull * blockIdx.x + threadIdx.x] = acc[threadIdx.x];
-}
-
-struct GroupLds {
-    uint32_t buf[kGroups][2][kGroupList];
-    uint32_t add[kGroups][kG];
-    uint32_t rem[kGroups][kG];
-};
-
-__global__ __launch_bounds__(kBlock) void k_delta_apply_group(DeltaTable tb, const uint4* __restrict__ cinfo,
-                                                              const uint64_t* __restrict__ svs,
-                                                              const DeltaSummary* sum,
-                                                              const uint32_t* __restrict__ reloc,
-                                                              const uint32_t* __restrict__ reloc_off,
-                                                              uint64_t list_base, uint64_t* part) {
-    __shared__ GroupLds sm;
-    __shared__ unsigned long long acc[2];
-    if (threadIdx.x < 2) acc[threadIdx.x] = 0;
-    __syncthreads();
-    const int lane = threadIdx.x & 63, gl = threadIdx.x & (kG - 1), grp = threadIdx.x / kG;
-    const int gshift = lane & ~(kG - 1);
-    const uint32_t lt = (1u << gl) - 1u;
-    const uint32_t n_dc = sum->n_dc;
-    int64_t de = 0, dl = 0;
-    uint32_t* add = sm.add[grp];
-    uint32_t* rem = sm.rem[grp];
-    const uint32_t stride = gridDim.x * kGroups;
-    const uint4* recs4 = reinterpret_cast<const uint4*>(tb.recs);
-    uint32_t c = blockIdx.x * kGroups + grp;
-    // Software pipeline over the group's cubes c, c + stride, ...: while cube c merges, the next
-    // cube's list (<= kGroupList words: kPref per lane) is in flight in registers and the header
-    // of the one after it is being fetched, so a cube's list latency is paid once per group, not
-    // once per cube. (Lists of different cubes are disjoint, and a relocated list moves to fresh
-    // space, so prefetching never reads words this group or another is about to write.)
-    constexpr int kPref = (int)(kGroupList / kG);
-    uint4 ci = make_uint4(0, 0, 0, 0), h0 = ci, h1 = ci, ci_n = ci, h0_n = ci, h1_n = ci;
-    uint32_t pref[kPref];
-    if (c < n_dc) {
-        ci = cinfo[c];
-        if (c + stride < n_dc) ci_n = cinfo[c + stride];
-        h0 = recs4[8ull * ci.x];
-        h1 = recs4[8ull * ci.x + 1];
-        if (c + stride < n_dc) {
-            h0_n = recs4[8ull * ci_n.x];
-            h1_n = recs4[8ull * ci_n.x + 1];
-        }
-#pragma unroll
-        for (int k = 0; k < kPref; ++k) {
-            const uint32_t i = (uint32_t)(gl + k * kG);
-            pref[k] = i < ci.w ? tb.list[h0.w + 1 + i] : 0u;
-        }
-    }
-    for (; c < n_dc; c += stride) {
-        const uint32_t cn = c + stride, cnn = c + 2 * stride;
-        uint4 ci_nn = ci_n;
-        if (cnn < n_dc) ci_nn = cinfo[cnn];
-        const uint32_t slot = ci.x, s0 = ci.y, nch = ci.z, oc = ci.w;
-        Record* rec = tb.recs + slot;
-        const uint32_t off = h0.w, cap0 = h1.z;
-        uint32_t* cur = sm.buf[grp][0];
-        uint32_t* nxt = sm.buf[grp][1];
-        wave_lds_sync();  // the previous cube's LDS reads are done
-#pragma unroll
-        for (int k = 0; k < kPref; ++k) {
-            const uint32_t i = (uint32_t)(gl + k * kG);
-            if (i < oc) cur[i] = pref[k];
-        }
-        if (cn < n_dc) {  // the next cube's list (its header arrived during the previous cube)
-#pragma unroll
-            for (int k = 0; k < kPref; ++k) {
-                const uint32_t i = (uint32_t)(gl + k * kG);
-                pref[k] = i < ci_n.w ? tb.list[h0_n.w + 1 + i] : 0u;
-            }
-        }
-        uint4 h0_nn = h0_n, h1_nn = h1_n;
-        if (cnn < n_dc) {
-            h0_nn = recs4[8ull * ci_nn.x];
-            h1_nn = recs4[8ull * ci_nn.x + 1];
-        }
-        wave_lds_sync();
-        uint32_t n = oc;
-        bool changed = false;
-        for (uint32_t t0 = 0; t0 < nch; t0 += kG) {
-            const uint32_t m = std::min<uint32_t>(kG, nch - t0);
-            const bool has = (uint32_t)gl < m;
-            const uint64_t v = has ? svs[s0 + t0 + gl] : 0ull;
-            uint64_t key = has ? ((v << 32) | (uint32_t)gl) : ~0ull;
-            const uint32_t kd = (uint32_t)(v >> 32);
-#pragma unroll
-            for (int k = 2; k <= kG; k <<= 1) {
-#pragma unroll
-                for (int j = k >> 1; j > 0; j >>= 1) {
-                    const uint64_t o = __shfl_xor(key, j, kG);
-                    const bool keep_min = ((gl & j) == 0) == ((gl & k) == 0);
-                    key = keep_min ? (o < key ? o : key) : (o > key ? o : key);
-                }
-            }
-            const uint32_t q = (uint32_t)(key >> 32);
-            const bool sub = __shfl(kd, (int)((uint32_t)key & (kG - 1)), kG) != 0;
-            const uint32_t qn = __shfl(q, (gl + 1) & (kG - 1), kG);
-            const bool last = has && ((uint32_t)gl == m - 1 || qn != q);
-            const uint32_t at = last ? lds_lower_bound(cur, n, q) : 0u;
-            const bool present = last && at < n && cur[at] == q;
-            const bool is_add = last && sub && !present, is_rm = last && !sub && present;
-            const uint32_t ga = (uint32_t)(__ballot(is_add) >> gshift) & 0xFFFFu;
-            const uint32_t gr = (uint32_t)(__ballot(is_rm) >> gshift) & 0xFFFFu;
-            const uint32_t nadd = (uint32_t)__popc(ga), nrm = (uint32_t)__popc(gr);
-            if (!(nadd | nrm)) continue;
-            changed = true;
-            const uint32_t add_rank = (uint32_t)__popc(ga & lt);
-            if (is_add) add[add_rank] = q;
-            if (is_rm) rem[__popc(gr & lt)] = q;
-            wave_lds_sync();
-            for (uint32_t k = gl; k < n; k += kG) {  // kept peers shift by the removals / adds below them
-                const uint32_t x = cur[k];
-                const uint32_t r = lds_lower_bound(rem, nrm, x);
-                if (r < nrm && rem[r] == x) continue;
-                nxt[k - r + lds_lower_bound(add, nadd, x)] = x;
-            }
-            if (is_add) nxt[add_rank + at - lds_lower_bound(rem, nrm, q)] = q;
-            wave_lds_sync();
-            uint32_t* t = cur;
-            cur = nxt;
-            nxt = t;
-            n = n + nadd - nrm;
-        }
-        if (changed) {
-        uint32_t dst = off, cap = cap0;
-        const uint32_t rl = reloc[c];
-        if (rl) {
-            dst = (uint32_t)(list_base + reloc_off[c]);
-            cap = rl - 1;
-        }
-        uint32_t* L = tb.list + dst;
-        uint64_t sig = 0;
-        for (uint32_t k = gl; k < n; k += kG) {
-            const uint32_t v = cur[k];
-            L[1 + k] = v;
-            sig |= peer_sig(v);
-        }
-#pragma unroll
-        for (int d = kG / 2; d >= 1; d >>= 1) sig |= __shfl_xor(sig, d, kG);
-        if (gl == 0) L[0] = n;
-        uint32_t* rw = reinterpret_cast<uint32_t*>(rec);  // the record line: 32 words, two per lane
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int w = gl + h * kG;
-            uint32_t v;
-            switch (w) {
-                case 0: v = h0.x; break;
-                case 1: v = h0.y; break;
-                case 2: v = n; break;
-                case 3: v = dst; break;
-                case 4: v = (uint32_t)sig; break;
-                case 5: v = (uint32_t)(sig >> 32); break;
-                case 6: v = cap; break;
-                case 7: v = h1.w; break;  // ext: the key's high word
-                default: v = (uint32_t)(w - kInlineWord0) < n ? cur[w - kInlineWord0] : kNone; break;
-            }
-            rw[w] = v;
-        }
-        if (gl == 0) {
-            de += (int64_t)n - (int64_t)oc;
-            dl += (int64_t)(oc == 0 && n > 0) - (int64_t)(oc > 0 && n == 0);
-        }
-        }  // changed
-        ci = ci_n;
-        h0 = h0_n;
-        h1 = h1_n;
-        ci_n = ci_nn;
-        h0_n = h0_nn;
-        h1_n = h1_nn;
-    }
-    if (de) atomicAdd(&acc[0], (unsigned long long)de);
-    if (dl) atomicAdd(&acc[1], (unsigned long long)dl);
-    __syncthreads();
-    if (threadIdx.x < 2) part[2ull * blockIdx.x + threadIdx.x] = acc[threadIdx.x];
-}
-
-// Adds the group path's per-block entry / live-cube deltas into the running totals.
+// Adds per-block entry / live-cube deltas (REMOVE_PEER) into the running totals.
 __global__ __launch_bounds__(kBlock) void k_delta_stats(const uint64_t* __restrict__ part, uint32_t nb,
                                                         uint64_t* dstat) {
     __shared__ unsigned long long acc[2];
@@ -554,6 +202,530 @@ __global__ __launch_bounds__(kBlock) void k_delta_stats(const uint64_t* __restri
     if (threadIdx.x == 0) {
         dstat[0] += acc[0];
         dstat[1] += acc[1];
+    }
+}
+
+
+// ---- the bucket apply: one wave per bucket, one lane per touched cube ------------------------
+constexpr int kWin = 256;        // ops per window (a bucket's ops are taken in op-order windows)
+constexpr int kLaneList = 256;         // old lists longer than this go to the wave path
+constexpr uint32_t kRoundWords = 1024;  // a round stages at most this many old-list words (and 64 cubes)
+constexpr uint32_t kWaveList = kRoundWords;  // the wave path stages lists up to this in LDS
+
+__device__ __forceinline__ uint32_t grown(uint32_t n) { return n + n / 2 + 4; }
+
+struct BucketLds {
+    uint64_t op[kWin];              // the window's ops, sorted: slot_lo << 48 | peer << 16 | pos << 8 | kind
+    uint32_t lst[kRoundWords];      // a round's staged old lists (flat), or the wave path's one list
+    union {
+        struct {                    // a round
+            uint8_t own[kRoundWords];  // staged word -> its cube (round-local)
+            uint8_t rmf[kRoundWords];  // staged word removed
+            uint8_t fl[kWin];          // per op: 1 add / 2 remove
+            uint16_t at[kWin];         // per op: #old peers below it
+            uint16_t pa[kWin + 1];     // exclusive prefix of add flags over the round's ops
+            uint16_t pr[kWin + 1];     // exclusive prefix of remove flags
+        } r;
+        uint32_t ar[2 * kWin];      // wave path: the cube's adds [0, kWin) and removes [kWin, 2 kWin)
+    } u;
+    uint64_t csig[64];              // round: per cube, OR of peer_sig over its new list
+    uint32_t cpre[65];              // round: per cube, first staged word
+    uint32_t cdst[64];              // round: per cube, where the new list goes (kNone: unchanged)
+    uint16_t cs[kWin + 1];          // cube starts in op[]
+    uint16_t big[kWin];             // cubes (cs index) the wave path takes
+    uint8_t cid[kWin];              // per op: its cube (window-local index mod 256)
+};
+
+// Bitonic sort of 64 * E u64 held strided (element r * 64 + lane in a[r]) by one wave, ascending.
+template <int E>
+__device__ __forceinline__ void wave_bitonic(uint64_t (&a)[4], int lane) {
+    constexpr int P = 64 * E;
+#pragma unroll
+    for (int k = 2; k <= P; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {  // partner: same lane, register r ^ (j / 64)
+#pragma unroll
+                for (int r = 0; r < E; ++r) {
+                    const int r2 = r ^ (j >> 6);
+                    if (r2 > r) {
+                        const bool up = ((r * 64 + lane) & k) == 0;
+                        const uint64_t x = a[r], y = a[r2];
+                        const bool sw = up ? (x > y) : (x < y);
+                        a[r] = sw ? y : x;
+                        a[r2] = sw ? x : y;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < E; ++r) {
+                    const uint64_t o = __shfl_xor(a[r], j, 64);
+                    const bool up = ((r * 64 + lane) & k) == 0;
+                    const bool keep_min = ((lane & j) == 0) == up;
+                    a[r] = keep_min ? (o < a[r] ? o : a[r]) : (o > a[r] ? o : a[r]);
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t op_peer(uint64_t x) { return (uint32_t)(x >> 16); }
+
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+// Record words 2..6 {count, list_off, sig lo, sig hi, cap} of slot.
+__device__ __forceinline__ void write_header(Record* rec, uint32_t nc, uint32_t off, uint64_t sig, uint32_t cap) {
+    uint32_t* rw = reinterpret_cast<uint32_t*>(rec);
+    *reinterpret_cast<uint2*>(rw + 2) = make_uint2(nc, off);
+    *reinterpret_cast<uint2*>(rw + 4) = make_uint2((uint32_t)sig, (uint32_t)(sig >> 32));
+    rw[6] = cap;
+}
+
+struct BucketArgs {
+    DeltaTable tb;
+    const uint64_t* keys;    // sorted by slot >> lowbits, stable
+    const uint32_t* bstart;  // [NBr + 1]
+    int lowbits;
+    DeltaStatus* status;
+    int64_t* dstat;          // running {entries, live cubes} deltas
+    uint64_t list_base;      // first free list word (t.list_used)
+    uint64_t list_room;      // words available past list_base
+    uint32_t dbg;            // timing experiments only (WQ_DELTA_DBG): 2 no merge, 4 no sort
+    uint64_t* stamps;        // diagnostics (WQ_DELTA_STAMPS): per bucket, cycles per phase
+};
+
+// Diagnostic phase stamps of the bucket apply (lane 0 of each wave; WQ_DELTA_STAMPS only).
+#define WQ_STAMP(k)                                                            \
+    do {                                                                       \
+        if (a.stamps && lane == 0) {                                           \
+            const uint64_t t_now = __builtin_amdgcn_s_memtime();               \
+            a.stamps[(uint64_t)blockIdx.x * 16 + (k)] += t_now - t_last;       \
+            t_last = t_now;                                                    \
+        }                                                                      \
+    } while (0)
+
+// Relocation space for `want` words (overflow: kNone, flag 4 — the cube is left unchanged).
+__device__ __forceinline__ uint32_t bump_alloc(const BucketArgs& a, uint32_t want) {
+    const uint64_t d = atomicAdd(reinterpret_cast<unsigned long long*>(&a.status->bump), (unsigned long long)want);
+    if (d + want > a.list_room) {
+        atomicOr(&a.status->flags, 4u);
+        return kNone;
+    }
+    return (uint32_t)(a.list_base + d);
+}
+
+__global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
+    __shared__ BucketLds sm;
+    if (a.status->flags & 3u) return;  // an op without a record: nothing applied, the rebuild takes the batch
+    const int lane = threadIdx.x;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t B = blockIdx.x;
+    const uint32_t s = a.bstart[B], e = a.bstart[B + 1];
+    uint64_t t_last = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+    const uint64_t lowmask = (1ull << a.lowbits) - 1ull;
+    uint32_t* L = a.tb.list;
+    int64_t de = 0, dl = 0;
+    uint32_t nwave = 0;
+    for (uint32_t w0 = s; w0 < e; w0 += kWin) {
+        if (w0 != s) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // this wave's own earlier writes: same CU, same L2
+        const uint32_t cnt = min((uint32_t)kWin, e - w0);
+        uint64_t v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t q = r * 64 + lane;
+            if (q < cnt) {
+                const uint64_t k = a.keys[w0 + q];
+                v[r] = (((k >> 33) & lowmask) << 48) | ((uint64_t)(uint32_t)k << 16) | ((uint64_t)q << 8) |
+                       ((k >> 32) & 1u);
+            } else {
+                v[r] = ~0ull;
+            }
+        }
+        if (a.dbg & 4u)
+            ;
+        else if (cnt <= 64)
+            wave_bitonic<1>(v, lane);
+        else if (cnt <= 128)
+            wave_bitonic<2>(v, lane);
+        else
+            wave_bitonic<4>(v, lane);
+        WQ_STAMP(0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm.op[r * 64 + lane] = v[r];
+        wave_lds_sync();
+        // cube heads -> cs
+        uint32_t ncub = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t q = r * 64 + lane;
+            const bool hd = q < cnt && (q == 0 || (sm.op[q] >> 48) != (sm.op[q - 1] >> 48));
+            const uint64_t m = __ballot(hd);
+            if (hd) sm.cs[ncub + __popcll(m & lt)] = (uint16_t)q;
+            if (q < cnt) sm.cid[q] = (uint8_t)(ncub + __popcll(m & (lt | (1ull << lane))) - 1);
+            ncub += (uint32_t)__popcll(m);
+        }
+        if (lane == 0) sm.cs[ncub] = (uint16_t)cnt;
+        WQ_STAMP(1);
+        wave_lds_sync();
+        // ---- rounds of up to 64 cubes, data-parallel ----
+        // One lane per cube reads its header; the round's old lists are staged flat into LDS; each
+        // op (the last of its peer run decides) finds its peer by binary search in its cube's
+        // list; ballot prefixes over the ops give every peer's new index (old index - removes
+        // below + adds below); kept and added peers are written straight to their places in the
+        // (in-place or relocated) list and the record's inline words; one lane per cube finishes
+        // the header. Lists longer than kLaneList go to the wave path below.
+        uint32_t nbig = 0;
+        for (uint32_t c0 = 0, n_round = 0; c0 < ncub; c0 += n_round) {
+            const uint32_t c = c0 + lane;
+            bool act = c < ncub;
+            uint32_t slot = 0, oc = 0, off = 0, cap = 0;
+            if (act) {
+                slot = (B << a.lowbits) | (uint32_t)(sm.op[sm.cs[c]] >> 48);
+                const uint32_t* rw = reinterpret_cast<const uint32_t*>(a.tb.recs + slot);
+                const uint2 cw = *reinterpret_cast<const uint2*>(rw + 2);
+                oc = cw.x;
+                off = cw.y;
+                cap = rw[6];
+            }
+            bool isbig = act && oc > (uint32_t)kLaneList;
+            uint32_t oc_st = isbig ? 0u : oc;
+            const uint32_t incl = wave_incl_scan_u32(oc_st, lane);
+            // the round: the cubes whose staged words fit kRoundWords (at least one: oc <= kLaneList)
+            n_round = (uint32_t)__popcll(__ballot(act && incl <= kRoundWords));
+            act = act && (uint32_t)lane < n_round;
+            isbig = isbig && act;
+            oc_st = act ? oc_st : 0u;
+            const uint32_t pre = incl - oc_st;
+            if (act) sm.cpre[lane] = pre;
+            if (lane == (int)n_round - 1) sm.cpre[n_round] = incl;
+            const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)n_round - 1);
+            const uint32_t qa0 = sm.cs[c0], qb0 = sm.cs[c0 + n_round];
+            wave_lds_sync();
+            WQ_STAMP(2);
+            // stage the round's old lists flat: word x belongs to the cube u with cpre[u] <= x
+            for (uint32_t x0 = 0; x0 < T; x0 += 64 * 8) {
+                uint32_t val[8], uu[8];
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const uint32_t x = x0 + r * 64 + lane;
+                    uint32_t lo = 0, hi = n_round - 1;  // last u with cpre[u] <= x
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi + 1) >> 1;
+                        if (sm.cpre[mid] <= x) lo = mid; else hi = mid - 1;
+                    }
+                    uu[r] = lo;
+                    const uint32_t off_u = (uint32_t)__shfl((int)off, (int)lo, 64);
+                    val[r] = x < T ? L[off_u + 1 + (x - sm.cpre[lo])] : 0u;
+                }
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const uint32_t x = x0 + r * 64 + lane;
+                    if (x < T) {
+                        sm.lst[x] = val[r];
+                        sm.u.r.own[x] = (uint8_t)uu[r];
+                        sm.u.r.rmf[x] = 0;
+                    }
+                }
+            }
+            wave_lds_sync();
+            WQ_STAMP(3);
+            // per op of the round: the deciding op of each peer run, present or not
+            for (uint32_t q0 = qa0; q0 < qb0; q0 += 64) {
+                const uint32_t q = q0 + lane;
+                uint8_t f = 0;
+                uint16_t atq = 0;
+                if (q < qb0) {
+                    const uint64_t x = sm.op[q];
+                    const uint32_t pp = op_peer(x);
+                    const bool last = q + 1 == qb0 || (sm.op[q + 1] >> 16) != (x >> 16);  // cube and peer
+                    const uint32_t lo = (uint32_t)sm.cid[q] - c0;  // the op's cube within the round
+                    const uint32_t b0 = sm.cpre[lo], n0 = sm.cpre[lo + 1] - b0;
+                    const bool small = !((uint32_t)__shfl((int)isbig, (int)lo, 64));
+                    if (last && small) {
+                        uint32_t l2 = 0, h2 = n0;
+                        while (l2 < h2) {
+                            const uint32_t mid = (l2 + h2) >> 1;
+                            if (sm.lst[b0 + mid] < pp) l2 = mid + 1; else h2 = mid;
+                        }
+                        const bool present = l2 < n0 && sm.lst[b0 + l2] == pp;
+                        atq = (uint16_t)l2;
+                        if ((x & 1u) && !present) f = 1;
+                        if (!(x & 1u) && present) {
+                            f = 2;
+                            sm.u.r.rmf[b0 + l2] = 1;
+                        }
+                    }
+                    sm.u.r.fl[q - qa0] = f;
+                    sm.u.r.at[q - qa0] = atq;
+                }
+            }
+            WQ_STAMP(4);
+            // exclusive prefixes of the add / remove flags over the round's ops
+            {
+                uint32_t ra = 0, rr = 0;
+                for (uint32_t q0 = 0; q0 < qb0 - qa0; q0 += 64) {
+                    const uint32_t q = q0 + lane;
+                    const uint8_t f = q < qb0 - qa0 ? sm.u.r.fl[q] : 0;
+                    const uint64_t ma = __ballot(f == 1), mr = __ballot(f == 2);
+                    if (q < qb0 - qa0) {
+                        sm.u.r.pa[q] = (uint16_t)(ra + __popcll(ma & lt));
+                        sm.u.r.pr[q] = (uint16_t)(rr + __popcll(mr & lt));
+                    }
+                    ra += (uint32_t)__popcll(ma);
+                    rr += (uint32_t)__popcll(mr);
+                }
+                if (lane == 0) {
+                    sm.u.r.pa[qb0 - qa0] = (uint16_t)ra;
+                    sm.u.r.pr[qb0 - qa0] = (uint16_t)rr;
+                }
+            }
+            wave_lds_sync();
+            WQ_STAMP(5);
+            // one lane per cube: new count, destination
+            uint32_t nc = oc, dst = kNone, ncap = cap;
+            if (act && !isbig) {
+                const uint32_t s0 = sm.cs[c] - qa0, s1 = sm.cs[c + 1] - qa0;
+                const uint32_t nadd = sm.u.r.pa[s1] - sm.u.r.pa[s0], nrm = sm.u.r.pr[s1] - sm.u.r.pr[s0];
+                nc = oc + nadd - nrm;
+                if (nadd | nrm) {
+                    dst = off;
+                    if (nc > cap) {
+                        ncap = grown(nc);
+                        dst = bump_alloc(a, 1 + ncap);
+                    }
+                    if (dst != kNone) {
+                        de += (int64_t)nc - (int64_t)oc;
+                        dl += (int64_t)(oc == 0 && nc > 0) - (int64_t)(oc > 0 && nc == 0);
+                    }
+                }
+                sm.cdst[lane] = dst;
+                sm.csig[lane] = 0;
+            }
+            wave_lds_sync();
+            WQ_STAMP(6);
+            // kept old peers: new index = old index - removes below + adds below
+            for (uint32_t x = lane; x < T; x += 64) {
+                const uint32_t u = sm.u.r.own[x], d = sm.cdst[u];
+                if (d == kNone || sm.u.r.rmf[x]) continue;
+                const uint32_t y = sm.lst[x];
+                const uint32_t s0 = sm.cs[c0 + u], s1 = sm.cs[c0 + u + 1];
+                uint32_t lo = s0, hi = s1;  // first op of the cube with peer >= y
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (op_peer(sm.op[mid]) < y) lo = mid + 1; else hi = mid;
+                }
+                const uint32_t k = (x - sm.cpre[u]) - (sm.u.r.pr[lo - qa0] - sm.u.r.pr[s0 - qa0]) +
+                                   (sm.u.r.pa[lo - qa0] - sm.u.r.pa[s0 - qa0]);
+                L[d + 1 + k] = y;
+                if (k < (uint32_t)kInline)
+                    reinterpret_cast<uint32_t*>(a.tb.recs + ((B << a.lowbits) | (uint32_t)(sm.op[s0] >> 48)))[kInlineWord0 + k] = y;
+                atomicOr(reinterpret_cast<unsigned long long*>(&sm.csig[u]), (unsigned long long)peer_sig(y));
+            }
+            WQ_STAMP(7);
+            // added peers: new index = #old below - removes below + adds below
+            for (uint32_t q = lane; q < qb0 - qa0; q += 64) {
+                if (sm.u.r.fl[q] != 1) continue;
+                const uint32_t qq = qa0 + q;
+                const uint32_t lo = (uint32_t)sm.cid[qq] - c0;
+                const uint32_t d = sm.cdst[lo];
+                if (d == kNone) continue;
+                const uint32_t s0 = sm.cs[c0 + lo] - qa0;
+                const uint32_t y = op_peer(sm.op[qq]);
+                const uint32_t k = sm.u.r.at[q] - (sm.u.r.pr[q] - sm.u.r.pr[s0]) + (sm.u.r.pa[q] - sm.u.r.pa[s0]);
+                L[d + 1 + k] = y;
+                if (k < (uint32_t)kInline)
+                    reinterpret_cast<uint32_t*>(a.tb.recs + ((B << a.lowbits) | (uint32_t)(sm.op[qq] >> 48)))[kInlineWord0 + k] = y;
+                atomicOr(reinterpret_cast<unsigned long long*>(&sm.csig[lo]), (unsigned long long)peer_sig(y));
+            }
+            wave_lds_sync();
+            WQ_STAMP(8);
+            // one lane per cube: count word, header, inline padding
+            if (act && !isbig && dst != kNone) {
+                L[dst] = nc;
+                Record* rec = a.tb.recs + slot;
+                write_header(rec, nc, dst, sm.csig[lane], ncap);
+                uint32_t* inl = reinterpret_cast<uint32_t*>(rec) + kInlineWord0;
+                for (uint32_t k = nc; k < min(oc, (uint32_t)kInline); ++k) inl[k] = kNone;  // beyond oc: kNone already
+            }
+            const uint64_t mb = __ballot(isbig);
+            if (isbig) sm.big[nbig + __popcll(mb & lt)] = (uint16_t)c;
+            nbig += (uint32_t)__popcll(mb);
+            wave_lds_sync();  // the next round restages lst
+        }
+        wave_lds_sync();
+        WQ_STAMP(9);
+        // ---- wave path: lists longer than kLaneList, one cube at a time ----
+        for (uint32_t bi = 0; bi < nbig; ++bi) {
+            const uint32_t c = sm.big[bi];
+            const uint32_t qa = sm.cs[c], qb = sm.cs[c + 1];
+            const uint32_t slot = (B << a.lowbits) | (uint32_t)(sm.op[qa] >> 48);
+            Record* rec = a.tb.recs + slot;
+            const uint4 h0 = reinterpret_cast<const uint4*>(rec)[0];
+            const uint32_t oc = h0.z, off = h0.w, cap = reinterpret_cast<const uint32_t*>(rec)[6];
+            const bool staged = oc <= kWaveList;
+            const uint32_t* G = L + off + 1;
+            if (staged)
+                for (uint32_t i = lane; i < oc; i += 64) sm.lst[i] = G[i];
+            wave_lds_sync();
+            const uint32_t* O = staged ? sm.lst : G;  // the old list (LDS or global)
+            uint32_t nadd = 0, nrm = 0;
+            for (uint32_t t0 = qa; t0 < qb; t0 += 64) {
+                const uint32_t t = t0 + lane;
+                bool is_add = false, is_rm = false;
+                uint32_t pp = 0;
+                if (t < qb) {
+                    const uint64_t x = sm.op[t];
+                    pp = op_peer(x);
+                    if (t + 1 == qb || op_peer(sm.op[t + 1]) != pp) {
+                        uint32_t lo = 0, hi = oc;
+                        while (lo < hi) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (O[mid] < pp) lo = mid + 1; else hi = mid;
+                        }
+                        const bool present = lo < oc && O[lo] == pp;
+                        is_add = (x & 1u) && !present;
+                        is_rm = !(x & 1u) && present;
+                    }
+                }
+                const uint64_t ma = __ballot(is_add), mr = __ballot(is_rm);
+                if (is_add) sm.u.ar[nadd + __popcll(ma & lt)] = pp;
+                if (is_rm) sm.u.ar[kWin + nrm + __popcll(mr & lt)] = pp;
+                nadd += (uint32_t)__popcll(ma);
+                nrm += (uint32_t)__popcll(mr);
+            }
+            wave_lds_sync();
+            if ((nadd | nrm) && !staged && oc + nadd - nrm <= cap) {
+                // a list longer than the LDS in place: compaction of the removals (forward, 64
+                // words at a time: a word only moves down), then the adds opened up backwards (a
+                // word only moves up), then the adds themselves
+                const uint32_t nc = oc + nadd - nrm;
+                const uint32_t* A = sm.u.ar;
+                const uint32_t* R = sm.u.ar + kWin;
+                uint32_t* W = L + off + 1;
+                uint32_t* inl = reinterpret_cast<uint32_t*>(rec) + kInlineWord0;
+                uint32_t gone = 0;
+                for (uint32_t c0 = 0; c0 < oc; c0 += 64) {
+                    const uint32_t i = c0 + lane;
+                    const uint32_t y = i < oc ? W[i] : 0u;
+                    const uint32_t r = lds_lower_bound(R, nrm, y);
+                    const bool rm = i < oc && r < nrm && R[r] == y;
+                    const uint64_t m = __ballot(rm);
+                    if (i < oc && !rm) W[i - gone - (uint32_t)__popcll(m & lt)] = y;
+                    gone += (uint32_t)__popcll(m);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // stores drained before the next reads
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // this wave's own writes, read back below
+                const uint32_t w = oc - nrm;
+                // each add's place among the kept peers (W[0, w) now), kept in the removes' LDS
+                uint32_t* KB = sm.u.ar + kWin;
+                for (uint32_t q = lane; q < nadd; q += 64) {
+                    const uint32_t y = A[q];
+                    uint32_t lo = 0, hi = w;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (W[mid] < y) lo = mid + 1; else hi = mid;
+                    }
+                    KB[q] = lo;
+                }
+                wave_lds_sync();
+                uint64_t sig = 0;
+                for (int64_t c0 = (int64_t)((w + 63) / 64) * 64 - 64; c0 >= 0; c0 -= 64) {
+                    const uint32_t j = (uint32_t)c0 + lane;
+                    if (j < w) {
+                        const uint32_t y = W[j];
+                        const uint32_t k = j + lds_lower_bound(A, nadd, y);
+                        W[k] = y;
+                        if (k < (uint32_t)kInline) inl[k] = y;
+                        sig |= peer_sig(y);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                }
+                for (uint32_t q = lane; q < nadd; q += 64) {
+                    const uint32_t y = A[q], k = KB[q] + q;
+                    W[k] = y;
+                    if (k < (uint32_t)kInline) inl[k] = y;
+                    sig |= peer_sig(y);
+                }
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) sig |= __shfl_xor(sig, d, 64);
+                if ((uint32_t)lane >= nc && lane < kInline) inl[lane] = kNone;
+                if (lane == 0) {
+                    L[off] = nc;
+                    write_header(rec, nc, off, sig, cap);
+                    de += (int64_t)nc - (int64_t)oc;
+                    dl += (int64_t)(oc == 0 && nc > 0) - (int64_t)(oc > 0 && nc == 0);
+                    nwave++;
+                }
+            }
+            if ((nadd | nrm) && (staged || oc + nadd - nrm > cap)) {
+                const uint32_t nc = oc + nadd - nrm;
+                uint32_t dst = off, ncap = cap;
+                if (nc > cap) {
+                    ncap = grown(nc);
+                    uint32_t d0 = 0;
+                    if (lane == 0) d0 = bump_alloc(a, 1 + ncap);
+                    dst = __shfl(d0, 0, 64);
+                }
+                if (dst != kNone) {
+                    const uint32_t* A = sm.u.ar;
+                    const uint32_t* R = sm.u.ar + kWin;
+                    uint32_t* out = L + dst + 1;
+                    uint32_t* inl = reinterpret_cast<uint32_t*>(rec) + kInlineWord0;
+                    uint64_t sig = 0;
+                    for (uint32_t i = lane; i < oc; i += 64) {
+                        const uint32_t y = O[i];
+                        const uint32_t r = lds_lower_bound(R, nrm, y);
+                        if (r < nrm && R[r] == y) continue;
+                        const uint32_t k = i - r + lds_lower_bound(A, nadd, y);
+                        out[k] = y;
+                        if (k < (uint32_t)kInline) inl[k] = y;
+                        sig |= peer_sig(y);
+                    }
+                    for (uint32_t q = lane; q < nadd; q += 64) {
+                        const uint32_t y = A[q];
+                        uint32_t lo = 0, hi = oc;
+                        while (lo < hi) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (O[mid] < y) lo = mid + 1; else hi = mid;
+                        }
+                        const uint32_t k = q + lo - lds_lower_bound(R, nrm, y);
+                        out[k] = y;
+                        if (k < (uint32_t)kInline) inl[k] = y;
+                        sig |= peer_sig(y);
+                    }
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) sig |= __shfl_xor(sig, d, 64);
+                    if ((uint32_t)lane >= nc && lane < kInline) inl[lane] = kNone;
+                    if (lane == 0) {
+                        L[dst] = nc;
+                        write_header(rec, nc, dst, sig, ncap);
+                        de += (int64_t)nc - (int64_t)oc;
+                        dl += (int64_t)(oc == 0 && nc > 0) - (int64_t)(oc > 0 && nc == 0);
+                        nwave++;
+                    }
+                }
+            }
+            wave_lds_sync();  // the next big cube reuses lst / ar
+        }
+    }
+    WQ_STAMP(10);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        de += __shfl_xor(de, d, 64);
+        dl += __shfl_xor(dl, d, 64);
+        nwave += __shfl_xor(nwave, d, 64);
+    }
+    if (lane == 0) {
+        if (de) atomicAdd(reinterpret_cast<unsigned long long*>(&a.dstat[0]), (unsigned long long)de);
+        if (dl) atomicAdd(reinterpret_cast<unsigned long long*>(&a.dstat[1]), (unsigned long long)dl);
+        if (nwave) atomicAdd(&a.status->n_wave, nwave);
     }
 }
 
@@ -712,6 +884,7 @@ __global__ void k_mat_write(const Record* __restrict__ recs, uint64_t rcap, cons
 }  // namespace
 
 int table_sync_delta_stats(wq_router* h) {
+    if (int rc = table_resolve(h, true)) return rc;
     if (!h->dstat_pending) {
         WQ_HIP(h, hipStreamSynchronize(h->stream));
         return WQ_OK;
@@ -726,73 +899,6 @@ int table_sync_delta_stats(wq_router* h) {
     return WQ_OK;
 }
 
-namespace {
-
-// The per-lane path (any cube size): sort by (slot, peer), one lane per touched cube.
-int delta_plan_lanes(wq_router* h, uint32_t n, DeltaTable tb, DeltaSummary* sum) {
-    DeltaWs& d = h->dws;
-    hipStream_t s = h->stream;
-    const uint32_t nb = grid_for(n);
-    int bits = 1;
-    while ((1ull << bits) < h->tab.rec_cap) bits++;
-    uint32_t* idx_a = h->idx_a.as<uint32_t>();
-    uint32_t* idx_b = h->idx_b.as<uint32_t>();
-    hipLaunchKernelGGL(k_iota, dim3(nb), dim3(kBlock), 0, s, idx_a, (uint64_t)n);
-    int rc = sort_pairs<uint32_t>(h, d.peer.as<uint32_t>(), h->key32_a.as<uint32_t>(), idx_a, idx_b, n, 32);
-    if (rc) return rc;
-    uint32_t* key_a = h->key64_a.as<uint32_t>();  // 32-bit slot columns in the 64-bit scratch
-    uint32_t* key_b = h->key64_b.as<uint32_t>();
-    hipLaunchKernelGGL(k_gather<uint32_t>, dim3(nb), dim3(kBlock), 0, s, d.slot.as<uint32_t>(), idx_b, key_a,
-                       (uint64_t)n);
-    if ((rc = sort_pairs<uint32_t>(h, key_a, key_b, idx_b, idx_a, n, bits))) return rc;
-    const uint32_t* spk = key_b;
-    uint32_t* head = h->flags.as<uint32_t>();
-    uint32_t* cid = h->scan.as<uint32_t>();
-    hipLaunchKernelGGL(k_delta_mark, dim3(nb), dim3(kBlock), 0, s, idx_a, spk, d.peer.as<uint32_t>(),
-                       d.kind.as<uint8_t>(), n, d.sp.as<uint32_t>(), d.skd.as<uint8_t>(), head);
-    if ((rc = scan_u32(h, head, cid, n, true))) return rc;
-    uint32_t* cube_start = h->cube_start.as<uint32_t>();
-    hipLaunchKernelGGL(k_delta_cubes, dim3(nb), dim3(kBlock), 0, s, head, cid, n, cube_start, sum);
-    hipLaunchKernelGGL(k_delta_plan, dim3(nb), dim3(kBlock), 0, s, tb, cube_start, spk, d.sp.as<uint32_t>(),
-                       d.skd.as<uint8_t>(), sum, n, d.plan.as<uint4>(), d.reloc.as<uint32_t>(),
-                       d.part.as<uint64_t>());
-    hipLaunchKernelGGL(k_delta_reduce, dim3(1), dim3(kBlock), 0, s, d.part.as<uint64_t>(), nb, sum);
-    return scan_u32(h, d.reloc.as<uint32_t>(), d.reloc_off.as<uint32_t>(), n, false);
-}
-
-// The group path's plan: sort by record slot, light plan per touched cube.
-int delta_plan_groups(wq_router* h, uint32_t n, DeltaSummary* sum) {
-    DeltaWs& d = h->dws;
-    Table& t = h->tab;
-    hipStream_t s = h->stream;
-    const uint32_t nb = grid_for(n);
-    int bits = 1;
-    while ((1ull << bits) < t.rec_cap) bits++;
-    // (slot, kind << 32 | peer) sorted by slot, stable: each cube's ops stay in op order
-    int rc = sort_pairs<uint32_t, uint64_t>(h, d.slot.as<uint32_t>(), h->key32_a.as<uint32_t>(), d.sv.as<uint64_t>(),
-                                            d.svs.as<uint64_t>(), n, bits);
-    if (rc) return rc;
-    const uint32_t* sslot = h->key32_a.as<uint32_t>();
-    uint32_t* head = h->flags.as<uint32_t>();
-    uint32_t* cid = h->scan.as<uint32_t>();
-    hipLaunchKernelGGL(k_slot_heads, dim3(nb), dim3(kBlock), 0, s, sslot, n, head);
-    if ((rc = scan_u32(h, head, cid, n, true))) return rc;
-    uint32_t* cube_start = h->cube_start.as<uint32_t>();
-    hipLaunchKernelGGL(k_delta_cubes, dim3(nb), dim3(kBlock), 0, s, head, cid, n, cube_start, sum);
-    hipLaunchKernelGGL(k_delta_plan_light, dim3(nb), dim3(kBlock), 0, s, t.recs.as<Record>(), cube_start, sslot,
-                       d.svs.as<uint64_t>(), sum, n, d.plan.as<uint4>(), d.reloc.as<uint32_t>(), d.part.as<uint64_t>());
-    hipLaunchKernelGGL(k_delta_reduce, dim3(1), dim3(kBlock), 0, s, d.part.as<uint64_t>(), nb, sum);
-    return scan_u32(h, d.reloc.as<uint32_t>(), d.reloc_off.as<uint32_t>(), n, false);
-}
-
-int read_summary(wq_router* h, const DeltaSummary* sum, DeltaSummary* hs) {
-    WQ_HIP(h, hipGetLastError());
-    WQ_HIP(h, hipMemcpyAsync(hs, sum, sizeof(*hs), hipMemcpyDeviceToHost, h->stream));
-    return table_sync_delta_stats(h);  // synchronises the stream
-}
-
-}  // namespace
-
 int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     *applied = false;
     if (n_ops == 0) {
@@ -803,90 +909,144 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     DeltaWs& d = h->dws;
     Table& t = h->tab;
     hipStream_t s = h->stream;
-    // every op may bring a new cube: keep the record table at load <= 1/2 through the claims
-    if (2 * (t.n_recs + n) > t.rec_cap) {
+    const int rbits = 64 - t.rec_shift;
+    // every op may bring a new cube: keep the record table at load <= 1/2 through the claims; the
+    // sort key holds a 31-bit slot
+    if (2 * (t.n_recs + n) > t.rec_cap || rbits > 30) {
         h->n_delta_fallbacks++;
         return WQ_OK;
     }
-    const uint32_t nb = grid_for(n);
-    WQ_ALLOC(h, d.slot, (uint64_t)n * 4);
-    WQ_ALLOC(h, d.peer, (uint64_t)n * 4);
-    WQ_ALLOC(h, d.kind, n);
-    WQ_ALLOC(h, d.sp, (uint64_t)n * 4);
-    WQ_ALLOC(h, d.sv, (uint64_t)n * 8);
-    WQ_ALLOC(h, d.svs, (uint64_t)n * 8);
-    WQ_ALLOC(h, d.skd, n);
-    WQ_ALLOC(h, d.plan, (uint64_t)n * 16);
-    WQ_ALLOC(h, d.reloc, (uint64_t)n * 4);
-    WQ_ALLOC(h, d.reloc_off, (uint64_t)n * 4);
-    WQ_ALLOC(h, d.part, ((uint64_t)nb + kGroupGrid) * 32);
-    WQ_ALLOC(h, d.summ, sizeof(DeltaSummary));
+    // buckets of ~128 ops (a wave's window is 256): sorted bits = log2(n / 128), at most 16 (two
+    // radix passes), and enough that a bucket spans at most 2^16 slots (the in-window key field)
+    int sbits = 0;
+    while (sbits < 16 && ((uint64_t)128 << (sbits + 1)) <= n) sbits++;
+    if (sbits < 1) sbits = 1;
+    if (sbits > rbits + 1) sbits = rbits + 1;
+    if (rbits + 1 - sbits > 16) sbits = rbits + 1 - 16;
+    const int lowbits = rbits + 1 - sbits;
+    const uint32_t NBr = 1u << (rbits - lowbits);
+    WQ_ALLOC(h, h->key64_a, (uint64_t)n * 8);
+    WQ_ALLOC(h, h->key64_b, (uint64_t)n * 8);
+    WQ_ALLOC(h, h->cube_start, ((uint64_t)NBr + 1) * 4);
+    WQ_ALLOC(h, d.summ, 128);  // DeltaStatus, then the host snapshot at +64
     if (!d.dstat.p) {
         WQ_ALLOC(h, d.dstat, 16);
         WQ_HIP(h, hipMemsetAsync(d.dstat.p, 0, 16, s));
     }
-    WQ_ALLOC(h, h->idx_a, (uint64_t)n * 4);
-    WQ_ALLOC(h, h->idx_b, (uint64_t)n * 4);
-    WQ_ALLOC(h, h->key32_a, (uint64_t)n * 4);
-    WQ_ALLOC(h, h->key64_a, (uint64_t)n * 8);
-    WQ_ALLOC(h, h->key64_b, (uint64_t)n * 8);
-    WQ_ALLOC(h, h->flags, (uint64_t)n * 4);
-    WQ_ALLOC(h, h->scan, (uint64_t)n * 4);
-    WQ_ALLOC(h, h->cube_start, ((uint64_t)n + 1) * 4);
-    DeltaSummary* sum = d.summ.as<DeltaSummary>();
-    WQ_HIP(h, hipMemsetAsync(sum, 0, sizeof(DeltaSummary), s));
-    hipLaunchKernelGGL(k_delta_events, dim3(nb), dim3(kBlock), 0, s, h->cur_ops, n, (double)h->cube_size,
+    DeltaStatus* status = d.summ.as<DeltaStatus>();
+    if (!h->pend.pinned) WQ_HIP(h, hipMemsetAsync(status, 0, sizeof(DeltaStatus), s));  // then k_delta_finish
+    uint64_t* keys = h->key64_a.as<uint64_t>();
+    uint64_t* skeys = h->key64_b.as<uint64_t>();
+    hipLaunchKernelGGL(k_delta_events, dim3(grid_for(n)), dim3(kBlock), 0, s, h->cur_ops, n, (double)h->cube_size,
                        (int64_t)h->cube_size, t.recs.as<Record>(), t.rclaim.as<uint32_t>(),
-                       kBatchTag | (uint32_t)(++h->n_delta_batches & 0x7FFFFFFFu), t.rec_cap - 1,
-                       t.rec_shift, h->hash_mask, d.slot.as<uint32_t>(), d.peer.as<uint32_t>(),
-                       d.kind.as<uint8_t>(), d.sv.as<uint64_t>(), sum);
-    DeltaTable tb{t.recs.as<Record>(), t.rclaim.as<uint32_t>(), t.rec_cap - 1, t.rec_shift, h->hash_mask,
-                  t.list.as<uint32_t>()};
-    int rc = delta_plan_groups(h, n, sum);
-    if (rc) return rc;
-    DeltaSummary hs;
-    if ((rc = read_summary(h, sum, &hs))) return rc;
-    // the claims of a batch that falls back stay as empty records (count 0): invisible to every
-    // query, dropped by the rebuild
-    t.n_recs += hs.new_recs;
-    if (hs.irregular & 2u) return set_error(h, WQ_E_INVALID, "bad op (kind or reserved world id)");
-    const bool groups = hs.n_big == 0 && !hs.irregular;
-    if (!groups && !hs.irregular) {  // a cube past the wave path's bounds: plan the batch per lane
-        if ((rc = delta_plan_lanes(h, n, tb, sum))) return rc;
-        if ((rc = read_summary(h, sum, &hs))) return rc;
-    }
+                       kBatchTag | (uint32_t)(++h->n_delta_batches & 0x7FFFFFFFu), t.rec_cap - 1, t.rec_shift,
+                       h->hash_mask, keys, status);
+    size_t bytes = 0;
+    const int b0 = 33 + lowbits, b1 = 34 + rbits;
+    // onesweep at every size (rocPRIM's default takes a merge sort below 2^20 items: ~20 launches)
+    using Onesweep = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                rocprim::default_config, 0>;
+    WQ_HIP(h, rocprim::radix_sort_keys<Onesweep>(nullptr, bytes, keys, skeys, (size_t)n, b0, b1, s));
+    WQ_ALLOC(h, h->sort_tmp, bytes);
+    WQ_HIP(h, rocprim::radix_sort_keys<Onesweep>(h->sort_tmp.p, bytes, keys, skeys, (size_t)n, b0, b1, s));
+    uint32_t* bstart = h->cube_start.as<uint32_t>();
+    hipLaunchKernelGGL(k_bucket_bounds, dim3(grid_for((uint64_t)NBr + 1)), dim3(kBlock), 0, s, skeys, n, lowbits, NBr,
+                       bstart);
+    BucketArgs ba;
+    ba.tb = DeltaTable{t.recs.as<Record>(), t.rclaim.as<uint32_t>(), t.rec_cap - 1, t.rec_shift, h->hash_mask,
+                       t.list.as<uint32_t>()};
+    ba.keys = skeys;
+    ba.bstart = bstart;
+    ba.lowbits = lowbits;
+    ba.status = status;
+    ba.dstat = d.dstat.as<int64_t>();
     const uint64_t list_limit = std::min<uint64_t>(t.list_cap, 0xFFFFFFFFull);
-    if (hs.irregular || t.list_used + hs.reloc_words > list_limit || 4 * t.n_recs > t.rec_cap) {
-        h->n_delta_fallbacks++;
-        return WQ_OK;  // no list or count changed: the caller rebuilds
+    ba.list_base = t.list_used;
+    ba.list_room = list_limit > t.list_used ? list_limit - t.list_used : 0;
+    static const uint32_t dbg = getenv("WQ_DELTA_DBG") ? (uint32_t)atoi(getenv("WQ_DELTA_DBG")) : 0u;
+    static const bool stamps = getenv("WQ_DELTA_STAMPS") != nullptr;
+    ba.dbg = dbg;
+    ba.stamps = nullptr;
+    if (stamps) {
+        WQ_ALLOC(h, h->idx_b, (uint64_t)NBr * 16 * 8);
+        WQ_HIP(h, hipMemsetAsync(h->idx_b.p, 0, (uint64_t)NBr * 16 * 8, s));
+        ba.stamps = h->idx_b.as<uint64_t>();
     }
-    if (groups) {
-        const uint32_t ng = std::min<uint32_t>((n + kGroups - 1) / kGroups, kGroupGrid);
-        hipLaunchKernelGGL(k_delta_apply_group, dim3(ng), dim3(kBlock), 0, s, tb, d.plan.as<uint4>(),
-                           d.svs.as<uint64_t>(), sum, d.reloc.as<uint32_t>(),
-                           d.reloc_off.as<uint32_t>(), t.list_used, d.part.as<uint64_t>());
-        // entry / live-cube deltas stay on the device until the next read-back (table_sync_delta_stats)
-        hipLaunchKernelGGL(k_delta_stats, dim3(1), dim3(kBlock), 0, s, d.part.as<uint64_t>(), ng,
-                           d.dstat.as<uint64_t>());
-        h->dstat_pending = true;
-    } else {
-        hipLaunchKernelGGL(k_delta_apply, dim3(nb), dim3(kBlock), 0, s, tb, h->cube_start.as<uint32_t>(),
-                           d.sp.as<uint32_t>(), d.skd.as<uint8_t>(), sum,
-                           d.plan.as<uint4>(), d.reloc.as<uint32_t>(), d.reloc_off.as<uint32_t>(), t.list_used);
-        h->st.n = (uint64_t)((int64_t)h->st.n + (int64_t)hs.d_entries);
-        t.n_cubes = (uint64_t)((int64_t)t.n_cubes + (int64_t)hs.d_live);
-    }
+    hipLaunchKernelGGL(k_delta_bucket, dim3(NBr), dim3(64), 0, s, ba);
     WQ_HIP(h, hipGetLastError());
-    // subscribes may widen peer boxes: switch the boxes off until the next full build (the count
-    // pass then searches every long list); per-op box atomics here cost more than they save
-    if (t.n_pbox) WQ_HIP(h, hipMemsetAsync(t.pbox.as<uint32_t>() + (uint64_t)kBoxWords * t.n_pbox, 0, 4, s));
-    t.list_used += hs.reloc_words;
+    if (ba.stamps) {  // diagnostics: mean cycles per bucket and phase
+        std::vector<uint64_t> st((size_t)NBr * 16);
+        WQ_HIP(h, hipMemcpyAsync(st.data(), ba.stamps, st.size() * 8, hipMemcpyDeviceToHost, s));
+        WQ_HIP(h, hipStreamSynchronize(s));
+        double sum[16] = {0};
+        for (uint32_t b = 0; b < NBr; ++b)
+            for (int k = 0; k < 16; ++k) sum[k] += (double)st[(size_t)b * 16 + k];
+        fprintf(stderr, "delta buckets %u n %u:", NBr, n);
+        for (int k = 0; k < 11; ++k) fprintf(stderr, " %d:%.0f", k, sum[k] / NBr);
+        fprintf(stderr, "\n");
+    }
+    if (!t.stale.p) {
+        WQ_ALLOC(h, t.stale, 4);
+        WQ_HIP(h, hipMemsetAsync(t.stale.p, 0, 4, s));
+    }
+    PendingDelta& pd = h->pend;
+    if (!pd.ev) WQ_HIP(h, hipEventCreateWithFlags(&pd.ev, hipEventDisableTiming));
+    if (!pd.pinned) WQ_HIP(h, hipHostMalloc(&pd.pinned, 64, hipHostMallocDefault));
+    uint64_t* snap = reinterpret_cast<uint64_t*>(d.summ.as<char>() + 64);
+    hipLaunchKernelGGL(k_delta_finish, dim3(1), dim3(1), 0, s, status, d.dstat.as<int64_t>(), snap,
+                       t.stale.as<uint32_t>(),
+                       t.n_pbox ? t.pbox.as<uint32_t>() + (uint64_t)kBoxWords * t.n_pbox : nullptr);
+    WQ_HIP(h, hipMemcpyAsync(pd.pinned, snap, 48, hipMemcpyDeviceToHost, s));
+    WQ_HIP(h, hipEventRecord(pd.ev, s));
+    h->dstat_pending = false;
+    pd.active = true;
+    pd.ops = h->cur_ops;
+    pd.n = n_ops;
+    pd.list_room = ba.list_room;
     h->st_stale = true;
     h->any_stale = true;
     h->n_delta_applies++;
-    if (!groups) h->n_delta_lane_batches++;
     *applied = true;
     return WQ_OK;
+}
+
+int table_rebuild_batch(wq_router* h, size_t n_ops);  // wq_table.hip: the full rebuild of h->cur_ops
+
+int table_resolve(wq_router* h, bool blocking) {
+    PendingDelta& pd = h->pend;
+    if (!pd.active) return WQ_OK;
+    if (!blocking) {
+        const hipError_t q = hipEventQuery(pd.ev);
+        if (q == hipErrorNotReady) return WQ_OK;
+        if (q != hipSuccess) return set_error(h, WQ_E_HIP, "hipEventQuery", q);
+    }
+    WQ_HIP(h, hipEventSynchronize(pd.ev));
+    pd.active = false;
+    Table& t = h->tab;
+    DeltaStatus hs;
+    int64_t v[2];
+    std::memcpy(&hs, pd.pinned, sizeof(hs));
+    std::memcpy(v, static_cast<const char*>(pd.pinned) + 32, sizeof(v));
+    // the claims of a batch that is not applied stay as empty records (count 0): invisible to
+    // every query, dropped by the rebuild
+    t.n_recs += hs.new_recs;
+    h->st.n = (uint64_t)((int64_t)h->st.n + v[0]);
+    t.n_cubes = (uint64_t)((int64_t)t.n_cubes + v[1]);
+    t.list_used += std::min<uint64_t>(hs.bump, pd.list_room);
+    if (hs.n_wave) h->n_delta_wave_batches++;
+    if (!hs.flags) return WQ_OK;
+    // not applied (1: an op without a packed key; 2: an invalid op) or applied except the cubes
+    // whose relocation did not fit (4): the rebuild takes the table as it stands plus the whole
+    // batch again — exact, since the batch fixes the final state of every pair it touches
+    h->n_delta_applies--;
+    WQ_HIP(h, hipMemsetAsync(t.stale.p, 0, 4, h->stream));
+    if (hs.flags & 2u) {
+        WQ_HIP(h, hipStreamSynchronize(h->stream));
+        return set_error(h, WQ_E_INVALID, "bad op (kind or reserved world id) in an earlier device batch");
+    }
+    h->n_delta_fallbacks++;
+    h->cur_ops = pd.ops;
+    return table_rebuild_batch(h, pd.n);
 }
 
 int table_remove_peers_inplace(wq_router* h, const uint64_t* keys, size_t n_rm) {

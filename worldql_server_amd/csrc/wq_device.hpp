@@ -217,6 +217,7 @@ struct TableView {
     const uint32_t* pbox;
     uint32_t n_pbox;            // peers [0, n_pbox) have a box; others hold no record cube
     const uint32_t* pbox_valid; // device word: 0 once an update could not keep the boxes
+    const uint32_t* stale;      // device word: non-zero while an incremental batch awaits re-application
 };
 
 // ---- per-peer boxes: a fast "certainly not subscribed" for long lists ---------------------

@@ -204,6 +204,7 @@ int launch_route_global(wq_router* h, const uint32_t* d_world, const uint32_t* d
     sp.capacity = capacity;
     sp.cnt = cur;
     sp.health = route_health(h);
+    sp.stale = h->tab.stale.as<uint32_t>();
     if ((rc = launch_tile_scan(h, sp))) return rc;
     hipLaunchKernelGGL(global_offsets_kernel, dim3(n_tiles), dim3(kBlock), 0, s, gp);
     if (gp.peers) hipLaunchKernelGGL(global_copy_kernel, dim3(kCopyGrid), dim3(kBlock), 0, s, gp);

@@ -64,17 +64,27 @@ struct Table {
     // per-peer boxes (wq_device.hpp PeerBox): kBoxWords words per peer, then the valid word
     DevBuf pbox;
     uint32_t n_pbox = 0;
+    // u32: non-zero while the last incremental batch could not be applied on the device (the
+    // next host call re-applies it); route kernels report error bit 8 meanwhile
+    DevBuf stale;
+};
+
+// The last incremental batch (wq_delta.hip), in flight: its status and stat deltas arrive in
+// pinned memory; the next host call folds them in (and re-applies the batch if it was not
+// applied) — the update itself never waits for the GPU.
+struct PendingDelta {
+    bool active = false;
+    hipEvent_t ev = nullptr;
+    void* pinned = nullptr;     // DeltaStatus (32 B) + i64 {entries, live cubes} deltas
+    const wq_op* ops = nullptr; // the batch (h->d_ops or the caller's device array)
+    size_t n = 0;
+    uint64_t list_room = 0;
 };
 
 // Scratch of the incremental update (wq_delta.hip).
 struct DeltaWs {
-    DevBuf slot, peer, kind;      // per op (u32, u32, u8)
-    DevBuf sp, skd;         // per op in (slot, peer, op) order: peer, kind (per-lane path)
-    DevBuf sv, svs;         // per op: kind << 32 | peer, and the same sorted by record slot (group path)
-    DevBuf plan;            // uint4 per delta cube {record slot, new count, changed, -}
-    DevBuf reloc, reloc_off;  // u32 per delta cube: words of a relocated list, their exclusive scan
-    DevBuf part, summ;      // per-block partial sums, the summary read back
-    DevBuf dstat;           // i64 x2: entry / live-cube deltas of group-path batches not yet read back
+    DevBuf part, summ;      // REMOVE_PEER per-block partial sums; a batch's DeltaStatus
+    DevBuf dstat;           // i64 x2: entry / live-cube deltas of batches not yet read back
     DevBuf rm_bits;         // REMOVE_PEER from every world: bitmap over peer ids
 };
 
@@ -121,7 +131,10 @@ struct wq_router {
     // regenerated from the records on demand (table_materialize / table_ensure_any).
     bool st_stale = false, any_stale = false;
     wq::DeltaWs dws;
-    uint64_t n_delta_applies = 0, n_delta_fallbacks = 0, n_delta_lane_batches = 0;
+    wq::PendingDelta pend;
+    // incremental batches applied, batches that fell back to the rebuild, applied batches in which
+    // some cube took the wave path (lists longer than kLaneList)
+    uint64_t n_delta_applies = 0, n_delta_fallbacks = 0, n_delta_wave_batches = 0;
     uint64_t n_delta_batches = 0;  // batch tags of the record claims (wq_delta.hip)
     bool dstat_pending = false;
 
@@ -165,6 +178,7 @@ inline TableView table_view(const wq_router* h) {
     v.n_pbox = h->tab.n_pbox;
     v.pbox = h->tab.n_pbox ? h->tab.pbox.as<uint32_t>() : nullptr;
     v.pbox_valid = h->tab.n_pbox ? h->tab.pbox.as<uint32_t>() + (uint64_t)kBoxWords * h->tab.n_pbox : nullptr;
+    v.stale = h->tab.stale.as<uint32_t>();
     return v;
 }
 // Sticky {error OR, overflow OR} words of every route / global call since the last
@@ -191,6 +205,9 @@ int table_remove_peers_inplace(wq_router* h, const uint64_t* keys, size_t n);
 // Folds the device-side entry / live-cube deltas of incremental batches into st.n / tab.n_cubes
 // (synchronises the stream).
 int table_sync_delta_stats(wq_router* h);
+// Folds in the in-flight incremental batch (blocking: waits for it; otherwise only if it has
+// finished) and re-applies it through the rebuild if the device could not apply it.
+int table_resolve(wq_router* h, bool blocking);
 // Regenerates `st` (grouped by cube, peers ascending) from the records, slots and lists.
 int table_materialize(wq_router* h);
 // Rebuilds the any-keys if incremental updates left them stale.

@@ -127,6 +127,9 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
                  uint32_t* d_peers, uint32_t* d_msgs, size_t capacity) {
     hipStream_t s = h->stream;
     RouteWs& rw = h->rws;
+    // fold in a finished incremental batch (never waits: an unfinished one that turns out not to
+    // be applied shows as error bit 8 in this tick's counters)
+    if (int rc = table_resolve(h, false)) return rc;
     const Cfg& cfg = kCfgs[h->route_cfg == 0 && h->heavy_fanout ? kCfgHeavy : h->route_cfg];
     wq_route_counters *cur, *nxt;
     int rc0 = route_counters(h, M, d_offsets, &cur, &nxt);
@@ -211,6 +214,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         tsp.capacity = capacity;
         tsp.cnt = cur;
         tsp.health = route_health(h);
+        tsp.stale = tv.stale;
         if (int rc = launch_tile_scan(h, tsp)) return rc;
         hipLaunchKernelGGL((spill_copy_kernel<kSpillStage, 2>), dim3(nb), dim3(kBlock), 0, s, sp);
         WQ_HIP(h, hipGetLastError());
@@ -257,6 +261,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     sp.capacity = capacity;
     sp.cnt = cur;
     sp.health = route_health(h);
+    sp.stale = tv.stale;
     if (int rc = launch_tile_scan(h, sp)) return rc;
 
     EmitParams ep;

@@ -142,10 +142,10 @@ int wq_router_destroy(wq_router* h) {
                       &h->cube_start, &h->rws.buf, &h->rws.info, &h->rws.e, &h->rws.tiles,
                       &h->h_in, &h->h_out, &h->tab.recs, &h->tab.rclaim, &h->tab.pbox, &h->shard_hist,
                       &h->rec_keys, &h->rec_w, &h->rec_s, &h->rec_r, &h->ppos, &h->rws.agg, &h->rws.spill, &h->rws.scan_tmp,
-                      &h->dws.slot, &h->dws.peer, &h->dws.kind, &h->dws.sp, &h->dws.skd, &h->dws.plan,
-                      &h->dws.reloc, &h->dws.reloc_off, &h->dws.part, &h->dws.summ, &h->dws.dstat,
-                      &h->dws.rm_bits, &h->dws.sv, &h->dws.svs};
+                      &h->dws.part, &h->dws.summ, &h->dws.dstat, &h->dws.rm_bits, &h->tab.stale};
     for (DevBuf* b : bufs) b->release();
+    if (h->pend.ev) (void)hipEventDestroy(h->pend.ev);
+    if (h->pend.pinned) (void)hipHostFree(h->pend.pinned);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
     return WQ_OK;
@@ -241,11 +241,12 @@ int wq_debug_set_route_config(wq_router* h, int cfg) {
 }
 
 int wq_debug_update_counts(wq_router* h, uint64_t* incremental, uint64_t* rebuild_fallbacks,
-                           uint64_t* lane_batches) {
-    if (!h || !incremental || !rebuild_fallbacks || !lane_batches) return WQ_E_INVALID;
+                           uint64_t* wave_batches) {
+    if (!h || !incremental || !rebuild_fallbacks || !wave_batches) return WQ_E_INVALID;
+    if (int rc = table_resolve(h, true)) return rc;
     *incremental = h->n_delta_applies;
     *rebuild_fallbacks = h->n_delta_fallbacks;
-    *lane_batches = h->n_delta_lane_batches;
+    *wave_batches = h->n_delta_wave_batches;
     return WQ_OK;
 }
 
@@ -479,6 +480,7 @@ int wq_is_subscribed(wq_router* h, size_t n, const uint32_t* world, const uint32
     if (n == 0) return WQ_OK;
     if (n >= 0xFFFFFFFFull) return WQ_E_INVALID;
     WQ_HIP(h, hipSetDevice(h->device));
+    if (int rc0 = table_resolve(h, true)) return rc0;
     const size_t o_w = 0, o_p = align256(n * 4), o_k = align256(o_p + n * 4), o_o = align256(o_k + n * 24);
     WQ_ALLOC(h, h->h_in, o_o + n);
     char* d = h->h_in.as<char>();

@@ -280,9 +280,15 @@ int set_error(wq_router* h, int code, const char* what, hipError_t e) {
 }
 
 // Apply one batch of subscribe / unsubscribe ops (no REMOVE_PEER inside).
+int table_rebuild_batch(wq_router* h, size_t n_ops);
+
 int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops, bool on_device) {
     if (n_ops == 0) return WQ_OK;
     hipStream_t s = h->stream;
+    // the previous incremental batch first (it may need re-applying from h->d_ops, so before the
+    // upload below overwrites it)
+    int rc = table_resolve(h, true);
+    if (rc) return rc;
     if (on_device) {
         h->cur_ops = ops;
     } else {
@@ -290,14 +296,20 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops, bool on_de
         WQ_HIP(h, hipMemcpyAsync(h->d_ops.p, ops, n_ops * sizeof(wq_op), hipMemcpyHostToDevice, s));
         h->cur_ops = h->d_ops.as<wq_op>();
     }
-    int rc;
     // small batches against a built table: update the touched cubes in place (wq_delta.hip). The
-    // entry count may lag by the device-side deltas of earlier batches: it only picks the path.
+    // entry count may lag by REMOVE_PEER deltas not yet read back: it only picks the path.
     if (h->st.n && h->tab.n_cubes && 4 * n_ops <= h->st.n) {
         bool applied = false;
         if ((rc = table_apply_delta(h, n_ops, &applied))) return rc;
         if (applied) return WQ_OK;
     }
+    return table_rebuild_batch(h, n_ops);
+}
+
+// The full rebuild: the live state plus the batch h->cur_ops, sorted and reduced "last op wins".
+int table_rebuild_batch(wq_router* h, size_t n_ops) {
+    hipStream_t s = h->stream;
+    int rc;
     if ((rc = table_sync_delta_stats(h))) return rc;
     const uint64_t S = h->st.n;
     const uint64_t N = S + n_ops;
@@ -393,6 +405,7 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops, bool on_de
 // (world_map.rs:41-61, area_map.rs:124-135).
 int table_remove_peers(wq_router* h, const uint64_t* keys, size_t n_rm) {
     // one in-place pass over every cube's list (wq_delta.hip); the state and any-keys go stale
+    if (int rc = table_resolve(h, true)) return rc;
     if (n_rm == 0 || (h->st.n == 0 && !h->dstat_pending)) return WQ_OK;
     return table_remove_peers_inplace(h, keys, n_rm);
 }

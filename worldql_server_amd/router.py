@@ -416,7 +416,7 @@ class Router:
 
     def update_counts(self, lanes: bool = False):
         """(batches applied incrementally, batches that fell back to the full rebuild)
-        [+ incremental batches that took the per-lane path, with lanes=True]."""
+        [+ incremental batches in which a cube took the wave path (list > 48 peers), lanes=True]."""
         a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         self._check(self.lib.wq_debug_update_counts(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         return (a.value, b.value, c.value) if lanes else (a.value, b.value)
