@@ -208,6 +208,7 @@ __global__ __launch_bounds__(kBlock) void k_delta_stats(const uint64_t* __restri
 
 // ---- the bucket apply: one wave per bucket, one lane per touched cube ------------------------
 constexpr int kWin = 256;        // ops per window (a bucket's ops are taken in op-order windows)
+constexpr uint32_t kInlineOnly = 0xFFFFFFFEu;  // a round cube's new list fits the record: no list write
 constexpr int kLaneList = 256;         // old lists longer than this go to the wave path
 constexpr uint32_t kRoundWords = 1024;  // a round stages at most this many old-list words (and 64 cubes)
 constexpr uint32_t kWaveList = kRoundWords;  // the wave path stages lists up to this in LDS
@@ -228,9 +229,14 @@ struct BucketLds {
         } r;
         uint32_t ar[2 * kWin];      // wave path: the cube's adds [0, kWin) and removes [kWin, 2 kWin)
     } u;
+    uint32_t hoc[kWin];             // window: per cube, old count (prefetched headers)
+    uint32_t hoff[kWin];            // window: per cube, list offset
+    uint32_t hcap[kWin];            // window: per cube, list capacity
+    uint64_t csrc[64];              // round: per cube, where its old peers are (inline words or list)
     uint64_t csig[64];              // round: per cube, OR of peer_sig over its new list
     uint32_t cpre[65];              // round: per cube, first staged word
     uint32_t cdst[64];              // round: per cube, where the new list goes (kNone: unchanged)
+    uint32_t cslot[64];             // round: per cube, its record slot
     uint16_t cs[kWin + 1];          // cube starts in op[]
     uint16_t big[kWin];             // cubes (cs index) the wave path takes
     uint8_t cid[kWin];              // per op: its cube (window-local index mod 256)
@@ -271,6 +277,21 @@ __device__ __forceinline__ void wave_bitonic(uint64_t (&a)[4], int lane) {
 
 __device__ __forceinline__ uint32_t op_peer(uint64_t x) { return (uint32_t)(x >> 16); }
 
+// lower_bound of v in a[0, n), n <= N, in log2(N) branch-free steps (independent searches of one
+// lane can overlap: no loop-carried control flow).
+template <int N>
+__device__ __forceinline__ uint32_t lds_lower_bound_fixed(const uint32_t* a, uint32_t n, uint32_t v) {
+    uint32_t lo = 0, len = n;
+#pragma unroll
+    for (int s = N; s > 1; s >>= 1) {
+        const uint32_t half = len >> 1;
+        const bool right = half && a[lo + half - 1] < v;
+        lo += right ? half : 0u;
+        len = right ? len - half : (half ? half : len);
+    }
+    return (len && a[lo] < v) ? lo + 1 : lo;
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -297,7 +318,6 @@ struct BucketArgs {
     int64_t* dstat;          // running {entries, live cubes} deltas
     uint64_t list_base;      // first free list word (t.list_used)
     uint64_t list_room;      // words available past list_base
-    uint32_t dbg;            // timing experiments only (WQ_DELTA_DBG): 2 no merge, 4 no sort
     uint64_t* stamps;        // diagnostics (WQ_DELTA_STAMPS): per bucket, cycles per phase
 };
 
@@ -348,9 +368,7 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                 v[r] = ~0ull;
             }
         }
-        if (a.dbg & 4u)
-            ;
-        else if (cnt <= 64)
+        if (cnt <= 64)
             wave_bitonic<1>(v, lane);
         else if (cnt <= 128)
             wave_bitonic<2>(v, lane);
@@ -372,6 +390,31 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
             ncub += (uint32_t)__popcll(m);
         }
         if (lane == 0) sm.cs[ncub] = (uint16_t)cnt;
+        wave_lds_sync();
+        // every cube's header at once (up to four record lines per lane in flight)
+        {
+            uint2 hw[4];
+            uint32_t hc[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t c = r * 64 + lane;
+                if (c < ncub) {
+                    const uint32_t slot = (B << a.lowbits) | (uint32_t)(sm.op[sm.cs[c]] >> 48);
+                    const uint32_t* rw = reinterpret_cast<const uint32_t*>(a.tb.recs + slot);
+                    hw[r] = *reinterpret_cast<const uint2*>(rw + 2);
+                    hc[r] = rw[6];
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t c = r * 64 + lane;
+                if (c < ncub) {
+                    sm.hoc[c] = hw[r].x;
+                    sm.hoff[c] = hw[r].y;
+                    sm.hcap[c] = hc[r];
+                }
+            }
+        }
         WQ_STAMP(1);
         wave_lds_sync();
         // ---- rounds of up to 64 cubes, data-parallel ----
@@ -388,12 +431,12 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
             uint32_t slot = 0, oc = 0, off = 0, cap = 0;
             if (act) {
                 slot = (B << a.lowbits) | (uint32_t)(sm.op[sm.cs[c]] >> 48);
-                const uint32_t* rw = reinterpret_cast<const uint32_t*>(a.tb.recs + slot);
-                const uint2 cw = *reinterpret_cast<const uint2*>(rw + 2);
-                oc = cw.x;
-                off = cw.y;
-                cap = rw[6];
+                oc = sm.hoc[c];
+                off = sm.hoff[c];
+                cap = sm.hcap[c];
             }
+            const uint64_t src_base = reinterpret_cast<uint64_t>(
+                oc <= (uint32_t)kInline ? reinterpret_cast<const uint32_t*>(a.tb.recs + slot) + kInlineWord0 : L + off + 1);
             bool isbig = act && oc > (uint32_t)kLaneList;
             uint32_t oc_st = isbig ? 0u : oc;
             const uint32_t incl = wave_incl_scan_u32(oc_st, lane);
@@ -407,55 +450,49 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
             if (lane == (int)n_round - 1) sm.cpre[n_round] = incl;
             const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)n_round - 1);
             const uint32_t qa0 = sm.cs[c0], qb0 = sm.cs[c0 + n_round];
+            if (act) {
+                sm.csrc[lane] = src_base;
+                sm.cslot[lane] = slot;
+                for (uint32_t i = 0; i < oc_st; ++i) sm.u.r.own[pre + i] = (uint8_t)lane;  // owner map
+            }
             wave_lds_sync();
             WQ_STAMP(2);
-            // stage the round's old lists flat: word x belongs to the cube u with cpre[u] <= x
-            for (uint32_t x0 = 0; x0 < T; x0 += 64 * 8) {
-                uint32_t val[8], uu[8];
+            // stage the round's old lists flat: all of the round's loads in flight at once
+            // (T <= kRoundWords = 16 per lane)
+            {
+                uint32_t val[kRoundWords / 64];
 #pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    const uint32_t x = x0 + r * 64 + lane;
-                    uint32_t lo = 0, hi = n_round - 1;  // last u with cpre[u] <= x
-                    while (lo < hi) {
-                        const uint32_t mid = (lo + hi + 1) >> 1;
-                        if (sm.cpre[mid] <= x) lo = mid; else hi = mid - 1;
-                    }
-                    uu[r] = lo;
-                    const uint32_t off_u = (uint32_t)__shfl((int)off, (int)lo, 64);
-                    val[r] = x < T ? L[off_u + 1 + (x - sm.cpre[lo])] : 0u;
-                }
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    const uint32_t x = x0 + r * 64 + lane;
+                for (int r = 0; r < (int)(kRoundWords / 64); ++r) {
+                    const uint32_t x = r * 64 + lane;
+                    val[r] = 0u;
                     if (x < T) {
-                        sm.lst[x] = val[r];
-                        sm.u.r.own[x] = (uint8_t)uu[r];
+                        const uint32_t u = sm.u.r.own[x];
+                        val[r] = reinterpret_cast<const uint32_t*>(sm.csrc[u])[x - sm.cpre[u]];
                         sm.u.r.rmf[x] = 0;
                     }
+                }
+#pragma unroll
+                for (int r = 0; r < (int)(kRoundWords / 64); ++r) {
+                    const uint32_t x = r * 64 + lane;
+                    if (x < T) sm.lst[x] = val[r];
                 }
             }
             wave_lds_sync();
             WQ_STAMP(3);
-            // per op of the round: the deciding op of each peer run, present or not
+            // per op of the round: the deciding op of each peer run (the last), present or not
             for (uint32_t q0 = qa0; q0 < qb0; q0 += 64) {
                 const uint32_t q = q0 + lane;
-                uint8_t f = 0;
-                uint16_t atq = 0;
                 if (q < qb0) {
                     const uint64_t x = sm.op[q];
                     const uint32_t pp = op_peer(x);
                     const bool last = q + 1 == qb0 || (sm.op[q + 1] >> 16) != (x >> 16);  // cube and peer
                     const uint32_t lo = (uint32_t)sm.cid[q] - c0;  // the op's cube within the round
                     const uint32_t b0 = sm.cpre[lo], n0 = sm.cpre[lo + 1] - b0;
-                    const bool small = !((uint32_t)__shfl((int)isbig, (int)lo, 64));
-                    if (last && small) {
-                        uint32_t l2 = 0, h2 = n0;
-                        while (l2 < h2) {
-                            const uint32_t mid = (l2 + h2) >> 1;
-                            if (sm.lst[b0 + mid] < pp) l2 = mid + 1; else h2 = mid;
-                        }
+                    uint8_t f = 0;
+                    uint32_t l2 = 0;
+                    if (last) {  // (a wave-path cube stages nothing: n0 = 0, and its cdst is kNone)
+                        l2 = lds_lower_bound_fixed<kLaneList>(sm.lst + b0, n0, pp);
                         const bool present = l2 < n0 && sm.lst[b0 + l2] == pp;
-                        atq = (uint16_t)l2;
                         if ((x & 1u) && !present) f = 1;
                         if (!(x & 1u) && present) {
                             f = 2;
@@ -463,10 +500,9 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                         }
                     }
                     sm.u.r.fl[q - qa0] = f;
-                    sm.u.r.at[q - qa0] = atq;
+                    sm.u.r.at[q - qa0] = (uint16_t)l2;
                 }
             }
-            WQ_STAMP(4);
             // exclusive prefixes of the add / remove flags over the round's ops
             {
                 uint32_t ra = 0, rr = 0;
@@ -487,16 +523,19 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                 }
             }
             wave_lds_sync();
-            WQ_STAMP(5);
+            WQ_STAMP(4);
             // one lane per cube: new count, destination
             uint32_t nc = oc, dst = kNone, ncap = cap;
+            if (act && isbig) sm.cdst[lane] = kNone;
             if (act && !isbig) {
                 const uint32_t s0 = sm.cs[c] - qa0, s1 = sm.cs[c + 1] - qa0;
                 const uint32_t nadd = sm.u.r.pa[s1] - sm.u.r.pa[s0], nrm = sm.u.r.pr[s1] - sm.u.r.pr[s0];
                 nc = oc + nadd - nrm;
                 if (nadd | nrm) {
-                    dst = off;
-                    if (nc > cap) {
+                    // <= kInline peers: the record's inline words only (the list block, if any,
+                    // goes stale); longer: the whole list rewritten, in place or relocated
+                    dst = nc <= (uint32_t)kInline ? kInlineOnly : off;
+                    if (nc > (uint32_t)kInline && nc > cap) {
                         ncap = grown(nc);
                         dst = bump_alloc(a, 1 + ncap);
                     }
@@ -510,47 +549,49 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
             }
             wave_lds_sync();
             WQ_STAMP(6);
-            // kept old peers: new index = old index - removes below + adds below
+            // kept old peers: new index = old index - removes below + adds below (the adds below y
+            // = the cube's ops up to the first with peer >= y: a fixed-step search, no branches)
+#pragma unroll 4
             for (uint32_t x = lane; x < T; x += 64) {
                 const uint32_t u = sm.u.r.own[x], d = sm.cdst[u];
                 if (d == kNone || sm.u.r.rmf[x]) continue;
                 const uint32_t y = sm.lst[x];
                 const uint32_t s0 = sm.cs[c0 + u], s1 = sm.cs[c0 + u + 1];
-                uint32_t lo = s0, hi = s1;  // first op of the cube with peer >= y
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (op_peer(sm.op[mid]) < y) lo = mid + 1; else hi = mid;
+                uint32_t lo = s0, len = s1 - s0;  // first op of the cube with peer >= y
+#pragma unroll
+                for (int st = 0; st < 8; ++st) {
+                    const uint32_t half = len >> 1;
+                    const bool right = half && op_peer(sm.op[lo + half - 1]) < y;
+                    lo += right ? half : 0u;
+                    len = right ? len - half : (half ? half : len);
                 }
+                if (len && op_peer(sm.op[lo]) < y) ++lo;
                 const uint32_t k = (x - sm.cpre[u]) - (sm.u.r.pr[lo - qa0] - sm.u.r.pr[s0 - qa0]) +
                                    (sm.u.r.pa[lo - qa0] - sm.u.r.pa[s0 - qa0]);
-                L[d + 1 + k] = y;
-                if (k < (uint32_t)kInline)
-                    reinterpret_cast<uint32_t*>(a.tb.recs + ((B << a.lowbits) | (uint32_t)(sm.op[s0] >> 48)))[kInlineWord0 + k] = y;
+                if (d != kInlineOnly) L[d + 1 + k] = y;
+                if (k < (uint32_t)kInline) reinterpret_cast<uint32_t*>(a.tb.recs + sm.cslot[u])[kInlineWord0 + k] = y;
                 atomicOr(reinterpret_cast<unsigned long long*>(&sm.csig[u]), (unsigned long long)peer_sig(y));
             }
             WQ_STAMP(7);
             // added peers: new index = #old below - removes below + adds below
             for (uint32_t q = lane; q < qb0 - qa0; q += 64) {
                 if (sm.u.r.fl[q] != 1) continue;
-                const uint32_t qq = qa0 + q;
-                const uint32_t lo = (uint32_t)sm.cid[qq] - c0;
-                const uint32_t d = sm.cdst[lo];
+                const uint32_t u = (uint32_t)sm.cid[qa0 + q] - c0, d = sm.cdst[u];
                 if (d == kNone) continue;
-                const uint32_t s0 = sm.cs[c0 + lo] - qa0;
-                const uint32_t y = op_peer(sm.op[qq]);
+                const uint32_t s0 = sm.cs[c0 + u] - qa0;
+                const uint32_t y = op_peer(sm.op[qa0 + q]);
                 const uint32_t k = sm.u.r.at[q] - (sm.u.r.pr[q] - sm.u.r.pr[s0]) + (sm.u.r.pa[q] - sm.u.r.pa[s0]);
-                L[d + 1 + k] = y;
-                if (k < (uint32_t)kInline)
-                    reinterpret_cast<uint32_t*>(a.tb.recs + ((B << a.lowbits) | (uint32_t)(sm.op[qq] >> 48)))[kInlineWord0 + k] = y;
-                atomicOr(reinterpret_cast<unsigned long long*>(&sm.csig[lo]), (unsigned long long)peer_sig(y));
+                if (d != kInlineOnly) L[d + 1 + k] = y;
+                if (k < (uint32_t)kInline) reinterpret_cast<uint32_t*>(a.tb.recs + sm.cslot[u])[kInlineWord0 + k] = y;
+                atomicOr(reinterpret_cast<unsigned long long*>(&sm.csig[u]), (unsigned long long)peer_sig(y));
             }
             wave_lds_sync();
             WQ_STAMP(8);
             // one lane per cube: count word, header, inline padding
             if (act && !isbig && dst != kNone) {
-                L[dst] = nc;
+                if (dst != kInlineOnly) L[dst] = nc;
                 Record* rec = a.tb.recs + slot;
-                write_header(rec, nc, dst, sm.csig[lane], ncap);
+                write_header(rec, nc, dst != kInlineOnly ? dst : off, sm.csig[lane], ncap);
                 uint32_t* inl = reinterpret_cast<uint32_t*>(rec) + kInlineWord0;
                 for (uint32_t k = nc; k < min(oc, (uint32_t)kInline); ++k) inl[k] = kNone;  // beyond oc: kNone already
             }
@@ -785,8 +826,10 @@ __global__ __launch_bounds__(kBlock) void k_remove_peers(DeltaTable tb, const Sl
             off = v.off;
             n = tb.list[off];
         }
-        uint32_t* L = tb.list + off + 1;
         uint32_t* rw = reinterpret_cast<uint32_t*>(tb.recs + e);
+        // a record cube with <= kInline peers keeps them only inline (its list block is stale)
+        const bool inl_only = is_rec && n <= (uint32_t)kInline;
+        uint32_t* L = inl_only ? rw + kInlineWord0 : tb.list + off + 1;
         uint32_t kept = 0;
         uint64_t sig = 0;
         for (uint32_t c0 = 0; c0 < n; c0 += kG) {
@@ -799,7 +842,7 @@ __global__ __launch_bounds__(kBlock) void k_remove_peers(DeltaTable tb, const Sl
                 sig |= peer_sig(x);
                 if (pos != k) {  // shifted by an earlier removal
                     L[pos] = x;
-                    if (is_rec && pos < (uint32_t)kInline) rw[kInlineWord0 + pos] = x;
+                    if (is_rec && !inl_only && pos < (uint32_t)kInline) rw[kInlineWord0 + pos] = x;
                 }
             }
             kept += (uint32_t)__popc(mk);
@@ -807,7 +850,7 @@ __global__ __launch_bounds__(kBlock) void k_remove_peers(DeltaTable tb, const Sl
         if (kept == n) continue;  // group-uniform: nothing removed here
 #pragma unroll
         for (int d = kG / 2; d >= 1; d >>= 1) sig |= __shfl_xor(sig, d, kG);
-        if (gl == 0) L[-1] = kept;
+        if (gl == 0 && !inl_only) L[-1] = kept;
         if (is_rec) {
             for (uint32_t k = kept + gl; k < n && k < (uint32_t)kInline; k += kG) rw[kInlineWord0 + k] = kNone;
             if (gl == 0) {
@@ -857,10 +900,12 @@ __global__ void k_mat_write(const Record* __restrict__ recs, uint64_t rcap, cons
     if (!n) return;
     uint32_t w, off;
     int64_t k[3];
+    const uint32_t* src;
     if (i < rcap) {
         const Record& r = recs[i];
         record_key(r, s, &w, k);
         off = r.list_off;
+        src = n <= (uint32_t)kInline ? r.peers : list + off + 1;  // short lists live inline only
     } else {
         const SlotView v = load_slot(slots, i - rcap);
         w = v.world;
@@ -868,6 +913,7 @@ __global__ void k_mat_write(const Record* __restrict__ recs, uint64_t rcap, cons
         k[1] = v.k1;
         k[2] = v.k2;
         off = v.off;
+        src = list + off + 1;
     }
     const uint64_t hh = cube_hash(w, k[0], k[1], k[2]) & hmask;
     const uint32_t o = pos[i];
@@ -877,7 +923,7 @@ __global__ void k_mat_write(const Record* __restrict__ recs, uint64_t rcap, cons
         st_kx[o + j] = k[0];
         st_ky[o + j] = k[1];
         st_kz[o + j] = k[2];
-        st_p[o + j] = list[off + 1 + j];
+        st_p[o + j] = src[j];
     }
 }
 
@@ -963,9 +1009,7 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     const uint64_t list_limit = std::min<uint64_t>(t.list_cap, 0xFFFFFFFFull);
     ba.list_base = t.list_used;
     ba.list_room = list_limit > t.list_used ? list_limit - t.list_used : 0;
-    static const uint32_t dbg = getenv("WQ_DELTA_DBG") ? (uint32_t)atoi(getenv("WQ_DELTA_DBG")) : 0u;
-    static const bool stamps = getenv("WQ_DELTA_STAMPS") != nullptr;
-    ba.dbg = dbg;
+    static const bool stamps = getenv("WQ_DELTA_STAMPS") != nullptr;  // diagnostics only
     ba.stamps = nullptr;
     if (stamps) {
         WQ_ALLOC(h, h->idx_b, (uint64_t)NBr * 16 * 8);

@@ -289,6 +289,27 @@ __device__ __forceinline__ uint64_t find_record(const TableView& t, uint64_t pk,
     }
 }
 
+// The cube's peers, ascending: a record cube with <= kInline peers keeps them only in its
+// record's inline words (its `list` block, if any, is stale: wq_delta.hip); longer record lists
+// and slot-table cubes are in `list`. *n = 0 when the cube has no peers.
+__device__ __forceinline__ const uint32_t* find_peers(const TableView& t, uint32_t w, int64_t x, int64_t y, int64_t z,
+                                                      uint32_t* n) {
+    uint64_t pk;
+    uint32_t ext;
+    *n = 0;
+    if (pack_key(w, x, y, z, t.sf, &pk, &ext)) {
+        uint4 h0, h1;
+        const uint64_t i = find_record(t, pk, ext, &h0, &h1);
+        if (!h1.w || !h0.z) return t.list;
+        *n = h0.z;
+        return h0.z <= (uint32_t)kInline ? t.recs[i].peers : t.list + h0.w + 1;
+    }
+    const uint32_t off = probe(t.slots, t.slot_mask, t.slot_shift, cube_hash(w, x, y, z) & t.hash_mask, w, x, y, z);
+    if (off == kNone) return t.list;
+    *n = t.list[off];
+    return t.list + off + 1;
+}
+
 // Offset of the cube's list in t.list, or kNone (both tables).
 __device__ __forceinline__ uint32_t find_list(const TableView& t, uint32_t w, int64_t x, int64_t y, int64_t z) {
     uint64_t pk;

@@ -16,7 +16,6 @@ __global__ void is_subscribed_kernel(const uint32_t* __restrict__ world, const u
                                      int raw, const void* __restrict__ kp, uint32_t n, TableView t,
                                      int64_t si, uint8_t* out) {
     const double sf = t.sf;
-    const uint32_t* list = t.list;
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     int64_t x, y, z;
@@ -32,14 +31,10 @@ __global__ void is_subscribed_kernel(const uint32_t* __restrict__ world, const u
         z = coord_clamp_dev(q[2], sf, si);
     }
     const uint32_t w = world[i];
-    const uint32_t off = find_list(t, w, x, y, z);
-    uint8_t r = 0;
-    if (off != kNone) {
-        const uint32_t cnt = list[off];
-        const uint32_t at = lower_bound_dev(list + off + 1, cnt, peer[i]);
-        r = (at < cnt && list[off + 1 + at] == peer[i]) ? 1 : 0;
-    }
-    out[i] = r;
+    uint32_t cnt = 0;
+    const uint32_t* lp = find_peers(t, w, x, y, z, &cnt);
+    const uint32_t at = lower_bound_dev(lp, cnt, peer[i]);
+    out[i] = (at < cnt && lp[at] == peer[i]) ? 1 : 0;
 }
 
 __global__ void is_subscribed_any_kernel(const uint32_t* __restrict__ world, const uint32_t* __restrict__ peer,
