@@ -85,7 +85,9 @@ typedef struct wq_route_counters {
     uint64_t n_pairs;      /* P: (message, peer) pairs after the replication filter */
     uint64_t n_candidates; /* F: peers read from the probed buckets before the filter */
     uint32_t overflow;     /* 1 if P exceeded the caller's capacity (outputs truncated) */
-    uint32_t error;        /* 4: a bounded spin gave up (WQ_E_TIMEOUT); 2: P > 2^32-1 (WQ_E_CAPACITY) */
+    uint32_t error;        /* 4: a bounded spin gave up (WQ_E_TIMEOUT); 2: P > 2^32-1 (WQ_E_CAPACITY);
+                              8: the table is missing an incremental batch the device could not
+                              apply (re-applied by the next wq_apply* / query call) */
 } wq_route_counters;
 
 /* ---- pinned host memory for the host-array entry points: buffers from wq_host_alloc move over
@@ -111,8 +113,15 @@ int wq_apply_ops(wq_router* h, const wq_op* ops, size_t n);
 /* The same for a batch already in device memory (e.g. assembled by the caller's own kernels):
  * subscribe / unsubscribe ops only — a REMOVE_PEER op or the reserved world id fails the whole
  * batch with WQ_E_INVALID before anything changes (use wq_remove_peers for disconnects).
- * The call blocks on one small read-back (the update plan's sizes); the update itself is ordered
- * on the handle's stream, before any later tick. */
+ * Asynchronous: an incremental batch (up to 1/4 of the table's entries) is enqueued on the
+ * handle's stream, before any later tick, and the call returns without waiting for the GPU; the
+ * NEXT call on the handle folds its status in (waiting only for that batch, not for later work).
+ * Keep d_ops unchanged until that next call has returned: a batch the device could not apply
+ * (an op whose key has no packed form — NaN / huge coordinates, off-grid raw keys, world ids
+ * >= 2^24 - 1 — or list space exhausted) is re-applied from it by the rebuild then, and routes
+ * issued in between report error bit 8 (WQ stale table) in their counters and in
+ * wq_route_health. An invalid op (REMOVE_PEER kind, reserved world) in such a batch is reported
+ * as WQ_E_INVALID by that next call, with the table left as before the batch. */
 int wq_apply_ops_device(wq_router* h, const wq_op* d_ops, size_t n);
 /* WorldMap::remove_peer for n peers (every world), world_map.rs:41-61. */
 int wq_remove_peers(wq_router* h, const uint32_t* peers, size_t n);
@@ -290,7 +299,8 @@ int wq_peer_major_device(wq_router* h, const uint32_t* d_offsets, const uint32_t
  * the previous wq_route_health on this handle; reading clears them (synchronises the stream). A
  * normal tick never writes them, so a caller that runs many _device ticks without reading their
  * counters checks the whole run here: error bit 4 = a bounded spin gave up (WQ_E_TIMEOUT), 2 =
- * more than 2^32-1 pairs in one tick; overflow = some tick's pairs exceeded its capacity. */
+ * more than 2^32-1 pairs in one tick, 8 = a tick ran on a table still missing an incremental
+ * batch (wq_apply_ops_device); overflow = some tick's pairs exceeded its capacity. */
 int wq_route_health(wq_router* h, uint32_t* error_bits, uint32_t* overflow);
 
 /* ---- instrumentation ----

@@ -240,3 +240,55 @@ def test_remove_peers_in_place_vs_oracle(hash_bits):
         check()
     inc, fb = r.update_counts()
     assert inc == 3 and fb == 0  # the churn after each removal stays incremental
+
+
+def test_device_batch_without_packed_key_is_reapplied():
+    """wq_apply_ops_device returns without waiting for the GPU. A batch with an op that has no
+    packed key (an off-grid raw key) cannot be applied by the incremental kernels: a tick issued
+    right after it is either exact (the handle already folded the batch in) or flagged with error
+    bit 8; the next call re-applies the batch through the rebuild, and from then on every tick is
+    exact again."""
+    import torch
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(31)
+    r, o = mk_router(), orc.COracle(16)
+    r.set_stream(torch.cuda.current_stream().cuda_stream)
+    base = _random_ops(rng, 40000, 2, 3000, 128.0, 1.0)
+    r.apply_ops(base)
+    o.apply_ops(base)
+    raw = abi.ops_array(np.zeros(2, np.uint32), np.array([5, 6], np.uint32), np.zeros(2, np.uint8),
+                        key=np.array([[16, 16, 17], [3, 0, 0]]))
+    b = abi.concat_ops([_random_ops(rng, 1500, 2, 3000, 128.0, 0.5), raw])
+    d_ops = torch.from_numpy(np.ascontiguousarray(b).view(np.uint8).copy()).to(dev)
+    r.apply_ops_device(d_ops.data_ptr(), len(b))
+    o.apply_ops(b)
+    M = 3000
+    pos = rng.uniform(-130, 130, (M, 3))
+    world = rng.integers(0, 2, M).astype(np.uint32)
+    sender = rng.integers(0, 3000, M).astype(np.uint32)
+    repl = rng.integers(0, 3, M).astype(np.uint8)
+    t_pos = torch.from_numpy(pos).to(dev)
+    t_w = torch.from_numpy(world.view(np.int32)).to(dev)
+    t_s = torch.from_numpy(sender.view(np.int32)).to(dev)
+    t_r = torch.from_numpy(repl).to(dev)
+    offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    cap = 64 * M
+    peers = torch.empty(cap, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+    r.route_device(t_pos.data_ptr(), t_w.data_ptr(), t_s.data_ptr(), t_r.data_ptr(), M, offs.data_ptr(),
+                   peers.data_ptr(), None, cap, cnt.data_ptr())
+    torch.cuda.synchronize(dev)
+    err = int(cnt.cpu().numpy()[20:24].view(np.uint32)[0])
+    want = o.route(pos, world, sender, repl)
+    if err == 0:  # the batch had been folded in (re-applied) before the tick
+        got_offs = offs.cpu().numpy().view(np.uint32)
+        assert (got_offs == want[0]).all()
+        assert (peers.cpu().numpy().view(np.uint32)[: got_offs[-1]] == want[1]).all()
+    else:
+        assert err == 8
+    inc, fb = r.update_counts()  # folds the batch in: re-applied through the rebuild
+    assert fb == 1
+    r.route_health()  # clear the sticky bits of the flagged tick, if any
+    _check(r, o, pos, world, sender, repl)
+    assert r.route_health() == (0, 0)
+    del d_ops

@@ -380,6 +380,9 @@ class Router:
     def check_health(self) -> None:
         """Raises WQError when any tick since the last check reported an error or an overflow."""
         e, o = self.route_health()
+        if e & 8:
+            raise WQError(abi.WQ_E_INVALID, f"a tick ran on a table still missing an incremental batch the "
+                                            f"device could not apply (error bits {e:#x})")
         if e & 4:
             raise WQError(abi.WQ_E_TIMEOUT, f"a route look-back spin gave up (error bits {e:#x})")
         if e or o:
