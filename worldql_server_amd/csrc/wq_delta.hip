@@ -964,9 +964,10 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     }
     // buckets of ~128 ops (a wave's window is 256): sorted bits = log2(n / 128), at most 16 (two
     // radix passes), and enough that a bucket spans at most 2^16 slots (the in-window key field)
-    int sbits = 0;
-    while (sbits < 16 && ((uint64_t)128 << (sbits + 1)) <= n) sbits++;
-    if (sbits < 1) sbits = 1;
+    // (the real buckets are 2^(sbits - 1): the top sorted bit only parts kNoKey ops off)
+    static const uint64_t per_bucket = getenv("WQ_DELTA_OPS_PER_BUCKET") ? strtoull(getenv("WQ_DELTA_OPS_PER_BUCKET"), nullptr, 10) : 128;
+    int sbits = 1;
+    while (sbits < 16 && (per_bucket << sbits) <= n) sbits++;
     if (sbits > rbits + 1) sbits = rbits + 1;
     if (rbits + 1 - sbits > 16) sbits = rbits + 1 - 16;
     const int lowbits = rbits + 1 - sbits;
