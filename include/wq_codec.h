@@ -1,4 +1,4 @@
-/* wq_codec.h — host-side wire codec feeding the routing tick.
+/* wq_codec.h — host-side wire codec either side of the routing tick.
  *
  * Replaces, for a whole batch of received frames at once, the per-message
  *   Message::deserialize          worldql_server/src/structures/message.rs:136-142
@@ -67,6 +67,74 @@ int wq_decode_messages(const uint8_t* data, const uint64_t* offsets, size_t n, w
 #define WQ_SAN_INVALID_CHARS 4
 #define WQ_SAN_TOO_LONG 5
 int wq_sanitize_world_name(const char* name, size_t len, char* out, size_t cap, size_t* out_len);
+
+/* ---- serialize: the egress half of F4 -------------------------------------------------------
+ * Replaces Message::serialize (structures/message.rs:120-134): Message -> MessageT (message.rs:28-52,
+ * record.rs:18-26, entity.rs:17-25), MessageT::pack (WorldQLFB_generated.rs:1133-1173, RecordT /
+ * EntityT::pack :619-645 / :838-864) into a reset FlatBufferBuilder (flatbuffers 2.0.0, Cargo.lock:
+ * 347-349), finish(root, None). The bytes are the ones that builder lays down: back-to-front, fields
+ * added in the generated create() order (:1045-1055, :449-457, :668-676), scalars equal to their
+ * default (Heartbeat, ExceptSelf) omitted, vtables shared within the frame. PeerMap::broadcast_to
+ * serializes a routed message once for all its recipients (transport/peer_map.rs:22-40); the batch
+ * entry point does that for a whole tick's messages on the host's cores. Host code only. */
+
+/* A Record (structures/record.rs:8-15) or an Entity (entity.rs:7-14). Strings are UTF-8 bytes
+ * (not NUL-terminated). For an Entity the position is not optional and has_position is ignored. */
+typedef struct wq_record_in {
+    uint8_t uuid[16];          /* written as uuid 0.8.2's to_string(): lower-case hyphenated */
+    uint8_t has_position;
+    uint8_t has_data;          /* data: Option<String> */
+    uint8_t has_flex;          /* flex: Option<Bytes> */
+    uint8_t pad_[5];
+    double position[3];
+    const char* world_name;
+    uint64_t world_len;
+    const char* data;
+    uint64_t data_len;
+    const uint8_t* flex;
+    uint64_t flex_len;
+} wq_record_in;
+
+/* A Message (structures/message.rs:13-24). */
+typedef struct wq_message_in {
+    uint8_t instruction;       /* wire code: 0..12, or 255 (Unknown, the Default) */
+    uint8_t replication;       /* 0 ExceptSelf, 1 IncludingSelf, 2 OnlySelf */
+    uint8_t has_position;
+    uint8_t has_parameter;
+    uint8_t has_flex;
+    uint8_t pad_[3];
+    uint8_t sender_uuid[16];
+    double position[3];
+    const char* parameter;
+    uint64_t parameter_len;
+    const char* world_name;
+    uint64_t world_len;
+    const uint8_t* flex;
+    uint64_t flex_len;
+    const wq_record_in* records;
+    uint64_t n_records;
+    const wq_record_in* entities;
+    uint64_t n_entities;
+} wq_message_in;
+
+#define WQ_SER_INVALID_ARG -1
+#define WQ_SER_SHORT -2        /* out has fewer than the needed bytes: the size is reported, nothing else */
+#define WQ_SER_INVALID_UTF8 -3 /* a string field is not UTF-8 (a Rust String cannot hold it) */
+#define WQ_SER_TOO_LARGE -4    /* the builder's 2 GiB limit (it panics there; 1 GiB frames at most) */
+
+/* One frame into out[0 .. *out_len). On WQ_SER_SHORT, *out_len is the size needed. */
+int wq_serialize_message(const wq_message_in* m, uint8_t* out, size_t cap, size_t* out_len);
+
+/* n frames back to back: frame i is out[offsets[i] .. offsets[i + 1]) (offsets has n + 1 entries,
+ * always filled when the messages are valid). WQ_SER_SHORT when offsets[n] > cap; on any other
+ * error the first failing message's code is returned. n_threads <= 0: a default from n and the
+ * host's cores. */
+int wq_serialize_messages(const wq_message_in* msgs, size_t n, uint8_t* out, size_t cap, uint64_t* offsets,
+                          int n_threads);
+
+/* An upper bound of the bytes wq_serialize_messages writes for these messages. With out holding
+ * at least this many bytes the frames are packed in place (one pass, no staging copy). */
+size_t wq_serialize_bound(const wq_message_in* msgs, size_t n);
 
 #ifdef __cplusplus
 }

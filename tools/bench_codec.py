@@ -1,5 +1,7 @@
-"""Throughput of the host wire codec (wq_decode_messages) on a tick of C2-sized
-LocalMessage frames (1M frames, one world, random sender uuids and positions), 1 and N threads.
+"""Throughput of the host wire codec on a tick of C2-sized LocalMessage frames
+(1M frames, one world, random sender uuids and positions), 1 and N threads: wq_decode_messages over
+the received frames, and wq_serialize_messages re-encoding the same messages for their recipients
+(Message::serialize, once per routed message as PeerMap::broadcast_to does).
 Usage: python tools/bench_codec.py [--frames N] [--threads T]"""
 import argparse
 import json
@@ -41,6 +43,37 @@ def main():
             best = min(best, time.perf_counter() - t0)
         assert (out["status"] == 0).all()
         res[f"threads_{t}"] = {"s": best, "frames_per_s": a.frames / best, "GB_per_s": len(data) / best / 1e9}
+    # serialize: the decoded fields back into frames (wq_message_in built with numpy, no Python loop)
+    import ctypes
+    lib = codec._lib()
+    world = b"world"
+    wbuf = ctypes.create_string_buffer(world)
+    mi = np.zeros(a.frames, dtype=np.dtype([("instruction", "u1"), ("replication", "u1"), ("has_position", "u1"),
+                                            ("has_parameter", "u1"), ("has_flex", "u1"), ("pad", "u1", 3),
+                                            ("sender_uuid", "u1", 16), ("position", "<f8", 3), ("rest", "<u8", 10)]))
+    assert mi.dtype.itemsize == ctypes.sizeof(codec.WqMessageIn)
+    mi["instruction"] = out["instruction"]
+    mi["replication"] = out["replication"]
+    mi["has_position"] = out["has_position"]
+    mi["sender_uuid"] = out["sender_uuid"]
+    mi["position"] = out["position"]
+    mi["rest"][:, 2] = ctypes.addressof(wbuf)  # world_name pointer
+    mi["rest"][:, 3] = len(world)
+    offs = np.zeros(a.frames + 1, dtype=np.uint64)
+    cap = lib.wq_serialize_bound(mi.ctypes.data, a.frames)
+    sbuf = np.zeros(cap, dtype=np.uint8)
+    for t in (1, a.threads):
+        best = 1e9
+        for _ in range(3):
+            t0 = time.perf_counter()
+            rc = lib.wq_serialize_messages(mi.ctypes.data, a.frames, sbuf.ctypes.data, cap, offs.ctypes.data, t)
+            best = min(best, time.perf_counter() - t0)
+            assert rc == 0
+        res[f"serialize_threads_{t}"] = {"s": best, "frames_per_s": a.frames / best,
+                                         "GB_per_s": int(offs[-1]) / best / 1e9}
+    back = codec.decode_packed(sbuf[:int(offs[-1])], offs)
+    assert (back["status"] == 0).all() and np.array_equal(back["sender_uuid"], out["sender_uuid"])
+    res["serialize_frame_bytes"] = int(offs[1])
     print(json.dumps(res))
 
 
