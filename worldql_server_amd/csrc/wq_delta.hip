@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <vector>
 
+#include "lane_xchg.hpp"
 #include "table_prims.hpp"
 
 namespace wq {
@@ -220,8 +221,7 @@ struct BucketLds {
     uint32_t lst[kRoundWords];      // a round's staged old lists (flat), or the wave path's one list
     union {
         struct {                    // a round
-            uint8_t own[kRoundWords];  // staged word -> its cube (round-local)
-            uint8_t rmf[kRoundWords];  // staged word removed
+            uint16_t wf[kRoundWords];  // staged word: bit 15 removed, bits 0-14 adds placed right before it
             uint8_t fl[kWin];          // per op: 1 add / 2 remove
             uint16_t at[kWin];         // per op: #old peers below it
             uint16_t pa[kWin + 1];     // exclusive prefix of add flags over the round's ops
@@ -237,10 +237,34 @@ struct BucketLds {
     uint32_t cpre[65];              // round: per cube, first staged word
     uint32_t cdst[64];              // round: per cube, where the new list goes (kNone: unchanged)
     uint32_t cslot[64];             // round: per cube, its record slot
+    uint16_t cR[64];                // round: per cube, removed staged words before its first word
+    uint16_t cA[64];                // round: per cube, adds placed before its first word
+    uint64_t smask[kRoundWords / 64];  // round: bit x = staged word x starts a cube's list
+    uint16_t mcum[kRoundWords / 64];   // round: list starts in the mask words before this one
+    uint8_t su[64];                 // round: the cubes with staged words, in order
+    uint64_t bigm[kWin / 64];       // window: cubes (cs index) the wave path takes
     uint16_t cs[kWin + 1];          // cube starts in op[]
-    uint16_t big[kWin];             // cubes (cs index) the wave path takes
     uint8_t cid[kWin];              // per op: its cube (window-local index mod 256)
 };
+
+// The round cube owning staged word x (the last list start at or before x).
+__device__ __forceinline__ uint32_t owner_of(const BucketLds& sm, uint32_t x) {
+    const uint32_t j = x >> 6;
+    const uint64_t upto = (2ull << (x & 63)) - 1ull;  // bits 0..x & 63 (all ones for bit 63)
+    return sm.su[sm.mcum[j] + (uint32_t)__popcll(sm.smask[j] & upto) - 1];
+}
+
+// a[r] of lane (lane ^ j), j a power of two below 64 (a constant once the sort is unrolled)
+__device__ __forceinline__ uint64_t xchg_dyn_u64(uint64_t v, int j, int lane) {
+    switch (j) {
+        case 1: return xchg_u64<1>(v, lane);
+        case 2: return xchg_u64<2>(v, lane);
+        case 4: return xchg_u64<4>(v, lane);
+        case 8: return xchg_u64<8>(v, lane);
+        case 16: return xchg_u64<16>(v, lane);
+        default: return xchg_u64<32>(v, lane);
+    }
+}
 
 // Bitonic sort of 64 * E u64 held strided (element r * 64 + lane in a[r]) by one wave, ascending.
 template <int E>
@@ -265,7 +289,7 @@ __device__ __forceinline__ void wave_bitonic(uint64_t (&a)[4], int lane) {
             } else {
 #pragma unroll
                 for (int r = 0; r < E; ++r) {
-                    const uint64_t o = __shfl_xor(a[r], j, 64);
+                    const uint64_t o = xchg_dyn_u64(a[r], j, lane);
                     const bool up = ((r * 64 + lane) & k) == 0;
                     const bool keep_min = ((lane & j) == 0) == up;
                     a[r] = keep_min ? (o < a[r] ? o : a[r]) : (o > a[r] ? o : a[r]);
@@ -298,6 +322,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
         const uint32_t t = __shfl_up(v, d, 64);
         if (lane >= d) v += t;
     }
+    return v;
+}
+
+// Inclusive wave64 prefix sum by DPP row shifts and row broadcasts (no LDS round trips).
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
     return v;
 }
 
@@ -390,6 +425,7 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
             ncub += (uint32_t)__popcll(m);
         }
         if (lane == 0) sm.cs[ncub] = (uint16_t)cnt;
+        if (lane < kWin / 64) sm.bigm[lane] = 0;
         wave_lds_sync();
         // every cube's header at once (up to four record lines per lane in flight)
         {
@@ -453,7 +489,23 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
             if (act) {
                 sm.csrc[lane] = src_base;
                 sm.cslot[lane] = slot;
-                for (uint32_t i = 0; i < oc_st; ++i) sm.u.r.own[pre + i] = (uint8_t)lane;  // owner map
+            }
+            // owner map: a bit at each staged list's first word, the cubes with words in order
+            if (lane < (int)(kRoundWords / 64)) sm.smask[lane] = 0;
+            wave_lds_sync();
+            {
+                const bool has = oc_st > 0;  // (implies act)
+                const uint64_t mh = __ballot(has);
+                if (has) {
+                    sm.su[__popcll(mh & lt)] = (uint8_t)lane;
+                    atomicOr(reinterpret_cast<unsigned long long*>(&sm.smask[pre >> 6]), 1ull << (pre & 63));
+                }
+            }
+            wave_lds_sync();
+            {
+                const uint32_t pc = lane < (int)(kRoundWords / 64) ? (uint32_t)__popcll(sm.smask[lane]) : 0u;
+                const uint32_t ic = wave_incl_scan_u32(pc, lane);
+                if (lane < (int)(kRoundWords / 64)) sm.mcum[lane] = (uint16_t)(ic - pc);
             }
             wave_lds_sync();
             WQ_STAMP(2);
@@ -466,9 +518,9 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                     const uint32_t x = r * 64 + lane;
                     val[r] = 0u;
                     if (x < T) {
-                        const uint32_t u = sm.u.r.own[x];
+                        const uint32_t u = owner_of(sm, x);
                         val[r] = reinterpret_cast<const uint32_t*>(sm.csrc[u])[x - sm.cpre[u]];
-                        sm.u.r.rmf[x] = 0;
+                        sm.u.r.wf[x] = 0;
                     }
                 }
 #pragma unroll
@@ -493,10 +545,16 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                     if (last) {  // (a wave-path cube stages nothing: n0 = 0, and its cdst is kNone)
                         l2 = lds_lower_bound_fixed<kLaneList>(sm.lst + b0, n0, pp);
                         const bool present = l2 < n0 && sm.lst[b0 + l2] == pp;
-                        if ((x & 1u) && !present) f = 1;
+                        const uint32_t wpos = b0 + l2;
+                        uint32_t* wf32 = reinterpret_cast<uint32_t*>(sm.u.r.wf) + (wpos >> 1);
+                        if ((x & 1u) && !present) {
+                            f = 1;
+                            // an add lands right before old word l2 (none after the last one)
+                            if (l2 < n0) atomicAdd(wf32, 1u << (16 * (wpos & 1u)));
+                        }
                         if (!(x & 1u) && present) {
                             f = 2;
-                            sm.u.r.rmf[b0 + l2] = 1;
+                            atomicOr(wf32, 0x8000u << (16 * (wpos & 1u)));
                         }
                     }
                     sm.u.r.fl[q - qa0] = f;
@@ -549,28 +607,51 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
             }
             wave_lds_sync();
             WQ_STAMP(6);
-            // kept old peers: new index = old index - removes below + adds below (the adds below y
-            // = the cube's ops up to the first with peer >= y: a fixed-step search, no branches)
-#pragma unroll 4
-            for (uint32_t x = lane; x < T; x += 64) {
-                const uint32_t u = sm.u.r.own[x], d = sm.cdst[u];
-                if (d == kNone || sm.u.r.rmf[x]) continue;
-                const uint32_t y = sm.lst[x];
-                const uint32_t s0 = sm.cs[c0 + u], s1 = sm.cs[c0 + u + 1];
-                uint32_t lo = s0, len = s1 - s0;  // first op of the cube with peer >= y
+            // kept old peers: new index = old index - removed words below it + adds placed at or
+            // below it, both from flat prefix sums over the round's staged words less their value
+            // at the cube's first word. Eight chunks of 64 words at a time (independent chains).
+            {
+                constexpr int NG = 2;
+                uint32_t cr = 0, ca = 0;
+#pragma unroll 1
+                for (uint32_t g0 = 0; g0 < T; g0 += NG * 64) {
+                    uint32_t rex[NG], aex[NG];
 #pragma unroll
-                for (int st = 0; st < 8; ++st) {
-                    const uint32_t half = len >> 1;
-                    const bool right = half && op_peer(sm.op[lo + half - 1]) < y;
-                    lo += right ? half : 0u;
-                    len = right ? len - half : (half ? half : len);
+                    for (int r = 0; r < NG; ++r) {
+                        const uint32_t x = g0 + r * 64 + lane;
+                        const uint32_t w = x < T ? (uint32_t)sm.u.r.wf[x] : 0u;
+                        const uint64_t mr = __ballot(w >> 15);
+                        const uint32_t ac = w & 0x7FFFu;
+                        const uint32_t ainc = wave_incl_scan_dpp(ac);
+                        rex[r] = cr + (uint32_t)__popcll(mr & lt);
+                        aex[r] = (ca + ainc - ac) | (w & 0x8000u) << 16 | ac << 16;  // bit 31 removed, 16-30 ac
+                        cr += (uint32_t)__popcll(mr);
+                        ca += (uint32_t)__builtin_amdgcn_readlane((int)ainc, 63);
+                    }
+#pragma unroll
+                    for (int r = 0; r < NG; ++r) {
+                        const uint32_t x = g0 + r * 64 + lane;
+                        if (x < T && ((sm.smask[x >> 6] >> lane) & 1ull)) {
+                            const uint32_t u = owner_of(sm, x);
+                            sm.cR[u] = (uint16_t)rex[r];
+                            sm.cA[u] = (uint16_t)aex[r];
+                        }
+                    }
+                    wave_lds_sync();
+#pragma unroll
+                    for (int r = 0; r < NG; ++r) {
+                        const uint32_t x = g0 + r * 64 + lane;
+                        if (x >= T || (aex[r] >> 31)) continue;
+                        const uint32_t u = owner_of(sm, x), d = sm.cdst[u];
+                        if (d == kNone) continue;
+                        const uint32_t y = sm.lst[x];
+                        const uint32_t ax = aex[r] & 0xFFFFu, ac = (aex[r] >> 16) & 0x7FFFu;
+                        const uint32_t k = (x - sm.cpre[u]) - (rex[r] - sm.cR[u]) + (ax + ac - sm.cA[u]);
+                        if (d != kInlineOnly) L[d + 1 + k] = y;
+                        if (k < (uint32_t)kInline) reinterpret_cast<uint32_t*>(a.tb.recs + sm.cslot[u])[kInlineWord0 + k] = y;
+                        atomicOr(reinterpret_cast<unsigned long long*>(&sm.csig[u]), (unsigned long long)peer_sig(y));
+                    }
                 }
-                if (len && op_peer(sm.op[lo]) < y) ++lo;
-                const uint32_t k = (x - sm.cpre[u]) - (sm.u.r.pr[lo - qa0] - sm.u.r.pr[s0 - qa0]) +
-                                   (sm.u.r.pa[lo - qa0] - sm.u.r.pa[s0 - qa0]);
-                if (d != kInlineOnly) L[d + 1 + k] = y;
-                if (k < (uint32_t)kInline) reinterpret_cast<uint32_t*>(a.tb.recs + sm.cslot[u])[kInlineWord0 + k] = y;
-                atomicOr(reinterpret_cast<unsigned long long*>(&sm.csig[u]), (unsigned long long)peer_sig(y));
             }
             WQ_STAMP(7);
             // added peers: new index = #old below - removes below + adds below
@@ -595,16 +676,19 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                 uint32_t* inl = reinterpret_cast<uint32_t*>(rec) + kInlineWord0;
                 for (uint32_t k = nc; k < min(oc, (uint32_t)kInline); ++k) inl[k] = kNone;  // beyond oc: kNone already
             }
-            const uint64_t mb = __ballot(isbig);
-            if (isbig) sm.big[nbig + __popcll(mb & lt)] = (uint16_t)c;
-            nbig += (uint32_t)__popcll(mb);
+            if (isbig) atomicOr(reinterpret_cast<unsigned long long*>(&sm.bigm[c >> 6]), 1ull << (c & 63));
+            nbig += (uint32_t)__popcll(__ballot(isbig));
             wave_lds_sync();  // the next round restages lst
         }
         wave_lds_sync();
         WQ_STAMP(9);
         // ---- wave path: lists longer than kLaneList, one cube at a time ----
+        uint32_t bj = 0;
+        uint64_t brem = sm.bigm[0];
         for (uint32_t bi = 0; bi < nbig; ++bi) {
-            const uint32_t c = sm.big[bi];
+            while (!brem) brem = sm.bigm[++bj];
+            const uint32_t c = bj * 64 + (uint32_t)__builtin_ctzll(brem);
+            brem &= brem - 1ull;
             const uint32_t qa = sm.cs[c], qb = sm.cs[c + 1];
             const uint32_t slot = (B << a.lowbits) | (uint32_t)(sm.op[qa] >> 48);
             Record* rec = a.tb.recs + slot;
