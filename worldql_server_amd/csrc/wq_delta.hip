@@ -7,8 +7,8 @@
 // touches, not to the whole table. Three steps, no host read-back between them:
 //   events   each op -> packed cube key and its record slot (a new cube claims its record here,
 //            count 0); the op becomes one u64 sort key  slot << 33 | kind << 32 | peer
-//   bucket   one stable rocPRIM radix sort over the slot's high 16 bits: a bucket (2^lowbits
-//            adjacent slots, ~100-200 ops at C5) is contiguous, in op order
+//   bucket   a stable LSD radix sort (k_sort_*: two passes of <= 8 bits) over the slot's high
+//            bits: a bucket (2^lowbits adjacent slots, ~100-200 ops at C5) is contiguous, in op order
 //   apply    one wave per bucket: the bucket's ops (windows of 256) sorted in registers by (slot,
 //            peer, op) with a bitonic network, then one LANE per touched cube: it stages the cube's
 //            list in LDS, counts adds / removes (the last op of a peer wins), merges straight into
@@ -334,6 +334,153 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
     return v;
+}
+
+// ---- the bucket sort: stable LSD radix passes over the sort key's bucket field --------------
+// Per pass (digit = kSortBits or fewer bits): a per-tile digit histogram (tile = 4096 keys in op
+// order), a per-digit exclusive scan over the tiles, and a stable scatter in which each tile's
+// block ranks its keys round by round (a wave matches equal digits by ballots, the four waves'
+// counts are combined per digit in LDS). Two passes cover the <= 16 bucket bits.
+constexpr int kSortTile = 4096;
+constexpr int kSortPer = kSortTile / kBlock;  // keys per thread per tile
+
+// Exclusive prefix of v over a 256-thread block (sc: 4 words of LDS); *total = the block's sum.
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sc, uint32_t* total) {
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t incl = wave_incl_scan_dpp(v);
+    if (lane == 63) sc[wave] = incl;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        const uint32_t x = sc[w];
+        pre += w < wave ? x : 0u;
+        tot += x;
+    }
+    __syncthreads();
+    *total = tot;
+    return pre + incl - v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sort_hist(const uint64_t* __restrict__ keys, uint32_t n, int sh,
+                                                      uint32_t dmask, uint32_t ntiles, uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t h[256];
+    const int t = threadIdx.x;
+    h[t] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+    uint32_t d[kSortPer];
+#pragma unroll
+    for (int r = 0; r < kSortPer; ++r) {
+        const uint64_t i = base + (uint64_t)r * kBlock + t;
+        d[r] = i < n ? (uint32_t)(keys[i] >> sh) & dmask : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int r = 0; r < kSortPer; ++r)
+        if (d[r] != 0xFFFFFFFFu) atomicAdd(&h[d[r]], 1u);
+    __syncthreads();
+    if ((uint32_t)t <= dmask) cnt[(uint64_t)t * ntiles + blockIdx.x] = h[t];
+}
+
+// One block per digit: its row of tile counts -> exclusive prefixes (in place), and the total.
+__global__ __launch_bounds__(kBlock) void k_sort_rowscan(uint32_t* __restrict__ cnt, uint32_t ntiles,
+                                                         uint32_t* __restrict__ tot) {
+    __shared__ uint32_t sc[kBlock / 64];
+    uint32_t* row = cnt + (uint64_t)blockIdx.x * ntiles;
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < ntiles; c0 += kBlock) {
+        const uint32_t j = c0 + threadIdx.x;
+        const uint32_t v = j < ntiles ? row[j] : 0u;
+        uint32_t s;
+        const uint32_t ex = block_excl_scan256(v, sc, &s);
+        if (j < ntiles) row[j] = carry + ex;
+        carry += s;
+    }
+    if (threadIdx.x == 0) tot[blockIdx.x] = carry;
+}
+
+// Each wave ranks a quarter of the tile (1024 consecutive keys, 64 per round) against its own
+// digit counters (no block barrier per round); the quarters are then combined per digit, the
+// tile's keys staged in LDS in digit order, and written out in runs (a digit's keys of one tile
+// are contiguous in the output).
+__global__ __launch_bounds__(kBlock) void k_sort_scatter(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
+                                                         uint32_t n, int sh, uint32_t dmask, int dbits,
+                                                         uint32_t ntiles, const uint32_t* __restrict__ rowpre,
+                                                         const uint32_t* __restrict__ tot) {
+    constexpr int NW = kBlock / 64, QR = kSortTile / kBlock;  // waves; rounds per wave
+    __shared__ uint64_t stage[kSortTile];
+    __shared__ uint32_t gbase[256], lstart[256], wcnt[NW][256], sc[NW];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t tile = blockIdx.x;
+    {
+        const bool dig = (uint32_t)t <= dmask;
+        const uint64_t rp = (uint64_t)t * ntiles + tile;
+        const uint32_t cur = dig ? rowpre[rp] : 0u;
+        const uint32_t nxt = dig ? (tile + 1 < ntiles ? rowpre[rp + 1] : tot[t]) : 0u;
+        uint32_t s0, s1;
+        const uint32_t gex = block_excl_scan256(dig ? tot[t] : 0u, sc, &s0);
+        const uint32_t lex = block_excl_scan256(nxt - cur, sc, &s1);  // this tile's keys of digit t
+        gbase[t] = gex + cur;
+        lstart[t] = lex;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) wcnt[w][t] = 0;
+    }
+    const uint64_t t0 = (uint64_t)tile * kSortTile;
+    const uint32_t cnt = (uint32_t)min((uint64_t)kSortTile, (uint64_t)n - t0);
+    const uint32_t q0 = (uint32_t)wave * (kSortTile / NW);  // this wave's quarter
+    uint64_t k[QR];
+#pragma unroll
+    for (int r = 0; r < QR; ++r) {
+        const uint32_t i = q0 + r * 64 + lane;
+        k[r] = i < cnt ? in[t0 + i] : 0ull;
+    }
+    __syncthreads();
+    uint32_t lr[QR];
+#pragma unroll
+    for (int r = 0; r < QR; ++r) {
+        const bool valid = q0 + r * 64 + lane < cnt;
+        const uint32_t d = (uint32_t)(k[r] >> sh) & dmask;
+        uint64_t eq = __ballot(valid);
+        for (int b = 0; b < dbits; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t m = __ballot(bit);
+            eq &= bit ? m : ~m;
+        }
+        const uint32_t rank = (uint32_t)__popcll(eq & lt);
+        const uint32_t old = valid ? wcnt[wave][d] : 0u;
+        lr[r] = old + rank;
+        wave_lds_sync();
+        if (valid && rank == 0) wcnt[wave][d] = old + (uint32_t)__popcll(eq);
+        wave_lds_sync();
+    }
+    __syncthreads();
+    if ((uint32_t)t <= dmask) {  // per digit: the waves' counts -> their exclusive prefixes
+        uint32_t acc = lstart[t];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t c = wcnt[w][t];
+            wcnt[w][t] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < QR; ++r) {
+        const bool valid = q0 + r * 64 + lane < cnt;
+        const uint32_t d = (uint32_t)(k[r] >> sh) & dmask;
+        if (valid) stage[wcnt[wave][d] + lr[r]] = k[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < QR; ++r) {
+        const uint32_t j = r * kBlock + t;
+        if (j < cnt) {
+            const uint64_t x = stage[j];
+            const uint32_t d = (uint32_t)(x >> sh) & dmask;
+            out[gbase[d] + (j - lstart[d])] = x;
+        }
+    }
 }
 
 // Record words 2..6 {count, list_off, sig lo, sig hi, cap} of slot.
@@ -1072,14 +1219,26 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
                        (int64_t)h->cube_size, t.recs.as<Record>(), t.rclaim.as<uint32_t>(),
                        kBatchTag | (uint32_t)(++h->n_delta_batches & 0x7FFFFFFFu), t.rec_cap - 1, t.rec_shift,
                        h->hash_mask, keys, status);
-    size_t bytes = 0;
-    const int b0 = 33 + lowbits, b1 = 34 + rbits;
-    // onesweep at every size (rocPRIM's default takes a merge sort below 2^20 items: ~20 launches)
-    using Onesweep = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                rocprim::default_config, 0>;
-    WQ_HIP(h, rocprim::radix_sort_keys<Onesweep>(nullptr, bytes, keys, skeys, (size_t)n, b0, b1, s));
-    WQ_ALLOC(h, h->sort_tmp, bytes);
-    WQ_HIP(h, rocprim::radix_sort_keys<Onesweep>(h->sort_tmp.p, bytes, keys, skeys, (size_t)n, b0, b1, s));
+    // stable LSD passes over the bucket field: key bits [33 + lowbits, 33 + lowbits + sbits)
+    const uint32_t ntiles = (uint32_t)((n + kSortTile - 1) / kSortTile);
+    WQ_ALLOC(h, d.sort_cnt, (uint64_t)256 * ntiles * 4);
+    WQ_ALLOC(h, d.sort_tot, 256 * 4);
+    const int fbits = rbits + 1 - lowbits;  // == sbits
+    const int p1 = std::min(fbits, 8), p2 = fbits - p1;
+    auto sort_pass = [&](const uint64_t* in, uint64_t* out, int sh, int bits) {
+        const uint32_t dmask = (1u << bits) - 1u;
+        hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(kBlock), 0, s, in, n, sh, dmask, ntiles,
+                           d.sort_cnt.as<uint32_t>());
+        hipLaunchKernelGGL(k_sort_rowscan, dim3(dmask + 1), dim3(kBlock), 0, s, d.sort_cnt.as<uint32_t>(), ntiles,
+                           d.sort_tot.as<uint32_t>());
+        hipLaunchKernelGGL(k_sort_scatter, dim3(ntiles), dim3(kBlock), 0, s, in, out, n, sh, dmask, bits, ntiles,
+                           d.sort_cnt.as<uint32_t>(), d.sort_tot.as<uint32_t>());
+    };
+    sort_pass(keys, skeys, 33 + lowbits, p1);
+    if (p2 > 0) {
+        sort_pass(skeys, keys, 33 + lowbits + p1, p2);
+        std::swap(keys, skeys);  // the sorted keys are in key64_a
+    }
     uint32_t* bstart = h->cube_start.as<uint32_t>();
     hipLaunchKernelGGL(k_bucket_bounds, dim3(grid_for((uint64_t)NBr + 1)), dim3(kBlock), 0, s, skeys, n, lowbits, NBr,
                        bstart);

@@ -86,6 +86,8 @@ struct DeltaWs {
     DevBuf part, summ;      // REMOVE_PEER per-block partial sums; a batch's DeltaStatus
     DevBuf dstat;           // i64 x2: entry / live-cube deltas of batches not yet read back
     DevBuf rm_bits;         // REMOVE_PEER from every world: bitmap over peer ids
+    DevBuf sort_cnt;        // bucket sort: per (digit, tile) key counts, then their row prefixes
+    DevBuf sort_tot;        // bucket sort: per digit key totals
 };
 
 // Route workspace, persistent across calls so a tick needs no memset: two counter slots (each
