@@ -29,31 +29,36 @@ struct TileScanParams {
     const uint32_t* stale = nullptr;  // the table's stale word (check_stale)
 };
 
-__device__ __forceinline__ uint64_t wave_incl_scan_add64(uint64_t v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
+// Inclusive wave64 prefix sum of u32 by DPP row shifts and row broadcasts (no LDS round trips).
+__device__ __forceinline__ uint32_t wave_incl_scan_u32_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
     return v;
 }
 
 // One pass of the block covers 16,384 tiles (C3's 39,063 take three): wave w scans its 1,024-tile
 // chunk as 16 coalesced rows of 64 (row k = tiles chunk + 64k + lane) with a running carry, the
 // chunk totals are scanned across the 16 waves in LDS, and the rows are written with the wave's
-// offset. Every load and store is one contiguous 256-byte wave access (a per-thread run of 16
-// tiles instead made each load touch 64 separate segments: ~58 us on C3; one tile per thread and
-// pass took 39 passes: ~70 us).
+// offset. Every load and store is one contiguous 256-byte wave access. The prefixes are u32 (as
+// the CSR offsets are; they wrap only when P > 2^32 - 1, which error bit 2 reports) and are scanned
+// by DPP; P itself is summed exactly in u64. (The first version scanned 64-bit values with
+// __shfl_up, 12 LDS permutes per row: 21 us for C2's 3,907 tiles.)
 constexpr int kScanRows = 16;
 
 static __global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScanParams p) {
-    __shared__ uint64_t s_wave[kScanWaves];
+    __shared__ uint32_t s_wave[kScanWaves];
+    __shared__ uint64_t s_tot[kScanWaves];
     __shared__ uint64_t s_F[kScanWaves];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint64_t carry = 0, F = 0;
     for (uint32_t base = 0; base < p.n_tiles; base += kScanThreads * kScanRows) {
         const uint32_t c0 = base + (uint32_t)wave * (64 * kScanRows) + lane;
         uint32_t v[kScanRows];
+        uint64_t lane_sum = 0;
 #pragma unroll
         for (int k = 0; k < kScanRows; ++k) {
             const uint32_t i = c0 + 64u * k;
@@ -61,27 +66,32 @@ static __global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScan
             v[k] = in ? p.tile_total[i] : 0u;
             F += in ? p.tile_F[i] : 0u;
         }
-        uint64_t run = 0;  // wave-local exclusive prefix of each row element
-        uint64_t ex[kScanRows];
+        uint32_t run = 0;  // wave-local exclusive prefix of each row element (u32, wrapping)
+        uint32_t ex[kScanRows];
 #pragma unroll
         for (int k = 0; k < kScanRows; ++k) {
-            const uint64_t incl = wave_incl_scan_add64(v[k], lane);
+            const uint32_t incl = wave_incl_scan_u32_dpp(v[k]);
             ex[k] = run + incl - v[k];
-            run += __shfl(incl, 63, 64);
+            run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            lane_sum += v[k];
         }
-        if (lane == 0) s_wave[wave] = run;
+        const uint64_t wtot = wave_sum_u64(lane_sum);  // exact
+        if (lane == 0) {
+            s_wave[wave] = run;
+            s_tot[wave] = wtot;
+        }
         __syncthreads();
-        uint64_t before = carry, tot = 0;
+        uint32_t before = (uint32_t)carry;
+        uint64_t tot = 0;
 #pragma unroll
         for (int u = 0; u < kScanWaves; ++u) {
-            const uint64_t t = s_wave[u];
-            if (u < wave) before += t;
-            tot += t;
+            if (u < wave) before += s_wave[u];
+            tot += s_tot[u];
         }
 #pragma unroll
         for (int k = 0; k < kScanRows; ++k) {
             const uint32_t i = c0 + 64u * k;
-            if (i < p.n_tiles) p.tile_prefix[i] = (uint32_t)(before + ex[k]);
+            if (i < p.n_tiles) p.tile_prefix[i] = before + ex[k];
         }
         carry += tot;
         __syncthreads();
@@ -133,7 +143,7 @@ static __global__ __launch_bounds__(kBlock) void tile_finish_kernel(TileScanPara
 
 constexpr uint32_t kScanOneBlockMax = 8192;  // tiles: up to here the one-block scan is the faster
 
-// The tick's tile scan (n_tiles >= 1): one block for a few thousand tiles (C2: 3,907, ~5 us),
+// The tick's tile scan (n_tiles >= 1): one block for a few thousand tiles (C2: 3,907),
 // rocPRIM + tile_finish_kernel beyond. P must fit the u32 offsets either way (error bit 2 if not);
 // a tick of > 2^32 pairs wraps the prefix, which the error bit already reports.
 inline int launch_tile_scan(wq_router* h, const TileScanParams& sp) {

@@ -161,7 +161,7 @@ __device__ __forceinline__ void stage_image(EmitRowSmem<STAGE>& es, const TableV
 // Copy a complete image of T outputs to the global output at g0 (every thread of the block; the
 // image is complete and a barrier passed): 16-byte quads aligned to the global output, the
 // block's first and last quads (shared with its neighbours) word by word.
-template <int STAGE>
+template <int STAGE, bool NT = false>
 __device__ __forceinline__ void copy_image_out(const EmitRowSmem<STAGE>& es, const EmitOut& out, uint32_t m0,
                                                uint64_t g0, uint32_t T) {
     const int tid = threadIdx.x;
@@ -174,10 +174,17 @@ __device__ __forceinline__ void copy_image_out(const EmitRowSmem<STAGE>& es, con
         if (qd >= lead && qd + 4 <= span && out0 + 4 <= out.capacity) {
             const u32x4_lds pv = *reinterpret_cast<const u32x4_lds*>(&es.op[qd - lead]);
             const uint32_t mv = *reinterpret_cast<const u32_a1*>(&es.om[qd - lead]);
-            *reinterpret_cast<uint4*>(out.peers + out0) = make_uint4(pv.x, pv.y, pv.z, pv.w);
-            if (out.msgs)
-                *reinterpret_cast<uint4*>(out.msgs + out0) = make_uint4(
-                    m0 + (mv & 0xFF), m0 + ((mv >> 8) & 0xFF), m0 + ((mv >> 16) & 0xFF), m0 + (mv >> 24));
+            const uint4 pq = make_uint4(pv.x, pv.y, pv.z, pv.w);
+            const uint4 mq = make_uint4(m0 + (mv & 0xFF), m0 + ((mv >> 8) & 0xFF), m0 + ((mv >> 16) & 0xFF), m0 + (mv >> 24));
+            if (NT) {  // streamed: nothing on the GPU reads the pairs back in this tick
+                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(v4u{pq.x, pq.y, pq.z, pq.w}, reinterpret_cast<v4u*>(out.peers + out0));
+                if (out.msgs)
+                    __builtin_nontemporal_store(v4u{mq.x, mq.y, mq.z, mq.w}, reinterpret_cast<v4u*>(out.msgs + out0));
+            } else {
+                *reinterpret_cast<uint4*>(out.peers + out0) = pq;
+                if (out.msgs) *reinterpret_cast<uint4*>(out.msgs + out0) = mq;
+            }
         } else {
 #pragma unroll
             for (uint32_t i = 0; i < 4; ++i) {
@@ -190,7 +197,7 @@ __device__ __forceinline__ void copy_image_out(const EmitRowSmem<STAGE>& es, con
     }
 }
 
-template <bool RAW_KEYS, int STAGE, int U>
+template <bool RAW_KEYS, int STAGE, int U, bool NT = false>
 __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
     // U: record lines in flight per lane in the fallback emit_row
     static_assert(STAGE % 4 == 0, "STAGE: whole 16-byte quads");
@@ -280,7 +287,7 @@ __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
     // ---- 5. offsets, copy-out ----
     if (m < p.in.M) p.offsets[m] = (uint32_t)(g0 + st);
     if (p.out.peers) {
-        if (fits) copy_image_out<STAGE>(sm.es, p.out, m0, g0, T);
+        if (fits) copy_image_out<STAGE, NT>(sm.es, p.out, m0, g0, T);
         else emit_direct<4>(sm.es, tv, p.out, m0, g0, T);
     }
     if (stamp) p.stamps[4 * b + 3] = __builtin_amdgcn_s_memrealtime();

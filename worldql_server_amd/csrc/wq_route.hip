@@ -52,22 +52,23 @@ void launch_count(const CountParams& p, hipStream_t s, unsigned grid) {
         hipLaunchKernelGGL((count_kernel<false, IPT, MINW, 0, FULL>), dim3(grid), dim3(kBlock), 0, s, p);
 }
 
-template <int STAGE, int U>
+template <int STAGE, int U, bool NT = false>
 void launch_tick(const TickParams& p, hipStream_t s, unsigned grid) {
     if (p.in.keys)
-        hipLaunchKernelGGL((tick_kernel<true, STAGE, U>), dim3(grid), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL((tick_kernel<true, STAGE, U, NT>), dim3(grid), dim3(kBlock), 0, s, p);
     else
-        hipLaunchKernelGGL((tick_kernel<false, STAGE, U>), dim3(grid), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL((tick_kernel<false, STAGE, U, NT>), dim3(grid), dim3(kBlock), 0, s, p);
 }
 
 #define WQ_CFG3(cipt, minw, stage) {kBlock * cipt, &launch_count<cipt, minw>, stage, 0, nullptr, 0, 0}
 #define WQ_CFG3H(r) {kBlock, &launch_count<1, 8>, 4096 + 2, 0, nullptr, 0, r}
-#define WQ_CFG1(stage, u) {kBlock, &launch_count<1, 8>, 4096, stage, &launch_tick<stage, u>, 0, 0}
+#define WQ_CFG1(stage, u) {kBlock, &launch_count<1, 8>, 4096, stage, &launch_tick<stage, u, true>, 0, 0}
 #define WQ_CFGS(stage) {kBlock, &launch_count<1, 8>, 4096, 0, nullptr, stage, 0}
 // Three launches: count (messages per lane, min waves per SIMD) / tile_scan / emit. One launch:
 // messages per block; its three-launch fallback (too many blocks to be resident) is count 4/2.
 const Cfg kCfgs[] = {
-    WQ_CFG1(2816, 2),         // 0: default, single launch; 20.3 KB LDS -> 8 blocks per CU (63.3 us on C2)
+    WQ_CFG1(2816, 2),         // 0: default, single launch; 20.3 KB LDS -> 8 blocks per CU (63.3 us on C2);
+                              //    the image leaves by non-temporal 16-byte stores (streamed, never re-read)
     WQ_CFG3(1, 8, 4096 + 2),  // 1: three launches (73 us on C2)
     WQ_CFG1(4096, 2),         // 2
     WQ_CFG3(1, 8, 4096 + 8),  // 3
@@ -82,6 +83,9 @@ const Cfg kCfgs[] = {
     //     before the peer loads land: 1467)
     WQ_CFG3H(116),
     WQ_CFG3H(108),            // 11: ... 8 per window
+    // 12: cfg 0 with plain (not non-temporal) copy-out stores: C2 64.8 us against cfg 0's 63.2
+    //     (tools/tune_route.py, 4 rounds; a non-temporal emit_map on C3 was 4% slower, not kept)
+    {kBlock, &launch_count<1, 8>, 4096, 2816, &launch_tick<2816, 2, false>, 0, 0},
 };
 #undef WQ_CFG1
 #undef WQ_CFGS
