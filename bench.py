@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--c2-shift", type=float, default=0.0,
                     help="C2 translated by this much on every axis (e.g. 2.5e7: Minecraft-scale coordinates)")
     ap.add_argument("--steps", type=int, default=None, help="timed ticks (default c3/c5 10, c4 20, c1/c2 50)")
-    ap.add_argument("--warmup", type=int, default=None, help="untimed ticks (default 10; c3/c4/c5 2)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed ticks (default c1/c2 200, c3 20: ~12-30 ms, so the clocks have ramped; c4/c5 2)")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink C2 (tests only; 1.0 = the headline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline's routing work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -67,7 +68,10 @@ def _default_steps(a):
     if a.steps is None:
         a.steps = {"c1": 50, "c2": 50, "c3": 10, "c4": 20, "c5": 10}[a.config]
     if a.warmup is None:
-        a.warmup = 10 if a.config in ("c1", "c2") else 2
+        # untimed ticks long enough for the GPU clocks to ramp after the host-side table build
+        # (measured: C2 61.3 us after 10 warm-up ticks, 60.0 us after 500; C3 1.423 / 1.412 ms
+        # after 2 / 30)
+        a.warmup = {"c1": 200, "c2": 200, "c3": 20}.get(a.config, 2)
 
 
 def algorithmic_bytes(M: int, F: int, P: int) -> int:
