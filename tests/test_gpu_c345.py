@@ -88,6 +88,46 @@ def test_radius_boundary_long_lists_and_missing_positions():
     assert 0 in seg and 2 in seg and 1 not in seg and 3 not in seg
 
 
+def test_radius_f32_first_test_edges():
+    """within_radius decides from an f32 copy of the peer positions when the f64 result is certain
+    and reads the f64 coordinates otherwise: peers on the sphere to a few ulps (the deferred case),
+    coordinates where f32 has an ulp of 1 (1e7), beyond f32 (1e39 -> inf), subnormals, +-inf and NaN,
+    a radius that is not representable, for a long list (60 peers) and an inline cube (20 peers)."""
+    r, o = mk_router(), orc.COracle(16)
+    rng = synth.SplitMix64(7)
+    n_a, n_b = 60, 20
+    centre_a, centre_b = np.array([8.1, 7.3, 9.7]), np.array([1e7 + 8.3, 8.2, -7.9])
+    peer = np.arange(n_a + n_b, dtype=np.uint32)
+    sub = np.concatenate([np.tile(centre_a, (n_a, 1)), np.tile(centre_b, (n_b, 1))])
+    ops = abi.ops_array(np.zeros(len(peer), np.uint32), peer, np.zeros(len(peer), np.uint8), pos=sub)
+    r.apply_ops(ops)
+    o.apply_ops(ops)
+    radius = 5.1
+    u = rng.uniform(-1.0, 1.0, 3 * (n_a + n_b)).reshape(-1, 3)
+    u /= np.linalg.norm(u, axis=1)[:, None]
+    k = (np.arange(n_a + n_b) % 9 - 4).astype(np.float64)  # -4 .. 4 ulps around the sphere
+    d = radius * (1.0 + k * 2.0 ** -52)
+    pp = np.concatenate([centre_a + d[:n_a, None] * u[:n_a], centre_b + d[n_a:, None] * u[n_a:]])
+    pp[50] = [1e39, 8.0, 8.0]        # beyond f32: inf in the copy
+    pp[51] = [5e-310, 7.0, 9.0]      # subnormal in f64, 0 in f32
+    pp[52] = [np.inf, 7.0, 9.0]
+    pp[53] = [-np.inf, 7.0, 9.0]
+    pp[54] = [np.nan, 7.0, 9.0]
+    pp[55] = centre_a                # distance 0
+    pp[56] = centre_a + [radius, 0.0, 0.0]
+    r.set_peer_positions(pp)
+    r.set_radius(radius)
+    M = 300
+    mpos = np.where((np.arange(M) % 2 == 0)[:, None], centre_a[None, :], centre_b[None, :])
+    jit = np.where((np.arange(M) % 3 == 0)[:, None], rng.uniform(-1e-9, 1e-9, 3 * M).reshape(M, 3), 0.0)
+    mpos = mpos + jit * np.abs(mpos)
+    sender = rng.below(n_a + n_b, M)
+    repl = rng.below(3, M).astype(np.uint8)
+    got = r.route(mpos, np.zeros(M, np.uint32), sender, repl)
+    want = o.route_radius(mpos, np.zeros(M, np.uint32), sender, repl, pp, radius)
+    assert _same(got, want) > 0
+
+
 def test_radius_needs_positions():
     from worldql_server_amd.router import WQError
     r = mk_router()

@@ -211,6 +211,7 @@ struct TableView {
     double sf;
     // C5 radius filter (wq_set_radius): peer positions (n_ppos x 3) and r^2; r2 < 0: off
     const double* ppos;
+    const float4* ppos4;  // the same positions rounded to f32 {x, y, z, 0}: the first, exact-or-defer test
     uint32_t n_ppos;
     double r2;
     // per-peer boxes of the record cubes each peer is subscribed to (PeerBox); nullptr: none
@@ -262,8 +263,24 @@ __device__ __forceinline__ bool box_may_hold(const TableView& t, uint32_t peer, 
 
 // C5: is peer p within the radius of message position (mx, my, mz)? f64, left to right, no FMA
 // (this file is compiled with contraction off), a peer without a position never is.
+// First from the f32 copy of the position (one aligned 16-byte load instead of 24 bytes that
+// straddle a cache line one time in five): with pf = (double)(float)p, |p - pf| <= |pf| 2^-23 (plus
+// 2^-120 below f32's normal range), so the reference's dx = fl(mx - px) is within
+// e = |pf| 2^-23 + 2^-120 + |ax| 2^-50 of ax = fl(mx - pf), its square within e (2|ax| + e) of ax^2,
+// and its three roundings add at most 2^-50 (d2 + E1). Only when the exact d2 could lie on either
+// side of r^2 (or a value is NaN / beyond f32) are the f64 coordinates read.
 __device__ __forceinline__ bool within_radius(const TableView& t, double mx, double my, double mz, uint32_t p) {
     if (p >= t.n_ppos) return false;
+    const float4 f = t.ppos4[p];
+    const double ax = mx - (double)f.x, ay = my - (double)f.y, az = mz - (double)f.z;
+    const double d2f = ax * ax + ay * ay + az * az;
+    const double ex = fabs((double)f.x) * 0x1p-23 + 0x1p-120 + fabs(ax) * 0x1p-50;
+    const double ey = fabs((double)f.y) * 0x1p-23 + 0x1p-120 + fabs(ay) * 0x1p-50;
+    const double ez = fabs((double)f.z) * 0x1p-23 + 0x1p-120 + fabs(az) * 0x1p-50;
+    const double E1 = ex * (2.0 * fabs(ax) + ex) + ey * (2.0 * fabs(ay) + ey) + ez * (2.0 * fabs(az) + ez);
+    const double E = E1 * 1.001 + d2f * 0x1p-40 + 0x1p-1000;
+    if (d2f + E <= t.r2) return true;   // NaN: false
+    if (d2f - E > t.r2) return false;   // NaN: false
     const double* q = t.ppos + 3ull * p;
     const double dx = mx - q[0];
     const double dy = my - q[1];

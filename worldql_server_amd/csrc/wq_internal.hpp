@@ -156,6 +156,7 @@ struct wq_router {
     wq::DevBuf h_in, h_out;
     // C5 radius filter (wq_set_radius / wq_set_peer_positions)
     wq::DevBuf ppos;
+    wq::DevBuf ppos4;  // f32 copy (float4 per peer) for the radius filter's first test
     uint64_t n_ppos = 0;
     double radius = 0.0;
     wq::ProfileEvents prof;
@@ -175,6 +176,7 @@ inline TableView table_view(const wq_router* h) {
     v.list = h->tab.list.as<uint32_t>();
     v.sf = (double)h->cube_size;
     v.ppos = h->ppos.as<double>();
+    v.ppos4 = h->ppos4.as<float4>();
     v.n_ppos = (uint32_t)h->n_ppos;
     v.r2 = h->radius > 0.0 ? h->radius * h->radius : -1.0;
     v.n_pbox = h->tab.n_pbox;

@@ -141,7 +141,7 @@ int wq_router_destroy(wq_router* h) {
                       &h->key64_b, &h->flags, &h->scan, &h->sort_tmp, &h->small, &h->cube_id,
                       &h->cube_start, &h->rws.buf, &h->rws.info, &h->rws.e, &h->rws.tiles,
                       &h->h_in, &h->h_out, &h->tab.recs, &h->tab.rclaim, &h->tab.pbox, &h->shard_hist,
-                      &h->rec_keys, &h->rec_w, &h->rec_s, &h->rec_r, &h->ppos, &h->rws.agg, &h->rws.spill, &h->rws.scan_tmp,
+                      &h->rec_keys, &h->rec_w, &h->rec_s, &h->rec_r, &h->ppos, &h->ppos4, &h->rws.agg, &h->rws.spill, &h->rws.scan_tmp,
                       &h->dws.part, &h->dws.summ, &h->dws.dstat, &h->dws.rm_bits, &h->tab.stale};
     for (DevBuf* b : bufs) b->release();
     if (h->pend.ev) (void)hipEventDestroy(h->pend.ev);
@@ -177,11 +177,24 @@ int wq_get_stats(wq_router* h, wq_stats* out) {
 
 int wq_debug_route_config_count(void) { return route_config_count(); }
 
+// The radius filter's f32 copy of the positions (round to nearest, as the error bound in
+// within_radius assumes).
+static __global__ void k_pos_f32(const double* __restrict__ pos, uint64_t n, float4* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = make_float4((float)pos[3 * i], (float)pos[3 * i + 1], (float)pos[3 * i + 2], 0.0f);
+}
+
 static int set_peer_positions(wq_router* h, const double* pos, size_t n, hipMemcpyKind kind) {
     if (!h || (n && !pos) || n > 0xFFFFFFFFull) return WQ_E_INVALID;
     WQ_HIP(h, hipSetDevice(h->device));
     WQ_ALLOC(h, h->ppos, (n ? n : 1) * 24);
+    WQ_ALLOC(h, h->ppos4, (n ? n : 1) * 16);
     if (n) WQ_HIP(h, hipMemcpyAsync(h->ppos.p, pos, n * 24, kind, h->stream));
+    if (n) {
+        hipLaunchKernelGGL(k_pos_f32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, h->ppos.as<double>(),
+                           (uint64_t)n, h->ppos4.as<float4>());
+        WQ_HIP(h, hipGetLastError());
+    }
     if (kind == hipMemcpyHostToDevice) WQ_HIP(h, hipStreamSynchronize(h->stream));
     h->n_ppos = n;
     return WQ_OK;
