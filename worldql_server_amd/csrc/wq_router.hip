@@ -178,10 +178,18 @@ int wq_get_stats(wq_router* h, wq_stats* out) {
 int wq_debug_route_config_count(void) { return route_config_count(); }
 
 // The radius filter's f32 copy of the positions (round to nearest, as the error bound in
-// within_radius assumes).
-static __global__ void k_pos_f32(const double* __restrict__ pos, uint64_t n, float4* __restrict__ out) {
+// within_radius assumes); with copy64, the f64 rows too (device-to-device: one pass over the input).
+static __global__ void k_pos_f32(const double* __restrict__ pos, uint64_t n, float4* __restrict__ out,
+                                 double* __restrict__ copy64) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = make_float4((float)pos[3 * i], (float)pos[3 * i + 1], (float)pos[3 * i + 2], 0.0f);
+    if (i >= n) return;
+    const double x = pos[3 * i], y = pos[3 * i + 1], z = pos[3 * i + 2];
+    out[i] = make_float4((float)x, (float)y, (float)z, 0.0f);
+    if (copy64) {
+        copy64[3 * i] = x;
+        copy64[3 * i + 1] = y;
+        copy64[3 * i + 2] = z;
+    }
 }
 
 static int set_peer_positions(wq_router* h, const double* pos, size_t n, hipMemcpyKind kind) {
@@ -189,10 +197,12 @@ static int set_peer_positions(wq_router* h, const double* pos, size_t n, hipMemc
     WQ_HIP(h, hipSetDevice(h->device));
     WQ_ALLOC(h, h->ppos, (n ? n : 1) * 24);
     WQ_ALLOC(h, h->ppos4, (n ? n : 1) * 16);
-    if (n) WQ_HIP(h, hipMemcpyAsync(h->ppos.p, pos, n * 24, kind, h->stream));
+    const bool d2d = kind == hipMemcpyDeviceToDevice;
+    if (n && !d2d) WQ_HIP(h, hipMemcpyAsync(h->ppos.p, pos, n * 24, kind, h->stream));
     if (n) {
-        hipLaunchKernelGGL(k_pos_f32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, h->ppos.as<double>(),
-                           (uint64_t)n, h->ppos4.as<float4>());
+        hipLaunchKernelGGL(k_pos_f32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream,
+                           d2d ? pos : h->ppos.as<double>(), (uint64_t)n, h->ppos4.as<float4>(),
+                           d2d ? h->ppos.as<double>() : nullptr);
         WQ_HIP(h, hipGetLastError());
     }
     if (kind == hipMemcpyHostToDevice) WQ_HIP(h, hipStreamSynchronize(h->stream));
