@@ -163,7 +163,7 @@ def run_c3(a, rank, world_size, local_rank, dev):
     t0 = time.perf_counter()
     w = synth_ext.config_c3(scale=a.scale)
     gen_s = time.perf_counter() - t0
-    if world_size > 1:
+    if world_size > 1 or a.shard == "cube":  # (--shard cube at N = 1: the same sharded tick over one RCCL rank)
         return _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s)
     M = len(w.world)
     r = Router(w.cube_size, local_rank)
@@ -228,7 +228,8 @@ def attach_rccl(r, rank: int, world_size: int) -> None:
     import torch.distributed as dist
     from worldql_server_amd.router import rccl_unique_id
     uid = [rccl_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(uid, src=0)
+    if world_size > 1:
+        dist.broadcast_object_list(uid, src=0)
     r.attach_rccl(world_size, rank, uid[0])
 
 
@@ -286,6 +287,24 @@ def _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s):
                          "whole sharded tick per GPU (shard + exchanges + owner route + unshard); bytes = the "
                          "tick's SURVEY §8(d) bytes / N"),
                 "synthetic (splitmix64, SURVEY.md §8(d) C3 generator)")
+    if not a.no_extra:
+        # SURVEY.md §8(e) step 5's other option: the same collective tick with the pairs left on the
+        # owner that routed them (wq_sharded_route_owner_device) — no return exchange
+        own = {"P": 0}
+
+        def tick_owner():
+            v = r.sharded_route_owner_device(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M)
+            own["P"] = int(v.n_pairs)
+        for _ in range(max(a.warmup, 1)):
+            tick_owner()
+        t_ms = timed_ticks(tick_owner, a.steps, stream, dev, world_size, [r])
+        t_max_ms, pairs_own = reduce_over_ranks(t_ms, own["P"], dev, world_size)
+        assert pairs_own == pairs_all, (pairs_own, pairs_all)  # every pair routed exactly once
+        out["extra"] = {"pairs_on_owner": {
+            "value": pairs_own * a.steps / (t_max_ms / 1e3), "unit": "pairs/s", "ms_per_step": t_max_ms / a.steps,
+            "n_gpus": world_size, "steps": a.steps, "warmup": a.warmup, "scaling": "strong",
+            "note": "same tick, pairs left on the owning GPU (no return all-to-all): "
+                    "shard -> RCCL all-to-all of the records -> route on the owners"}}
     r.close()
     return out
 

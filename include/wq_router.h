@@ -284,6 +284,26 @@ int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_
                                  size_t capacity, size_t* n_pairs);
 int wq_sharded_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity);
 
+/* The owner-side form of the sharded tick ("pairs stay on the owner"):
+ * the same collective shard -> exchange -> route, but the (message, peer) pairs are not sent back.
+ * On return, *out describes what THIS shard routed — the R messages it owns, as the records it
+ * received (recs[i].msg = the message's index in its ingesting shard's batch; records from source
+ * shard s are recs[seg[s] .. seg[s+1])) with their recipients as a CSR (offsets[R + 1], peers[P]),
+ * each message's peers ascending. Device pointers into the handle's workspace, valid until the
+ * next sharded call on it. A transport that sends from the owner (or re-partitions by peer) needs
+ * no return exchange: across the shards every message appears exactly once. */
+typedef struct wq_owner_view {
+    const wq_msg_rec* recs;
+    const uint32_t* offsets;
+    const uint32_t* peers;
+    uint64_t n_recs;
+    uint64_t n_pairs;
+    uint32_t seg[WQ_MAX_SHARDS + 1];
+} wq_owner_view;
+int wq_sharded_route_owner_device(wq_router* h, const double* d_pos, const int64_t* d_keys,
+                                  const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
+                                  size_t n_msgs, wq_owner_view* out);
+
 /* ---- F2: per-peer send lists (PeerMap::broadcast_to, worldql_server/src/transport/peer_map.rs:151-163)
  * The transpose of a tick's message-major CSR for a transport that batches per peer: for every
  * peer p < n_peers whose bit is set in d_connected (bit p % 32 of word p / 32; NULL = every peer

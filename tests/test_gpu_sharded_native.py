@@ -127,6 +127,75 @@ def test_hub_sharded_ticks_vs_whole_table_oracle(G):
     hub.close()
 
 
+@pytest.mark.parametrize("G", [1, 2, 3])
+def test_hub_owner_form_vs_whole_table_oracle(G):
+    """wq_sharded_route_owner_device: the pairs stay on their owner; across the shards every message of
+    every ingesting slice appears exactly once, with the oracle's recipients."""
+    import torch
+    from worldql_server_amd.router import Hub, Router
+    w, churn = _workload(seed=13)
+    M = len(w.world)
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    results, errors = [None] * G, []
+
+    def body(rank):
+        try:
+            r = routers[rank]
+            r.attach_hub(hub, rank)
+            lo, hi = _slice(M, G, rank)
+            r.sharded_apply_ops(w.ops)
+            r.sharded_apply_ops(churn)
+            n = hi - lo
+            pos = torch.from_numpy(np.ascontiguousarray(w.pos[lo:hi])).to(dev)
+            wo = torch.from_numpy(np.ascontiguousarray(w.world[lo:hi]).view(np.int32)).to(dev)
+            se = torch.from_numpy(np.ascontiguousarray(w.sender[lo:hi]).view(np.int32)).to(dev)
+            rp = torch.from_numpy(np.ascontiguousarray(w.repl[lo:hi])).to(dev)
+            torch.cuda.synchronize(dev)
+            v = r.sharded_route_owner_device(pos.data_ptr(), wo.data_ptr(), se.data_ptr(), rp.data_ptr(), n)
+            R, P = int(v.n_recs), int(v.n_pairs)
+            hip = ctypes.CDLL("libamdhip64.so.7")
+            hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+            recs = np.empty(max(R, 1), abi.MSG_REC_DTYPE)
+            offs = np.empty(R + 1, np.uint32)
+            peers = np.empty(max(P, 1), np.uint32)
+            torch.cuda.synchronize(dev)
+            if R:
+                assert hip.hipMemcpy(recs.ctypes.data, v.recs, R * 40, 2) == 0
+                assert hip.hipMemcpy(peers.ctypes.data, v.peers, P * 4, 2) == 0 or P == 0
+            assert hip.hipMemcpy(offs.ctypes.data, v.offsets, (R + 1) * 4, 2) == 0
+            results[rank] = (recs[:R], offs, peers[:P], list(v.seg[:G + 1]))
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=body, args=(k,)) for k in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    assert not errors, errors
+    got = {}
+    for rank in range(G):
+        recs, offs, peers, seg = results[rank]
+        assert offs[0] == 0 and offs[-1] == len(peers) and seg[-1] == len(recs)
+        for src in range(G):
+            for i in range(seg[src], seg[src + 1]):
+                key = (src, int(recs[i]["msg"]))
+                assert key not in got  # each message is routed by exactly one owner
+                got[key] = peers[offs[i]:offs[i + 1]]
+    for src in range(G):
+        lo, hi = _slice(M, G, src)
+        w_offs, w_peers = _expected([w.ops, churn], w, lo, hi)
+        for m in range(hi - lo):
+            want = w_peers[w_offs[m]:w_offs[m + 1]]
+            assert (got.pop((src, m)) == want).all(), (src, m)
+    assert not got
+    for r in routers:
+        r.close()
+    hub.close()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -4,6 +4,8 @@ Pure data: importing this module loads no native code.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 
 WQ_OK = 0
@@ -78,6 +80,12 @@ def concat_ops(parts) -> np.ndarray:
 MAX_SHARDS = 64
 RCCL_ID_BYTES = 128  # WQ_RCCL_ID_BYTES
 SHARD_ALL = 0xFFFFFFFF  # owner of a REMOVE_PEER op
+
+# struct wq_owner_view (wq_sharded_route_owner_device): device pointers + counts + source segments
+class OwnerView(ctypes.Structure):
+    _fields_ = [("recs", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("peers", ctypes.c_void_p),
+                ("n_recs", ctypes.c_uint64), ("n_pairs", ctypes.c_uint64), ("seg", ctypes.c_uint32 * (MAX_SHARDS + 1))]
+
 
 # struct wq_msg_rec: 40 bytes on the wire between GPUs
 REC_POS = 1  # wq_msg_rec.flags: key holds the f64 position bits (radius filter on)

@@ -491,35 +491,21 @@ int wq_sharded_apply_ops(wq_router* h, const wq_op* ops, size_t n) {
     return wq_apply_ops(h, mine.data(), mine.size());
 }
 
-int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
-                                 const uint32_t* d_sender, const uint8_t* d_repl, size_t n_msgs, uint32_t* d_offsets,
-                                 uint32_t* d_peers, uint32_t* d_msgs, size_t capacity, size_t* n_pairs) {
-    if (!h || !d_offsets || !n_pairs || (n_msgs && (!d_world || !d_sender || !d_repl || (!d_pos && !d_keys))) ||
-        (capacity && !d_peers))
-        return WQ_E_INVALID;
-    if (n_msgs >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
-    WQ_HIP(h, hipSetDevice(h->device));
-    if (capacity > 0xFFFFFFFFull) capacity = 0xFFFFFFFFull;
+// Steps 1-3 of a sharded tick, shared by the origin and owner forms: shard this rank's messages,
+// exchange the counts (host read 1) and the records, route what this shard owns into
+// own_off / own_peers. *R_out = records received, *seg = their source segments. A local route
+// failure is left in *late_out (the caller keeps the collective going); a return value != WQ_OK is
+// an exchange or argument failure.
+static int shard_exchange_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                                const uint32_t* d_sender, const uint8_t* d_repl, size_t n_msgs, uint64_t* R_out,
+                                SegBounds* seg_out, int* late_out, std::string* late_msg_out) {
     hipStream_t s = h->stream;
-    *n_pairs = 0;
-    if (!h->shard) {  // G = 1 without an exchange: the single-GPU tick, P read back
-        int rc = launch_route(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs, capacity);
-        if (rc) return rc;
-        wq_route_counters c;
-        WQ_HIP(h, hipMemcpyAsync(&c, h->rws.last, sizeof(c), hipMemcpyDeviceToHost, s));
-        WQ_HIP(h, hipStreamSynchronize(s));
-        *n_pairs = n_msgs ? c.n_pairs : 0;
-        if (c.error & 4u) return set_error(h, WQ_E_TIMEOUT, "route look-back spin gave up");
-        if (c.error) return set_error(h, WQ_E_CAPACITY, "more than 2^32-1 pairs in one tick");
-        if (n_msgs && c.n_pairs > capacity) return set_error(h, WQ_E_CAPACITY, "output capacity too small");
-        return WQ_OK;
-    }
     ShardCtx& sc = *h->shard;
-    const uint32_t G = sc.G, me = sc.rank;
+    const uint32_t G = sc.G;
     const size_t M = n_msgs;
     sc.last_ready = false;
-    int late = WQ_OK;  // a local failure, reported once the tick's exchanges are complete
-    std::string late_msg;
+    int& late = *late_out;  // a local failure, reported once the tick's exchanges are complete
+    std::string& late_msg = *late_msg_out;
 
     // 1. shard
     WQ_ALLOC(h, sc.recs, (M ? M : 1) * sizeof(wq_msg_rec));
@@ -530,7 +516,7 @@ int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_
                                    cnt_send);
     if (rc) return rc;  // nothing exchanged yet: every rank's failure here is local and symmetric-safe
     // 2. counts, then the records
-    std::vector<size_t> four(G, 4), eight(G, 8);
+    std::vector<size_t> four(G, 4);
     {
         Xfer x{{cnt_send}, {four.data()}, {cnt_recv}, {four.data()}, 1};
         if ((rc = exchange(h, x))) return rc;
@@ -570,6 +556,44 @@ int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_
         late_msg = h->err;
         WQ_HIP(h, hipMemsetAsync(sc.own_off.p, 0, (R + 1) * 4, s));
     }
+    *R_out = R;
+    *seg_out = seg;
+    return WQ_OK;
+}
+
+int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                                 const uint32_t* d_sender, const uint8_t* d_repl, size_t n_msgs, uint32_t* d_offsets,
+                                 uint32_t* d_peers, uint32_t* d_msgs, size_t capacity, size_t* n_pairs) {
+    if (!h || !d_offsets || !n_pairs || (n_msgs && (!d_world || !d_sender || !d_repl || (!d_pos && !d_keys))) ||
+        (capacity && !d_peers))
+        return WQ_E_INVALID;
+    if (n_msgs >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
+    WQ_HIP(h, hipSetDevice(h->device));
+    if (capacity > 0xFFFFFFFFull) capacity = 0xFFFFFFFFull;
+    hipStream_t s = h->stream;
+    *n_pairs = 0;
+    if (!h->shard) {  // G = 1 without an exchange: the single-GPU tick, P read back
+        int rc = launch_route(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs, capacity);
+        if (rc) return rc;
+        wq_route_counters c;
+        WQ_HIP(h, hipMemcpyAsync(&c, h->rws.last, sizeof(c), hipMemcpyDeviceToHost, s));
+        WQ_HIP(h, hipStreamSynchronize(s));
+        *n_pairs = n_msgs ? c.n_pairs : 0;
+        if (c.error & 4u) return set_error(h, WQ_E_TIMEOUT, "route look-back spin gave up");
+        if (c.error) return set_error(h, WQ_E_CAPACITY, "more than 2^32-1 pairs in one tick");
+        if (n_msgs && c.n_pairs > capacity) return set_error(h, WQ_E_CAPACITY, "output capacity too small");
+        return WQ_OK;
+    }
+    ShardCtx& sc = *h->shard;
+    const uint32_t G = sc.G, me = sc.rank;
+    const size_t M = n_msgs;
+    int late = WQ_OK;  // a local failure, reported once the tick's exchanges are complete
+    std::string late_msg;
+    uint64_t R = 0;
+    SegBounds seg;
+    int rc = shard_exchange_route(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, &R, &seg, &late, &late_msg);
+    if (rc) return rc;
+    std::vector<size_t> eight(G, 8);
     // 4. per-record counts, per-source pair counts, exchanged
     WQ_ALLOC(h, sc.own_e, (R ? R : 1) * 4);
     WQ_ALLOC(h, sc.pc, 2 * G * 8 + sizeof(wq_route_counters));
@@ -637,6 +661,50 @@ int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_
     sc.last_P = P;
     sc.last_ready = true;
     return copy_out(h, d_offsets, d_peers, d_msgs, capacity);
+}
+
+int wq_sharded_route_owner_device(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                                  const uint32_t* d_sender, const uint8_t* d_repl, size_t n_msgs, wq_owner_view* out) {
+    if (!h || !out || (n_msgs && (!d_world || !d_sender || !d_repl || (!d_pos && !d_keys)))) return WQ_E_INVALID;
+    if (n_msgs >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
+    WQ_HIP(h, hipSetDevice(h->device));
+    if (!h->shard) return set_error(h, WQ_E_INVALID, "no exchange attached (wq_shard_attach_*)");
+    memset(out, 0, sizeof(*out));
+    hipStream_t s = h->stream;
+    ShardCtx& sc = *h->shard;
+    int late = WQ_OK;
+    std::string late_msg;
+    uint64_t R = 0;
+    SegBounds seg;
+    int rc = shard_exchange_route(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, &R, &seg, &late, &late_msg);
+    if (rc) return rc;
+    if (late) {  // nothing else is exchanged in this form: report it now
+        h->err = late_msg;
+        return late;
+    }
+    // the pairs stay here (first option): only this shard's counters are read
+    wq_route_counters c{};
+    if (R) {
+        WQ_HIP(h, hipMemcpyAsync(&c, h->rws.last, sizeof(c), hipMemcpyDeviceToHost, s));
+        WQ_HIP(h, hipStreamSynchronize(s));
+        if (c.error & 4u) return set_error(h, WQ_E_TIMEOUT, "owner route: look-back spin gave up");
+        if (c.error) return set_error(h, WQ_E_CAPACITY, "owner route: more than 2^32-1 pairs");
+        if (c.n_pairs > sc.own_cap) {  // the pair buffer was short: offsets are right, route again
+            sc.own_cap = c.n_pairs + c.n_pairs / 4 + 4096;
+            if (sc.own_cap > 0xFFFFFFFFull) sc.own_cap = 0xFFFFFFFFull;
+            WQ_ALLOC(h, sc.own_peers, sc.own_cap * 4);
+            if ((rc = launch_route_records(h, sc.recv.as<wq_msg_rec>(), R, sc.own_off.as<uint32_t>(),
+                                           sc.own_peers.as<uint32_t>(), nullptr, sc.own_cap)))
+                return rc;
+        }
+    }
+    out->recs = sc.recv.as<wq_msg_rec>();
+    out->offsets = sc.own_off.as<uint32_t>();
+    out->peers = sc.own_peers.as<uint32_t>();
+    out->n_recs = R;
+    out->n_pairs = R ? c.n_pairs : 0;
+    for (uint32_t d = 0; d <= sc.G; ++d) out->seg[d] = seg.b[d];
+    return WQ_OK;
 }
 
 int wq_sharded_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity) {

@@ -98,6 +98,7 @@ def load_library(build_if_missing: bool = True):
         "wq_sharded_apply_ops": ([vp, vp, sz], i32),
         "wq_sharded_route_tick_device": ([vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, ctypes.POINTER(sz)], i32),
         "wq_sharded_copy_out": ([vp, vp, vp, vp, sz], i32),
+        "wq_sharded_route_owner_device": ([vp, vp, vp, vp, vp, vp, sz, ctypes.POINTER(abi.OwnerView)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -344,6 +345,15 @@ class Router:
         if rc not in (0, abi.WQ_E_CAPACITY):
             self._check(rc)
         return rc, n.value
+
+    def sharded_route_owner_device(self, pos_ptr, world_ptr, sender_ptr, repl_ptr, n_msgs, keys_ptr=None):
+        """The owner-side form of the collective sharded tick: the pairs stay on the shard that routed
+        them. Returns an abi.OwnerView of device pointers valid until the next sharded call."""
+        v = abi.OwnerView()
+        self._check(self.lib.wq_sharded_route_owner_device(self.h, pos_ptr or None, keys_ptr or None, world_ptr or None,
+                                                           sender_ptr or None, repl_ptr or None, n_msgs,
+                                                           ctypes.byref(v)))
+        return v
 
     def sharded_copy_out(self, offsets_ptr, peers_ptr, msgs_ptr, capacity) -> None:
         self._check(self.lib.wq_sharded_copy_out(self.h, offsets_ptr, peers_ptr or None, msgs_ptr or None, capacity))
