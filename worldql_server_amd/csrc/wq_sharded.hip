@@ -295,37 +295,98 @@ __global__ void k_counts_by_msg(const wq_msg_rec* __restrict__ recs, const uint3
 __global__ void k_set_last(uint32_t* __restrict__ a, uint32_t at, uint32_t v) { a[at] = v; }
 
 // Block b moves the runs of records [256b, 256b + 256) — record i's e[i] peers at ret_off[i] in
-// record order — to offsets[msg_i] in message order (one output per thread per pass; the record of
-// output r by a binary search over the block's run starts in LDS, as emit_direct does).
+// record order — to offsets[msg_i] in message order. Windows of W = R * 256 of the block's outputs:
+// each record marks where its run enters the window in a u16 owner map (index + 1), a block-wide
+// max-scan carries each owner over its outputs, and thread t moves outputs t, t + 256, ... of the
+// window (contiguous reads; each run written contiguously at its message's offset). C3 on one
+// shard: 1,059 us (about 5 GB moved: 4.7 TB/s), 1,088 us with an 8-step binary search over the
+// run starts per output instead — the move is bandwidth-bound either way.
+template <int R>
 __global__ __launch_bounds__(kBlock) void k_unshard(const wq_msg_rec* __restrict__ recs, const uint32_t* __restrict__ ret_off,
                                                     const uint32_t* __restrict__ peers_in, uint32_t M, uint32_t P,
                                                     const uint32_t* __restrict__ offsets, uint32_t* __restrict__ peers,
                                                     uint32_t* __restrict__ msgs) {
+    static_assert(R % 8 == 0, "map rows of whole 16-byte words");
+    constexpr uint32_t W = R * kBlock;
+    __shared__ alignas(16) uint16_t map[W];
     __shared__ uint32_t st[kBlock], dst[kBlock], msg[kBlock];
-    const uint32_t i0 = blockIdx.x * kBlock, i = i0 + threadIdx.x;
+    __shared__ uint32_t wave_max[kWaves];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t i0 = blockIdx.x * kBlock, i = i0 + tid;
     const uint32_t base = ret_off[i0];
     const uint32_t end = i0 + kBlock < M ? ret_off[i0 + kBlock] : P;
+    const uint32_t T = end - base;
+    uint32_t my_st = 0, my_e = 0;
     if (i < M) {
         const uint32_t m = recs[i].msg;
-        st[threadIdx.x] = ret_off[i] - base;
-        dst[threadIdx.x] = offsets[m];
-        msg[threadIdx.x] = m;
-    } else {
-        st[threadIdx.x] = 0xFFFFFFFFu;  // past every output: the search never lands here
+        const uint32_t a = ret_off[i];
+        my_st = a - base;
+        my_e = (i + 1 < M ? ret_off[i + 1] : P) - a;
+        st[tid] = my_st;
+        dst[tid] = offsets[m];
+        msg[tid] = m;
     }
-    __syncthreads();
-    const uint32_t T = end - base;
-    for (uint32_t r = threadIdx.x; r < T; r += kBlock) {
-        uint32_t lo = 0, n = kBlock;  // last j with st[j] <= r
+    uint4* my_map = reinterpret_cast<uint4*>(map) + tid * (R / 8);
+    for (uint32_t w0 = 0; w0 < T; w0 += W) {
 #pragma unroll
-        for (int it = 0; it < 8; ++it) {
-            const uint32_t half = n >> 1;
-            if (st[lo + half] <= r) lo += half;
-            n -= half;
+        for (int q = 0; q < R / 8; ++q) my_map[q] = make_uint4(0, 0, 0, 0);
+        lds_barrier();
+        if (my_e && my_st + my_e > w0 && my_st < w0 + W) map[(my_st > w0 ? my_st : w0) - w0] = (uint16_t)(tid + 1);
+        lds_barrier();
+        uint4 v[R / 8];
+#pragma unroll
+        for (int q = 0; q < R / 8; ++q) v[q] = my_map[q];
+        uint32_t run = 0;
+#pragma unroll
+        for (int q = 0; q < R / 8; ++q) {
+            uint32_t* w = reinterpret_cast<uint32_t*>(&v[q]);
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                uint32_t lo = w[h] & 0xFFFFu, hi = w[h] >> 16;
+                run = lo > run ? lo : run;
+                lo = run;
+                run = hi > run ? hi : run;
+                w[h] = lo | (run << 16);
+            }
         }
-        const uint32_t o = dst[lo] + (r - st[lo]);
-        peers[o] = peers_in[base + r];
-        if (msgs) msgs[o] = msg[lo];
+        const uint32_t incl = wave_incl_scan_max(run, lane);
+        uint32_t pre = __shfl_up(incl, 1, 64);
+        if (lane == 0) pre = 0;
+        if (lane == 63) wave_max[wave] = incl;
+        lds_barrier();
+#pragma unroll
+        for (int u = 0; u < kWaves; ++u)
+            if (u < wave) pre = wave_max[u] > pre ? wave_max[u] : pre;
+#pragma unroll
+        for (int q = 0; q < R / 8; ++q) {
+            uint32_t* w = reinterpret_cast<uint32_t*>(&v[q]);
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const uint32_t lo = w[h] & 0xFFFFu, hi = w[h] >> 16;
+                w[h] = (lo > pre ? lo : pre) | ((hi > pre ? hi : pre) << 16);
+            }
+            my_map[q] = v[q];
+        }
+        lds_barrier();
+        const uint32_t last = (T - 1 - w0) < W - 1 ? (T - 1 - w0) : W - 1;
+        uint32_t pv[R], oo[R], own[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            const uint32_t x = (uint32_t)(u * kBlock + tid) < last ? (uint32_t)(u * kBlock + tid) : last;
+            const uint32_t j = (uint32_t)map[x] - 1u;
+            const uint32_t r = w0 + x;
+            pv[u] = peers_in[base + r];
+            oo[u] = dst[j] + (r - st[j]);
+            own[u] = j;
+        }
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            if (w0 + u * kBlock + tid < T) {
+                peers[oo[u]] = pv[u];
+                if (msgs) msgs[oo[u]] = msg[own[u]];
+            }
+        }
+        lds_barrier();  // the next window rewrites the map
     }
 }
 
@@ -367,7 +428,7 @@ int copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_m
     if (P > capacity) return set_error(h, WQ_E_CAPACITY, "sharded tick: output capacity too small (required size in *n_pairs)");
     if (M && P) {
         const unsigned g = (unsigned)((M + kBlock - 1) / kBlock);
-        hipLaunchKernelGGL(k_unshard, dim3(g), dim3(kBlock), 0, s, sc.recs.as<wq_msg_rec>(), sc.ret_off.as<uint32_t>(),
+        hipLaunchKernelGGL(k_unshard<16>, dim3(g), dim3(kBlock), 0, s, sc.recs.as<wq_msg_rec>(), sc.ret_off.as<uint32_t>(),
                            sc.ret_peers.as<uint32_t>(), (uint32_t)M, (uint32_t)P, d_offsets, d_peers, d_msgs);
         WQ_HIP(h, hipGetLastError());
     }
