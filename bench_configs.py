@@ -306,6 +306,30 @@ def _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s):
             "note": "same tick, pairs left on the owning GPU (no return all-to-all): "
                     "shard -> RCCL all-to-all of the records -> route on the owners"}}
     r.close()
+    if not a.no_extra:
+        # the alternative 288 GB of HBM allows: every GPU holds the WHOLE table (C3: ~10 GB; every op
+        # is applied on every GPU) and routes its own slice with the single-GPU tick — no exchange
+        rr = Router(w.cube_size, local_rank)
+        rr.set_stream(stream.cuda_stream)
+        rr.apply_ops(w.ops)
+        rr.set_fanout_hint(40.0)
+        cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+
+        def tick_replica():
+            rr.route_device(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
+                            peers.data_ptr(), msgs.data_ptr(), cap, cnt.data_ptr())
+        for _ in range(max(a.warmup, 1)):
+            tick_replica()
+        t_ms = timed_ticks(tick_replica, a.steps, stream, dev, world_size, [rr])
+        P_rep = int(_counters(cnt).reshape(-1)[0]["n_pairs"])
+        t_max_ms, pairs_rep = reduce_over_ranks(t_ms, P_rep, dev, world_size)
+        assert pairs_rep == pairs_all, (pairs_rep, pairs_all)
+        out["extra"]["replicated_table"] = {
+            "value": pairs_rep * a.steps / (t_max_ms / 1e3), "unit": "pairs/s", "ms_per_step": t_max_ms / a.steps,
+            "n_gpus": world_size, "steps": a.steps, "warmup": a.warmup, "scaling": "strong",
+            "note": "every GPU holds the whole table (all ops applied everywhere) and routes its own M/N "
+                    "messages with the single-GPU tick: no exchange"}
+        rr.close()
     return out
 
 
