@@ -269,9 +269,8 @@ __device__ __forceinline__ bool box_may_hold(const TableView& t, uint32_t peer, 
 // e = |pf| 2^-23 + 2^-120 + |ax| 2^-50 of ax = fl(mx - pf), its square within e (2|ax| + e) of ax^2,
 // and its three roundings add at most 2^-50 (d2 + E1). Only when the exact d2 could lie on either
 // side of r^2 (or a value is NaN / beyond f32) are the f64 coordinates read.
-__device__ __forceinline__ bool within_radius(const TableView& t, double mx, double my, double mz, uint32_t p) {
-    if (p >= t.n_ppos) return false;
-    const float4 f = t.ppos4[p];
+// The f32 test alone: 1 = certainly within, 0 = certainly not, -1 = read the f64 coordinates.
+__device__ __forceinline__ int radius_f32_test(const float4 f, double mx, double my, double mz, double r2) {
     const double ax = mx - (double)f.x, ay = my - (double)f.y, az = mz - (double)f.z;
     const double d2f = ax * ax + ay * ay + az * az;
     const double ex = fabs((double)f.x) * 0x1p-23 + 0x1p-120 + fabs(ax) * 0x1p-50;
@@ -279,14 +278,25 @@ __device__ __forceinline__ bool within_radius(const TableView& t, double mx, dou
     const double ez = fabs((double)f.z) * 0x1p-23 + 0x1p-120 + fabs(az) * 0x1p-50;
     const double E1 = ex * (2.0 * fabs(ax) + ex) + ey * (2.0 * fabs(ay) + ey) + ez * (2.0 * fabs(az) + ez);
     const double E = E1 * 1.001 + d2f * 0x1p-40 + 0x1p-1000;
-    if (d2f + E <= t.r2) return true;   // NaN: false
-    if (d2f - E > t.r2) return false;   // NaN: false
+    if (d2f + E <= r2) return 1;   // NaN: false
+    if (d2f - E > r2) return 0;    // NaN: false
+    return -1;
+}
+
+// The reference's f64 predicate itself (peer p has a position).
+__device__ __forceinline__ bool radius_f64(const TableView& t, double mx, double my, double mz, uint32_t p) {
     const double* q = t.ppos + 3ull * p;
     const double dx = mx - q[0];
     const double dy = my - q[1];
     const double dz = mz - q[2];
     const double d2 = dx * dx + dy * dy + dz * dz;
     return d2 <= t.r2;
+}
+
+__device__ __forceinline__ bool within_radius(const TableView& t, double mx, double my, double mz, uint32_t p) {
+    if (p >= t.n_ppos) return false;
+    const int d = radius_f32_test(t.ppos4[p], mx, my, mz, t.r2);
+    return d >= 0 ? d > 0 : radius_f64(t, mx, my, mz, p);
 }
 
 // Header (chunks 0-1) of the record probe sequence for (pk, ext): walks while the slot holds
