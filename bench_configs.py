@@ -21,6 +21,7 @@ the timed region; a tick's timed work is everything the tick does on the GPU.
 from __future__ import annotations
 
 import json
+import os
 import time
 
 import numpy as np
@@ -54,6 +55,16 @@ def _pmc_traffic(name: str, M: int, P: int):
     if d.get("messages_per_tick") != M or d.get("pairs_per_tick") != P:
         return None
     return d["hbm_bytes_per_launch"]
+
+
+def _pmc_tick_traffic(name: str, scale: float):
+    """HBM bytes per whole C4 / C5 tick from a committed tools/pmc_churn.sh summary (the bench's own
+    deterministic workload, averaged over its 12 profiled ticks), or None (other scales)."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", name)
+    if scale != 1.0 or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)["hbm_bytes_per_tick"]
 
 
 def _counters(cnt):
@@ -444,7 +455,8 @@ def run_c4(a, rank, world_size, local_rank, dev):
                  "parallelism": f"world-sharded x{world_size}", "table_build_s": round(build_s, 3),
                  "generate_s": round(gen_s, 1)},
                 {"bound": "hbm", "achieved": B / (t_max_ms / steps / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
-                 "unit": "GB/s", "frac": B / (t_max_ms / steps / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                 "unit": "GB/s", "frac": B / (t_max_ms / steps / 1e3) / 1e9 / HBM_PEAK_GBS,
+                 "traffic": _pmc_tick_traffic("r02_pmc_c4.json", a.scale) if world_size == 1 else None,
                  "kernel": "whole tick (incremental update + route); route launch alone below",
                  "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
                 "synthetic (splitmix64, SURVEY.md §8(d) C4 generator)")
@@ -537,7 +549,8 @@ def run_c5(a, rank, world_size, local_rank, dev):
                  "incremental_updates": res["incremental"], "rebuild_fallbacks": res["fallbacks"],
                  "parallelism": "1 GPU", "table_build_s": round(build_s, 3), "generate_s": round(gen_s, 1)},
                 {"bound": "hbm", "achieved": B / (res["t_ms"] / steps / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
-                 "unit": "GB/s", "frac": B / (res["t_ms"] / steps / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                 "unit": "GB/s", "frac": B / (res["t_ms"] / steps / 1e3) / 1e9 / HBM_PEAK_GBS,
+                 "traffic": _pmc_tick_traffic("r02_pmc_c5.json", a.scale),
                  "kernel": "whole tick (incremental update + positions + radius route); route launches alone below",
                  "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
                 "synthetic (splitmix64, SURVEY.md §8(d) C5 generator)")
