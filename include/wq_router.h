@@ -152,7 +152,10 @@ int wq_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_key
  * evaluated left to right in f64 without FMA contraction, m = the message position, p = the
  * peer's position from the latest wq_set_peer_positions; a peer id >= n_peers has no position and
  * is dropped. Ticks with the filter on take message positions (keys must be NULL).
- * radius <= 0 or NaN turns the filter off. */
+ * radius <= 0 or NaN turns the filter off. The handle keeps the positions (24 B per peer) and an
+ * f32 copy (16 B per peer) that decides every pair whose f64 result it can bound; the rest read
+ * the f64 copy, so results are exactly the f64 predicate's. The _device form reads d_pos on the
+ * handle's stream (asynchronous). */
 int wq_set_peer_positions(wq_router* h, const double* pos, size_t n_peers);
 int wq_set_peer_positions_device(wq_router* h, const double* d_pos, size_t n_peers);
 int wq_set_radius(wq_router* h, double radius);
