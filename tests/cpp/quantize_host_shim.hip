@@ -1,6 +1,7 @@
 // Test-only shim: runs the __host__ __device__ quantiser of wq_device.hpp on the CPU so the
 // exact-divisibility rewrite of `abs % size == 0.0` is checked against the
-// oracle's fmod form without a GPU. The GPU instance is checked in tests/test_gpu_quantize.py.
+// oracle's fmod form without a GPU. The GPU instance is checked in tests/test_gpu_routing.py
+// (test_quantize_*).
 #include <stddef.h>
 #include <stdint.h>
 
