@@ -1,6 +1,10 @@
 """The multi-GPU tick behind the C ABI (wq_sharded_route_tick_device, csrc/wq_sharded.hip) against
 the oracle holding the WHOLE table (sharding must not change any result).
 
+Both return forms: "slots" (default — 20-byte slots out, row references plus one pool of cube lists
+per destination back) and "expanded" (40-byte records out, expanded pairs back; the radius
+filter's form, forced here with wq_debug_set_shard_form).
+
 Exchanges exercised:
   hub       G in {1, 2, 3, 5} router handles as threads of this process, all on cuda:0;
   callback  2 processes on cuda:0 whose exchange is a gloo all-to-all (the C path with the
@@ -46,11 +50,13 @@ def _slice(M, G, rank):
     return rank * M // G, (rank + 1) * M // G
 
 
-def _tick(r, w, lo, hi, dev, cap=None):
-    """One sharded tick of messages [lo, hi) on router r; returns (rc, offsets, peers, msgs)."""
+def _tick(r, w, lo, hi, dev, cap=None, keys=None):
+    """One sharded tick of messages [lo, hi) on router r; returns (rc, offsets, peers, msgs).
+    keys (M x 3 int64, optional): raw CubeArea keys instead of the positions."""
     import torch
     M = hi - lo
     pos = torch.from_numpy(np.ascontiguousarray(w.pos[lo:hi])).to(dev)
+    kt = None if keys is None else torch.from_numpy(np.ascontiguousarray(keys[lo:hi])).to(dev)
     wo = torch.from_numpy(np.ascontiguousarray(w.world[lo:hi]).view(np.int32)).to(dev)
     se = torch.from_numpy(np.ascontiguousarray(w.sender[lo:hi]).view(np.int32)).to(dev)
     rp = torch.from_numpy(np.ascontiguousarray(w.repl[lo:hi])).to(dev)
@@ -59,8 +65,9 @@ def _tick(r, w, lo, hi, dev, cap=None):
     peers = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
     msgs = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
-    rc, P = r.sharded_route_device(pos.data_ptr(), wo.data_ptr(), se.data_ptr(), rp.data_ptr(), M, offs.data_ptr(),
-                                   peers.data_ptr(), msgs.data_ptr(), cap)
+    rc, P = r.sharded_route_device(None if kt is not None else pos.data_ptr(), wo.data_ptr(), se.data_ptr(),
+                                   rp.data_ptr(), M, offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap,
+                                   keys_ptr=None if kt is None else kt.data_ptr())
     if rc == abi.WQ_E_CAPACITY:
         peers = torch.empty(P, dtype=torch.int32, device=dev)
         msgs = torch.empty(P, dtype=torch.int32, device=dev)
@@ -78,8 +85,9 @@ def _check(got, want, M):
     assert (msgs == np.repeat(np.arange(M, dtype=np.uint32), np.diff(offs.astype(np.int64)))).all()
 
 
-@pytest.mark.parametrize("G", [1, 2, 3, 5])
-def test_hub_sharded_ticks_vs_whole_table_oracle(G):
+@pytest.mark.parametrize("G,form", [(1, "slots"), (2, "slots"), (3, "slots"), (5, "slots"), (2, "expanded"),
+                                    (3, "expanded")])
+def test_hub_sharded_ticks_vs_whole_table_oracle(G, form):
     import torch
     from worldql_server_amd.router import Hub, Router
     w, churn = _workload()
@@ -93,6 +101,7 @@ def test_hub_sharded_ticks_vs_whole_table_oracle(G):
         try:
             r = routers[rank]
             r.attach_hub(hub, rank)
+            r.set_shard_form(form == "expanded")
             assert r.shard_info() == (G, rank)
             lo, hi = _slice(M, G, rank)
             r.sharded_apply_ops(w.ops)
@@ -294,3 +303,190 @@ def test_rccl_exchange_two_processes_one_gpu():
     if any(v[0] == "rccl-attach" for v in res.values()):
         pytest.skip(f"RCCL refuses two ranks on one GPU here: {res}")
     assert [res[k][0] for k in range(2)] == ["ok", "ok"], res
+
+
+def _irregular_workload():
+    """Regular traffic plus messages and subscriptions whose cubes have no packed key (the two-slot
+    form on the wire): coordinates beyond +-2^23 cubes, +-inf, a world id >= 2^24 - 1, and raw
+    off-grid CubeArea keys. Returns (workload, keys[M x 3] for the same messages, the key ops)."""
+    base = synth.uniform_box(21, 1500, 6000, 64.0, neighbourhood=True, repl_mode="mixed", n_worlds=2)
+    rng = np.random.default_rng(21)
+    n = 240
+    huge = rng.uniform(-48, 48, (n, 3)) + np.array([3e12, -5e11, 1e10])
+    inf = np.tile(np.array([[np.inf, 1.0, -np.inf]]), (n, 1))
+    normal = rng.uniform(-48, 48, (n, 3))
+    wide_world = 0xFFFFFFF0
+    sub_peers = rng.integers(0, 1500, 3 * n).astype(np.uint32)
+    ops = abi.concat_ops([
+        base.ops,
+        abi.ops_array(np.zeros(n, np.uint32), sub_peers[:n], np.zeros(n, np.uint8), pos=huge),
+        abi.ops_array(np.ones(n, np.uint32), sub_peers[n:2 * n], np.zeros(n, np.uint8), pos=inf),
+        abi.ops_array(np.full(n, wide_world, np.uint32), sub_peers[2 * n:], np.zeros(n, np.uint8), pos=normal),
+    ])
+    m_pos = np.concatenate([base.pos, huge[rng.permutation(n)], inf, normal[rng.permutation(n)]])
+    m_world = np.concatenate([base.world, np.zeros(n, np.uint32), np.ones(n, np.uint32),
+                              np.full(n, wide_world, np.uint32)])
+    M = len(m_world)
+    perm = rng.permutation(M)  # irregular messages spread over every slot group
+    w = synth.Workload("irregular", 16, ops, np.ascontiguousarray(m_pos[perm]), m_world[perm],
+                       rng.integers(0, 1500, M).astype(np.uint32), rng.integers(0, 4, M).astype(np.uint8), 1500)
+    keys = orc.quantize_np(w.pos, 16).reshape(-1, 3)
+    # off-grid raw keys (unreachable from any Vector3): subscribed by key, routed by key
+    off = rng.integers(-5, 5, (n, 3)).astype(np.int64) * 16 + 3
+    key_ops = abi.ops_array(np.zeros(n, np.uint32), rng.integers(0, 1500, n), np.zeros(n, np.uint8), key=off)
+    keys[:n] = off
+    return w, keys, key_ops
+
+
+@pytest.mark.parametrize("form", ["slots", "expanded"])
+def test_hub_irregular_keys_vs_whole_table_oracle(form):
+    """Keys without a packed form travel as two slots (head + tail); positions and raw keys both."""
+    import torch
+    from worldql_server_amd.router import Hub, Router
+    w, keys, key_ops = _irregular_workload()
+    M = len(w.world)
+    G = 3
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    results, errors = [None] * G, []
+
+    def body(rank):
+        try:
+            r = routers[rank]
+            r.attach_hub(hub, rank)
+            r.set_shard_form(form == "expanded")
+            lo, hi = _slice(M, G, rank)
+            r.sharded_apply_ops(w.ops)
+            r.sharded_apply_ops(key_ops)
+            results[rank] = (_tick(r, w, lo, hi, dev), _tick(r, w, lo, hi, dev, keys=keys))
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=body, args=(k,)) for k in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    assert not errors, errors
+    o = orc.COracle(16)
+    o.apply_ops(w.ops)
+    o.apply_ops(key_ops)
+    total = 0
+    for rank in range(G):
+        lo, hi = _slice(M, G, rank)
+        by_pos, by_key = results[rank]
+        _check(by_pos, o.route(w.pos[lo:hi], w.world[lo:hi], w.sender[lo:hi], w.repl[lo:hi])[:2], hi - lo)
+        want = o.route(None, w.world[lo:hi], w.sender[lo:hi], w.repl[lo:hi], keys=keys[lo:hi])[:2]
+        _check(by_key, want, hi - lo)
+        total += len(by_key[2])
+    assert total > 0
+    for r in routers:
+        r.close()
+    hub.close()
+
+
+@pytest.mark.parametrize("form,step", [("slots", 1), ("slots", 3), ("expanded", 1), ("expanded", 3)])
+def test_hub_local_failure_keeps_the_collective(form, step):
+    """A shard whose local step fails (test hook) still completes every exchange of the tick: both
+    shards return an error instead of one of them waiting on the other, the hub stays usable, and
+    the next tick is exact again (no early return between exchanges)."""
+    import time
+
+    import torch
+    from worldql_server_amd.router import Hub, Router, WQError
+    w, churn = _workload(seed=17)
+    M = len(w.world)
+    G = 2
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    results, errors = [None] * G, []
+
+    def body(rank):
+        try:
+            r = routers[rank]
+            r.attach_hub(hub, rank)
+            r.set_shard_form(form == "expanded")
+            lo, hi = _slice(M, G, rank)
+            r.sharded_apply_ops(w.ops)
+            if rank == 1:
+                r.inject_shard_failure(step)
+            t0 = time.perf_counter()
+            try:
+                _tick(r, w, lo, hi, dev)
+                first = None
+            except WQError as e:
+                first = e.code
+            dt = time.perf_counter() - t0
+            results[rank] = (first, dt, _tick(r, w, lo, hi, dev))
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=body, args=(k,)) for k in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    assert not errors, errors
+    for rank in range(G):
+        lo, hi = _slice(M, G, rank)
+        first, dt, second = results[rank]
+        assert first == abi.WQ_E_INVALID, (rank, first)  # every shard of the tick reports it
+        assert dt < 60.0                                 # ... without waiting out the hub's timeout
+        _check(second, _expected([w.ops], w, lo, hi), hi - lo)
+    for r in routers:
+        r.close()
+    hub.close()
+
+
+def test_hub_full_c3_two_shards_route_check():
+    """The north_star configuration through the sharded tick: full C3 (1M peers x 27 cubes, 10M
+    hotspot messages, P = 4.17e8) as 2 shards of one process on cuda:0, each ingesting half of the
+    messages; every message's recipients checked against the whole-table oracle (wqo_route_check),
+    and the slot form's traffic between the shards measured (wq_shard_last_bytes)."""
+    import torch
+    from worldql_server_amd import synth_ext
+    from worldql_server_amd.router import Hub, Router
+    w = synth_ext.config_c3()
+    M = len(w.world)
+    G = 2
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    results, errors = [None] * G, []
+
+    def body(rank):
+        try:
+            r = routers[rank]
+            r.attach_hub(hub, rank)
+            r.set_fanout_hint(40.0)
+            lo, hi = _slice(M, G, rank)
+            r.sharded_apply_ops(w.ops)
+            got = _tick(r, w, lo, hi, dev, cap=48 * (hi - lo))
+            results[rank] = (got[0], got[1], got[2], r.shard_last_bytes())
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=body, args=(k,)) for k in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(600)
+    assert not errors, errors
+    for r in routers:
+        r.close()
+    hub.close()
+    o = orc.COracle(16)
+    o.apply_ops(w.ops)
+    P = 0
+    for rank in range(G):
+        lo, hi = _slice(M, G, rank)
+        rc, offs, peers, (sent, recvd) = results[rank]
+        assert rc == 0 and int(offs[-1]) == len(peers)
+        bad, first = o.route_check(w.pos[lo:hi], w.world[lo:hi], w.sender[lo:hi], w.repl[lo:hi], offs, peers)
+        assert bad == 0, f"shard {rank}: {bad} messages differ, first {first}"
+        P += len(peers)
+        # what crossed: far less than the expanded pairs a remote owner would otherwise return
+        assert 0 < sent < 4 * len(peers), (sent, len(peers))
+    assert P > 4e8

@@ -75,6 +75,11 @@ __device__ __forceinline__ void check_stale(const TableView& t, wq_route_counter
     if (t.stale && *t.stale) flag_route(c, health, kErrStale, 0u);
 }
 
+// Compact message slots of the sharded tick (wq_shard.hip shard_scatter20_kernel): five words each,
+// the kind in bits 8-15 of word 4 (its low byte is the replication code).
+constexpr int kSlotWords = 5;
+constexpr uint32_t kSlotReg = 0, kSlotHead = 1, kSlotTail = 2;
+
 struct RouteIn {
     const double* pos;
     const int64_t* keys;
@@ -83,6 +88,7 @@ struct RouteIn {
     const uint8_t* repl;
     uint32_t M;
     int64_t si;
+    const uint32_t* slots = nullptr;  // count_kernel<..., SLOTS = true>: M compact slots instead of the above
 };
 
 }  // namespace wq

@@ -57,28 +57,47 @@ constexpr uint32_t kStDone = 0, kStProbe = 1, kStVerify = 2;
 // m >= in.M), with F (candidates) and E (recipients) accumulated into the caller's sums.
 // FULL: the whole record line is read in the first round (the sender filter then needs no extra
 // round) and its peer chunks 2-7 are handed back in peers_out (FULL only; valid for inline records).
-template <bool RAW_KEYS, int IPT, int DBG = 0, bool FULL = false>
+template <bool RAW_KEYS, int IPT, int DBG = 0, bool FULL = false, bool SLOTS = false>
 __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& tv, uint32_t m0,
                                            uint32_t (&e_out)[IPT], uint2 (&inf_out)[IPT], uint64_t& F_local,
                                            uint32_t& E_local, uint4 (*peers_out)[6] = nullptr) {
     const int tid = threadIdx.x;
 
     // ---- A: inputs (all loads first), quantise (kernel 1), packed key, home slot ----
-    uint32_t in_w[IPT], in_me[IPT];
+    // SLOTS: compact slots of the sharded tick (route_common.hpp) — the key arrives packed (a
+    // regular slot), or as full coordinates in a head + tail pair; a tail slot routes to nobody.
+    uint32_t in_w[IPT], in_me[IPT], in_kind[IPT];
     uint8_t in_rp[IPT];
     uint64_t in_c[IPT][3];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
         const uint32_t m = m0 + i * kBlock + tid;
         const uint32_t mm = m < in.M ? m : 0;
-        in_w[i] = in.world[mm];
-        in_me[i] = in.sender[mm];
-        in_rp[i] = in.repl[mm];
-        const uint64_t* src = RAW_KEYS ? reinterpret_cast<const uint64_t*>(in.keys)
-                                       : reinterpret_cast<const uint64_t*>(in.pos);
-        in_c[i][0] = src[3ull * mm];
-        in_c[i][1] = src[3ull * mm + 1];
-        in_c[i][2] = src[3ull * mm + 2];
+        if (SLOTS) {
+            const uint32_t* r = in.slots + (uint64_t)kSlotWords * mm;
+            const uint32_t r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
+            in_c[i][0] = ((uint64_t)r1 << 32) | r0;  // packed key, or x of a head
+            in_c[i][1] = r2;                         // ext, or the world of a head
+            in_c[i][2] = 0;
+            in_w[i] = r2;
+            in_me[i] = r3;
+            in_rp[i] = (uint8_t)(r4 & 0xFFu);
+            in_kind[i] = (r4 >> 8) & 0xFFu;
+            if (in_kind[i] == kSlotHead && m < in.M) {  // rare: y, z in the tail slot
+                in_c[i][1] = ((uint64_t)r[6] << 32) | r[5];
+                in_c[i][2] = ((uint64_t)r[8] << 32) | r[7];
+            }
+        } else {
+            in_w[i] = in.world[mm];
+            in_me[i] = in.sender[mm];
+            in_rp[i] = in.repl[mm];
+            in_kind[i] = kSlotReg;
+            const uint64_t* src = RAW_KEYS ? reinterpret_cast<const uint64_t*>(in.keys)
+                                           : reinterpret_cast<const uint64_t*>(in.pos);
+            in_c[i][0] = src[3ull * mm];
+            in_c[i][1] = src[3ull * mm + 1];
+            in_c[i][2] = src[3ull * mm + 2];
+        }
     }
     uint64_t pk[IPT];
     uint32_t ext[IPT], sl[IPT], st[IPT];
@@ -86,21 +105,34 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
         const uint32_t m = m0 + i * kBlock + tid;
-        const bool valid = m < in.M;
+        const bool valid = m < in.M && in_kind[i] != kSlotTail;
         const uint32_t w = in_w[i];
-        int64_t x, y, z;
-        if (RAW_KEYS) {
-            x = (int64_t)in_c[i][0];
-            y = (int64_t)in_c[i][1];
-            z = (int64_t)in_c[i][2];
-        } else {
-            x = coord_clamp_dev(__longlong_as_double((long long)in_c[i][0]), tv.sf, in.si);
-            y = coord_clamp_dev(__longlong_as_double((long long)in_c[i][1]), tv.sf, in.si);
-            z = coord_clamp_dev(__longlong_as_double((long long)in_c[i][2]), tv.sf, in.si);
-        }
+        int64_t x = 0, y = 0, z = 0;
         pk[i] = 0;
         ext[i] = 0;
-        const bool reg = pack_key(w, x, y, z, tv.sf, &pk[i], &ext[i]);
+        bool reg;
+        if (SLOTS) {
+            reg = in_kind[i] == kSlotReg;
+            if (reg) {
+                pk[i] = in_c[i][0];
+                ext[i] = (uint32_t)in_c[i][1];
+            } else {
+                x = (int64_t)in_c[i][0];
+                y = (int64_t)in_c[i][1];
+                z = (int64_t)in_c[i][2];
+            }
+        } else {
+            if (RAW_KEYS) {
+                x = (int64_t)in_c[i][0];
+                y = (int64_t)in_c[i][1];
+                z = (int64_t)in_c[i][2];
+            } else {
+                x = coord_clamp_dev(__longlong_as_double((long long)in_c[i][0]), tv.sf, in.si);
+                y = coord_clamp_dev(__longlong_as_double((long long)in_c[i][1]), tv.sf, in.si);
+                z = coord_clamp_dev(__longlong_as_double((long long)in_c[i][2]), tv.sf, in.si);
+            }
+            reg = pack_key(w, x, y, z, tv.sf, &pk[i], &ext[i]);
+        }
         // lanes with nothing to probe read a dummy line spread by message index (never one shared
         // line: a chip-wide hot line serialises on its L2 channel)
         sl[i] = reg ? (uint32_t)slot_of(rec_hash(pk[i], ext[i]) & tv.hash_mask, tv.rec_shift)
@@ -250,7 +282,7 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
     }
 }
 
-template <bool RAW_KEYS, int IPT, int MINW, int DBG = 0, bool FULL = false>
+template <bool RAW_KEYS, int IPT, int MINW, int DBG = 0, bool FULL = false, bool SLOTS = false>
 __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
     __shared__ uint64_t wave_F[kWaves];
     __shared__ uint64_t wave_E[kWaves];
@@ -266,7 +298,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
     uint32_t E_local = 0;
     uint32_t e_out[IPT];
     uint2 inf_out[IPT];
-    count_rows<RAW_KEYS, IPT, DBG, FULL>(p.in, p.t, m0, e_out, inf_out, F_local, E_local);
+    count_rows<RAW_KEYS, IPT, DBG, FULL, SLOTS>(p.in, p.t, m0, e_out, inf_out, F_local, E_local);
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
         const uint32_t m = m0 + i * kBlock + tid;

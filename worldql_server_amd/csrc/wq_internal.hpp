@@ -161,6 +161,8 @@ struct wq_router {
     double radius = 0.0;
     wq::ProfileEvents prof;
     wq::ShardCtx* shard = nullptr;  // wq_shard_attach_*: this handle is one shard of G
+    bool shard_expanded = false;    // wq_debug_set_shard_form: expanded pairs back instead of row references
+    int shard_inject = 0;           // wq_debug_inject_shard_failure: fail the next sharded tick's step 1 or 3
 };
 
 namespace wq {

@@ -48,9 +48,28 @@ __device__ __forceinline__ void msg_key(const ShardIn& in, uint32_t m, int64_t& 
     }
 }
 
-// (1a) per-block owner histogram, stored owner-major: counts[d * nblk + b]. A flat exclusive scan
-// of that array is then directly each (owner, block) pair's first output slot.
-template <bool RAW>
+// Compact records (COMPACT = true; the sharded tick of wq_sharded.hip with the radius filter off):
+// 20-byte slots of five words. A message whose cube has a packed key (pack_key: the regular case)
+// takes one slot
+//   {pk lo, pk hi, ext, sender, repl | kSlotReg << 8}
+// and any other (raw off-grid keys, NaN / huge coordinates, world ids >= 2^24 - 1) takes two:
+//   {x lo, x hi, world, sender, repl | kSlotHead << 8}, {y lo, y hi, z lo, z hi, kSlotTail << 8}.
+// The owner needs no message index (the answers return in slot order), so the ingesting GPU keeps
+// slot -> message in perm[] (kNone for a tail). Half the bytes of a 40-byte wq_msg_rec on xGMI.
+// (the shared definitions — kSlot*, kSlotWords — are in route_common.hpp)
+
+template <bool RAW, bool COMPACT>
+__device__ __forceinline__ uint32_t msg_weight(const ShardIn& in, uint32_t w, int64_t x, int64_t y, int64_t z) {
+    if (!COMPACT) return 1u;
+    uint64_t pk;
+    uint32_t ext;
+    return pack_key(w, x, y, z, in.sf, &pk, &ext) ? 1u : 2u;
+}
+
+// (1a) per-block owner histogram (records, or compact slots), stored owner-major:
+// counts[d * nblk + b]. A flat exclusive scan of that array is then directly each (owner, block)
+// pair's first output slot.
+template <bool RAW, bool COMPACT = false>
 __global__ void __launch_bounds__(kBlock) shard_count_kernel(ShardIn in, uint32_t* __restrict__ counts) {
     __shared__ uint32_t cnt[WQ_MAX_SHARDS];
     for (uint32_t d = threadIdx.x; d < in.G; d += kBlock) cnt[d] = 0;
@@ -62,16 +81,19 @@ __global__ void __launch_bounds__(kBlock) shard_count_kernel(ShardIn in, uint32_
         if (m < in.M) {
             int64_t x, y, z;
             msg_key<RAW>(in, m, x, y, z);
-            atomicAdd(&cnt[shard_of(in.world[m], x, y, z, in.G)], 1u);
+            const uint32_t w = in.world[m];
+            atomicAdd(&cnt[shard_of(w, x, y, z, in.G)], msg_weight<RAW, COMPACT>(in, w, x, y, z));
         }
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < in.G; d += kBlock) counts[(uint64_t)d * in.nblk + blockIdx.x] = cnt[d];
 }
 
-// (1b) one block: exclusive scan of the n = G * nblk histogram entries in place; per-owner totals.
+// (1b) one block: exclusive scan of the n = G * nblk histogram entries in place; per-owner totals
+// at dest_counts[d * stride].
 __global__ void __launch_bounds__(kScanThreads1)
-    shard_scan_kernel(uint32_t* __restrict__ v, uint32_t nblk, uint32_t G, uint32_t* __restrict__ dest_counts) {
+    shard_scan_kernel(uint32_t* __restrict__ v, uint32_t nblk, uint32_t G, uint32_t* __restrict__ dest_counts,
+                      uint32_t stride) {
     __shared__ uint32_t wsum[kScanThreads1 / 64];
     __shared__ uint32_t carry_s;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -102,7 +124,89 @@ __global__ void __launch_bounds__(kScanThreads1)
     for (uint32_t d = threadIdx.x; d < G; d += kScanThreads1) {
         const uint32_t lo = v[(uint64_t)d * nblk];
         const uint32_t hi = d + 1 < G ? v[(uint64_t)(d + 1) * nblk] : total;
-        dest_counts[d] = hi - lo;
+        dest_counts[(uint64_t)d * stride] = hi - lo;
+    }
+}
+
+// (1c') the compact form of (1c): the same stable, ballot-ranked scatter, where a message weighs
+// its slot count (1 regular, 2 head + tail) in the ranks; writes the slots and perm[slot].
+template <bool RAW>
+__global__ void __launch_bounds__(kBlock)
+    shard_scatter20_kernel(ShardIn in, const uint32_t* __restrict__ base, uint32_t* __restrict__ out,
+                           uint32_t* __restrict__ perm) {
+    __shared__ uint32_t wc[kShardIPT * kWaves][WQ_MAX_SHARDS];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t k = threadIdx.x; k < kShardIPT * kWaves * WQ_MAX_SHARDS; k += kBlock) (&wc[0][0])[k] = 0;
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1;
+    const uint32_t m0 = blockIdx.x * kShardTile + threadIdx.x;
+    int64_t kx[kShardIPT], ky[kShardIPT], kz[kShardIPT];
+    uint64_t pk[kShardIPT];
+    uint32_t ext[kShardIPT], own[kShardIPT], rank[kShardIPT];
+    bool reg[kShardIPT];
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint32_t m = m0 + i * kBlock;
+        const bool valid = m < in.M;
+        own[i] = 0xFFFFFFFFu;
+        rank[i] = 0;
+        reg[i] = true;
+        if (valid) {
+            msg_key<RAW>(in, m, kx[i], ky[i], kz[i]);
+            const uint32_t w = in.world[m];
+            own[i] = shard_of(w, kx[i], ky[i], kz[i], in.G);
+            reg[i] = pack_key(w, kx[i], ky[i], kz[i], in.sf, &pk[i], &ext[i]);
+        }
+        const uint64_t wide = __ballot(valid && !reg[i]);
+        uint64_t todo = __ballot(valid);
+        while (todo) {
+            const int leader = __ffsll((unsigned long long)todo) - 1;
+            const uint32_t d = __shfl(own[i], leader, 64);
+            const uint64_t mask = __ballot(own[i] == d);
+            if (own[i] == d) rank[i] = __popcll(mask & lt) + __popcll(mask & wide & lt);
+            if (lane == leader) wc[i * kWaves + wave][d] = __popcll(mask) + __popcll(mask & wide);
+            todo &= ~mask;
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < in.G; d += kBlock) {
+        uint32_t run = base[(uint64_t)d * in.nblk + blockIdx.x];
+#pragma unroll
+        for (int k = 0; k < kShardIPT * kWaves; ++k) {
+            const uint32_t t = wc[k][d];
+            wc[k][d] = run;
+            run += t;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint32_t m = m0 + i * kBlock;
+        if (m >= in.M) continue;
+        const uint32_t slot = wc[i * kWaves + wave][own[i]] + rank[i];
+        uint32_t* o = out + (uint64_t)kSlotWords * slot;
+        const uint32_t rp = in.repl[m];
+        if (reg[i]) {
+            o[0] = (uint32_t)pk[i];
+            o[1] = (uint32_t)(pk[i] >> 32);
+            o[2] = ext[i];
+            o[3] = in.sender[m];
+            o[4] = rp | (kSlotReg << 8);
+            perm[slot] = m;
+        } else {
+            o[0] = (uint32_t)(uint64_t)kx[i];
+            o[1] = (uint32_t)((uint64_t)kx[i] >> 32);
+            o[2] = in.world[m];
+            o[3] = in.sender[m];
+            o[4] = rp | (kSlotHead << 8);
+            o[5] = (uint32_t)(uint64_t)ky[i];
+            o[6] = (uint32_t)((uint64_t)ky[i] >> 32);
+            o[7] = (uint32_t)(uint64_t)kz[i];
+            o[8] = (uint32_t)((uint64_t)kz[i] >> 32);
+            o[9] = kSlotTail << 8;
+            perm[slot] = m;
+            perm[slot + 1] = kNone;
+        }
     }
 }
 
@@ -253,12 +357,49 @@ int launch_shard_messages(wq_router* h, const double* d_pos, const int64_t* d_ke
     else
         hipLaunchKernelGGL((shard_count_kernel<false>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist);
     WQ_HIP(h, hipGetLastError());
-    hipLaunchKernelGGL(shard_scan_kernel, dim3(1), dim3(kScanThreads1), 0, s, hist, in.nblk, G, d_counts);
+    hipLaunchKernelGGL(shard_scan_kernel, dim3(1), dim3(kScanThreads1), 0, s, hist, in.nblk, G, d_counts, 1u);
     WQ_HIP(h, hipGetLastError());
     if (d_keys)
         hipLaunchKernelGGL((shard_scatter_kernel<true>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist, d_out);
     else
         hipLaunchKernelGGL((shard_scatter_kernel<false>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist, d_out);
+    WQ_HIP(h, hipGetLastError());
+    return WQ_OK;
+}
+
+// Compact slots (see shard_scatter20_kernel): d_slots holds up to 2M slots of kSlotWords words,
+// d_perm 2M words; the slot count for owner d lands at d_counts[d * stride].
+int launch_shard_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                       const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, uint32_t* d_slots,
+                       uint32_t* d_perm, uint32_t* d_counts, uint32_t stride) {
+    hipStream_t s = h->stream;
+    if (M == 0) return WQ_OK;  // the caller zeroed the counts
+    ShardIn in;
+    in.pos = d_pos;
+    in.keys = d_keys;
+    in.world = d_world;
+    in.sender = d_sender;
+    in.repl = d_repl;
+    in.M = (uint32_t)M;
+    in.G = G;
+    in.nblk = (uint32_t)((M + kShardTile - 1) / kShardTile);
+    in.sf = (double)h->cube_size;
+    in.si = (int64_t)h->cube_size;
+    in.pos_rec = false;
+    WQ_ALLOC(h, h->shard_hist, (uint64_t)in.nblk * G * 4);
+    uint32_t* hist = h->shard_hist.as<uint32_t>();
+    if (d_keys)
+        hipLaunchKernelGGL((shard_count_kernel<true, true>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist);
+    else
+        hipLaunchKernelGGL((shard_count_kernel<false, true>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist);
+    WQ_HIP(h, hipGetLastError());
+    hipLaunchKernelGGL(shard_scan_kernel, dim3(1), dim3(kScanThreads1), 0, s, hist, in.nblk, G, d_counts, stride);
+    WQ_HIP(h, hipGetLastError());
+    if (d_keys)
+        hipLaunchKernelGGL((shard_scatter20_kernel<true>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist, d_slots, d_perm);
+    else
+        hipLaunchKernelGGL((shard_scatter20_kernel<false>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist, d_slots,
+                           d_perm);
     WQ_HIP(h, hipGetLastError());
     return WQ_OK;
 }

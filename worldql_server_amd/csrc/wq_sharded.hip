@@ -36,12 +36,16 @@
 #include <rccl/rccl.h>
 #include <rocprim/rocprim.hpp>
 
-#include "route_common.hpp"
+#include "route_count.hpp"
+#include "route_gather.hpp"
 
 namespace wq {
 int launch_shard_messages(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
                           const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, wq_msg_rec* d_out,
                           uint32_t* d_counts);
+int launch_shard_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                       const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, uint32_t* d_slots,
+                       uint32_t* d_perm, uint32_t* d_counts, uint32_t stride);
 int launch_route_records(wq_router* h, const wq_msg_rec* d_recs, size_t M, uint32_t* d_offsets, uint32_t* d_peers,
                          uint32_t* d_msgs, size_t capacity);
 int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
@@ -145,6 +149,14 @@ RcclApi& rccl() {
 
 constexpr int kXNone = 0, kXHub = 1, kXRccl = 2, kXCallback = 3;
 constexpr double kHubTimeoutS = 120.0;
+// The small exchange vectors (ShardCtx::small, allocated at attach): the slot counts exchange
+// {slots, status} u32 x 2 per shard (send at kSmallA, receive after it), the pool-size exchange
+// {pool words, recipients, status, 0} u64 x 4 per shard (send at kSmallC, receive after it), and
+// the per-source recipient sums of the owner (u64 per shard at kSmallPairs).
+constexpr size_t kSmallA = 0, kSmallC = 1024, kSmallPairs = 6144, kSmallBytes = 8192;
+static_assert(kSmallA + 4 * WQ_MAX_SHARDS * 4 <= kSmallC && kSmallC + 8 * WQ_MAX_SHARDS * 8 <= kSmallPairs &&
+                  kSmallPairs + WQ_MAX_SHARDS * 8 <= kSmallBytes,
+              "small exchange vector layout");
 
 }  // namespace
 
@@ -170,14 +182,22 @@ struct ShardCtx {
     ncclComm_t comm = nullptr;
     wq_exchange_fn fn = nullptr;
     void* fn_ctx = nullptr;
-    // workspace
+    // workspace of the expanded-return tick (radius filter on) and the owner form
     DevBuf recs, recv, cnt2, pc, own_off, own_peers, own_e, ret_e, ret_off, ret_peers, by_msg, tmp, small;
     uint64_t own_cap = 0;
     std::vector<uint32_t> sc, rc;
     std::vector<uint64_t> ps, pr;
+    // workspace of the slot tick (compact slots out, row references + cube-list pools back)
+    DevBuf slots, perm, rslots, ocnt, hslot, plen, poff, claim, lead, self_ref, ref_send, ref_recv, pool_send,
+        pool_recv, desc_fill, desc_msg, e_msg, self_w;
+    uint64_t claim_cap = 0;  // claim table entries (power of two); 0 = not allocated
+    uint64_t ticks = 0;      // slot ticks run: the claim table's tag
+    // bytes this shard sent to / received from OTHER shards in its latest tick (xGMI volume)
+    uint64_t last_sent = 0, last_recv = 0;
     // the latest tick, kept for wq_sharded_copy_out after WQ_E_CAPACITY
     uint64_t last_M = 0, last_P = 0;
     bool last_ready = false;
+    bool last_slots = false;  // the latest tick was a slot tick (copy_out = scan + gather of desc_msg)
 };
 
 namespace {
@@ -277,12 +297,21 @@ int exchange(wq_router* h, const Xfer& x) {
     return set_error(h, WQ_E_INVALID, "no exchange attached");
 }
 
-// per received record: its recipient count; per source segment: its pair count
+// per received record: its recipient count; per source segment: {pair count, status}. A route that
+// reported an error (counter bits: 4 spin, 2 > 2^32 pairs, 8 stale table) sends no pairs, and its
+// status tells every source so, before any pair is exchanged.
 __global__ void k_owner_counts(const uint32_t* __restrict__ off, uint32_t R, SegBounds seg, uint32_t G,
-                               uint32_t* __restrict__ e, uint64_t* __restrict__ pc) {
+                               uint32_t* __restrict__ e, unsigned long long* __restrict__ pc,
+                               const wq_route_counters* __restrict__ cnt, const uint32_t* __restrict__ stale) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i < R) e[i] = off[i + 1] - off[i];
-    if (blockIdx.x == 0 && threadIdx.x < G) pc[threadIdx.x] = (uint64_t)off[seg.b[threadIdx.x + 1]] - off[seg.b[threadIdx.x]];
+    if (blockIdx.x == 0 && threadIdx.x < G) {
+        uint32_t err = cnt ? cnt->error : 0u;
+        if (stale && *stale) err |= kErrStale;
+        const uint32_t d = threadIdx.x;
+        pc[2 * d] = err ? 0ull : (unsigned long long)(off[seg.b[d + 1]] - off[seg.b[d]]);
+        pc[2 * d + 1] = (unsigned long long)err << 32;
+    }
 }
 
 // counts in message order: by_msg[rec.msg] = e of the record (every message has one record)
@@ -399,6 +428,220 @@ int scan_excl(wq_router* h, DevBuf& tmp, const uint32_t* in, uint32_t* out, size
     return WQ_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// the slot tick: compact slots to the owners, row references and cube-list pools back
+// ---------------------------------------------------------------------------------------------
+// What an owner returns per received slot (12 bytes, uint3 {x, y, z}): the message's recipients as
+// a row of words — z = kind << 30 | skipped index (kRefSkipNone: none), y = the row's source length
+// (OnlySelf: the recipient count, 0 or 1), x = where the source is:
+//   POOL    word offset in the pool the owner ships to this source (remote owners only): each cube
+//           a source's messages hit is shipped to it ONCE per tick, whatever the number of messages
+//   LIST    the cube's list in this handle's table (an owner's own messages: nothing is copied)
+//   INLINE  the record slot whose inline peers are the row (ditto)
+//   SELF    the sender itself (OnlySelf, when subscribed), or an empty row
+// The ingesting GPU turns every reference into a {len, skip, pointer} descriptor in message order
+// and gathers the CSR with gather_rows_kernel (route_gather.hpp).
+constexpr uint32_t kRefPool = 0, kRefList = 1, kRefInline = 2, kRefSelf = 3;
+constexpr uint32_t kRefSkipNone = 0x3FFFFFFFu;
+constexpr int kRefClaimTagBits = 26;  // claim words: tag << 38 | source << 32 | cube locator
+
+// Largest s < G with sb.b[s] <= i (segments may be empty).
+__device__ __forceinline__ uint32_t seg_find(const SegBounds& sb, uint32_t G, uint32_t i) {
+    uint32_t lo = 0, hi = G;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sb.b[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+struct RefOwnerParams {
+    const uint32_t* e;     // count pass: filtered recipients per slot
+    const uint2* info;     // count pass: locator per slot (route_count.hpp finish_message)
+    const uint32_t* list;
+    const Record* recs;
+    SegBounds seg;         // received slots per source shard
+    uint32_t G, me, R, tag;
+    unsigned long long* claim;  // (cube, source) claims of this tick, open addressing
+    uint32_t* lead;             // claim slot -> the slot that claimed it
+    uint64_t cmask;
+    uint32_t* cnt;         // per slot: the cube's peer count (OnlySelf: e)
+    uint32_t* hslot;       // per slot: its claim slot
+    uint32_t* plen;        // per slot: words it adds to its source's pool (R + 1 entries, last 0)
+    unsigned long long* seg_pairs;  // per source: recipients of its slots
+    const uint32_t* poff;  // exclusive scan of plen
+    uint3* ref_send;       // references of the remote sources' slots (own segment left out)
+    uint3* self_ref;       // references of this shard's own slots
+    uint4* desc_fill;      // pool rows: the claiming slot copies its cube's peers
+};
+
+__device__ __forceinline__ uint32_t slot_cnt(const uint2 inf, uint32_t e, const uint32_t* list) {
+    if (inf.x & kLocSelf) return e;
+    if (inf.x & kLocGlobal) return list[inf.x & ~kLocGlobal];
+    return inf.y == kNone ? 0u : inf.y >> 24;  // inline record, or no subscriber at all
+}
+
+// (owner) per received slot: the cube's peer count, and for a remote source's slot the claim of its
+// (source, cube) pair — the first claimer ships the cube's peers in that source's pool, the others
+// point at them. Per-source recipient sums go to seg_pairs (LDS first, a few global atomics per block).
+__global__ __launch_bounds__(kBlock) void k_ref_claim(RefOwnerParams p) {
+    __shared__ unsigned long long acc[WQ_MAX_SHARDS];
+    const int tid = threadIdx.x;
+    for (uint32_t d = tid; d < p.G; d += kBlock) acc[d] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * kBlock + tid;
+    uint32_t s = 0, ei = 0;
+    if (i < p.R) {
+        s = seg_find(p.seg, p.G, i);
+        const uint2 inf = p.info[i];
+        ei = p.e[i];
+        const uint32_t cnt = slot_cnt(inf, ei, p.list);
+        bool leader = false;
+        uint64_t hs = 0;
+        if (s != p.me && !(inf.x & kLocSelf) && cnt) {
+            const unsigned long long key = ((unsigned long long)p.tag << 38) | ((unsigned long long)s << 32) | inf.x;
+            uint64_t hv = ((uint64_t)inf.x | ((uint64_t)s << 32)) * 0x9E3779B97F4A7C15ull;
+            hv ^= hv >> 29;
+            hs = hv & p.cmask;
+            for (;;) {
+                unsigned long long v = __hip_atomic_load(p.claim + hs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((v >> 38) != p.tag) {  // a previous tick's word: free
+                    const unsigned long long old = atomicCAS(p.claim + hs, v, key);
+                    if (old == v) {
+                        leader = true;
+                        break;
+                    }
+                    v = old;
+                }
+                if (v == key) break;
+                if ((v >> 38) == p.tag) hs = (hs + 1) & p.cmask;
+            }
+            if (leader) p.lead[hs] = i;
+        }
+        p.cnt[i] = cnt;
+        p.hslot[i] = (uint32_t)hs;
+        p.plen[i] = leader ? cnt : 0u;
+    }
+    if (i == p.R) p.plen[i] = 0;
+    // per-source recipient sums
+    const uint32_t s0 = __shfl(s, 0, 64);
+    if (__all(i >= p.R || s == s0)) {
+        const uint64_t w = wave_sum_u64(ei);
+        if ((tid & 63) == 0 && w) atomicAdd(&acc[s0], (unsigned long long)w);
+    } else if (i < p.R && ei) {
+        atomicAdd(&acc[s], (unsigned long long)ei);
+    }
+    __syncthreads();
+    for (uint32_t d = tid; d < p.G; d += kBlock)
+        if (acc[d]) atomicAdd(p.seg_pairs + d, acc[d]);
+}
+
+// (owner) per received slot: its reference (own slots: straight into the table; remote: into the
+// source's pool) and, for a claiming slot, the pool row copying its cube's peers.
+__global__ __launch_bounds__(kBlock) void k_ref_make(RefOwnerParams p) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= p.R) return;
+    const uint32_t s = seg_find(p.seg, p.G, i);
+    const uint2 inf = p.info[i];
+    const uint32_t cnt = p.cnt[i];
+    uint32_t kind = kRefSelf, off = 0, skip = kRefSkipNone;
+    if (inf.x & kLocSelf) {
+        kind = kRefSelf;
+    } else if (inf.x & kLocGlobal) {
+        kind = kRefList;
+        off = (inf.x & ~kLocGlobal) + 1;
+        skip = inf.y == kNone ? kRefSkipNone : inf.y;
+    } else if (inf.y != kNone) {
+        kind = kRefInline;
+        off = inf.x;
+        const uint32_t s24 = inf.y & kSkipNone24;
+        skip = s24 == kSkipNone24 ? kRefSkipNone : s24;
+    }  // else: no subscriber — an empty SELF row
+    if (s == p.me) {
+        p.self_ref[i - p.seg.b[s]] = make_uint3(off, cnt, (kind << 30) | skip);
+        p.desc_fill[i] = make_uint4(0, kNone, 0, 0);
+        return;
+    }
+    uint4 fill = make_uint4(0, kNone, 0, 0);
+    uint3 ref;
+    if (kind == kRefList || kind == kRefInline) {
+        const uint32_t j = p.lead[p.hslot[i]];
+        ref = make_uint3(p.poff[j] - p.poff[p.seg.b[s]], cnt, (kRefPool << 30) | skip);
+        if (j == i) {
+            const uint32_t* src = kind == kRefList ? p.list + off
+                                                   : reinterpret_cast<const uint32_t*>(p.recs) + ((uint64_t)off * 32 + kInlineWord0);
+            const uint64_t a = reinterpret_cast<uint64_t>(src);
+            fill = make_uint4(cnt, kNone, (uint32_t)a, (uint32_t)(a >> 32));
+        }
+    } else {
+        ref = make_uint3(0, cnt, (kRefSelf << 30) | kRefSkipNone);
+    }
+    p.desc_fill[i] = fill;
+    const uint32_t a = p.seg.b[p.me], nself = p.seg.b[p.me + 1] - a;
+    p.ref_send[i < a ? i : i - nself] = ref;
+}
+
+// (owner) the per-destination words of the pool-size exchange: {pool words, recipients, status, 0}.
+// status = error bits of the count pass (2: > 2^32 pairs in a block, 8: stale table) << 32.
+__global__ void k_ref_sizes(const uint32_t* __restrict__ poff, SegBounds seg, uint32_t G, uint32_t me,
+                            const unsigned long long* __restrict__ seg_pairs, const wq_route_counters* __restrict__ cnt,
+                            const uint32_t* __restrict__ stale, unsigned long long* __restrict__ out) {
+    const uint32_t d = threadIdx.x;
+    if (d >= G) return;
+    uint32_t err = cnt->error;
+    if (stale && *stale) err |= kErrStale;
+    out[4 * d] = d == me ? 0ull : (unsigned long long)(poff[seg.b[d + 1]] - poff[seg.b[d]]);
+    out[4 * d + 1] = seg_pairs[d];
+    out[4 * d + 2] = (unsigned long long)err << 32;
+    out[4 * d + 3] = 0;
+}
+
+struct ResolveParams {
+    const uint32_t* perm;     // sent slot -> message (kNone: a tail slot)
+    const uint32_t* sender;   // the caller's d_sender
+    const uint3* ref_recv;    // references from the remote owners, in sent-slot order (own segment left out)
+    const uint3* self_ref;    // references of this shard's own slots
+    uint32_t self_a, self_b;  // this shard's own segment of the sent slots
+    SegBounds sseg;           // sent slots per owner
+    uint32_t G, n;
+    const uint32_t* pool;     // the pools received, owner after owner
+    uint64_t pbase[WQ_MAX_SHARDS + 1];
+    const uint32_t* list;
+    const Record* recs;
+    uint4* desc_msg;          // per message: {recipients, skip, pointer}
+    uint32_t* e_msg;          // per message: recipients (M + 1 entries, last 0)
+    uint32_t* self_w;         // per message: the sender, for OnlySelf rows
+};
+
+// (ingesting GPU) per sent slot: the message's row descriptor, in message order.
+__global__ __launch_bounds__(kBlock) void k_ref_resolve(ResolveParams p) {
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= p.n) return;
+    const uint32_t m = p.perm[k];
+    if (m == kNone) return;  // the tail of a two-slot message
+    const bool own = k >= p.self_a && k < p.self_b;
+    const uint3 ref = own ? p.self_ref[k - p.self_a] : p.ref_recv[k < p.self_a ? k : k - (p.self_b - p.self_a)];
+    const uint32_t kind = ref.z >> 30, sk = ref.z & kRefSkipNone;
+    uint32_t skip = sk == kRefSkipNone ? kNone : sk;
+    const uint32_t* src;
+    uint32_t e;
+    if (kind == kRefSelf) {
+        e = ref.y;
+        skip = kNone;
+        if (e) p.self_w[m] = p.sender[m];
+        src = p.self_w + m;
+    } else {
+        e = ref.y - (skip != kNone ? 1u : 0u);
+        if (kind == kRefPool) src = p.pool + p.pbase[seg_find(p.sseg, p.G, k)] + ref.x;
+        else if (kind == kRefList) src = p.list + ref.x;
+        else src = reinterpret_cast<const uint32_t*>(p.recs) + ((uint64_t)ref.x * 32 + kInlineWord0);
+    }
+    const uint64_t a = reinterpret_cast<uint64_t>(src);
+    p.desc_msg[m] = make_uint4(e, skip, (uint32_t)a, (uint32_t)(a >> 32));
+    p.e_msg[m] = e;
+}
+
 int attach(wq_router* h, uint32_t G, uint32_t rank) {
     if (!h || G == 0 || G > WQ_MAX_SHARDS || rank >= G) return WQ_E_INVALID;
     if (h->shard) return set_error(h, WQ_E_INVALID, "an exchange is already attached (wq_shard_detach first)");
@@ -406,6 +649,33 @@ int attach(wq_router* h, uint32_t G, uint32_t rank) {
     if (!h->shard) return WQ_E_OOM;
     h->shard->G = G;
     h->shard->rank = rank;
+    // the small exchange vectors live here for the handle's whole attachment: a tick never has to
+    // allocate before its first exchange
+    if (h->shard->small.ensure(kSmallBytes) != hipSuccess) {
+        delete h->shard;
+        h->shard = nullptr;
+        return set_error(h, WQ_E_OOM, "hipMalloc of the shard exchange vectors");
+    }
+    return WQ_OK;
+}
+
+// The slot tick's CSR from its message-order descriptors: offsets = exclusive scan of e_msg (whose
+// last entry is 0, so offsets[M] = P), then the rows gathered (outputs beyond capacity not written).
+int slots_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity) {
+    ShardCtx& sc = *h->shard;
+    const uint64_t M = sc.last_M;
+    hipStream_t s = h->stream;
+    size_t bytes = 0;
+    WQ_HIP(h, rocprim::exclusive_scan(nullptr, bytes, sc.e_msg.as<uint32_t>(), d_offsets, 0u, M + 1,
+                                      rocprim::plus<uint32_t>(), s));
+    WQ_ALLOC(h, sc.tmp, bytes);
+    WQ_HIP(h, rocprim::exclusive_scan(sc.tmp.p, bytes, sc.e_msg.as<uint32_t>(), d_offsets, 0u, M + 1,
+                                      rocprim::plus<uint32_t>(), s));
+    if (M && capacity) {
+        GatherParams gp{d_offsets, sc.desc_msg.as<uint4>(), (uint32_t)M, d_peers, d_msgs, capacity};
+        hipLaunchKernelGGL(gather_rows_kernel<16>, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, gp);
+        WQ_HIP(h, hipGetLastError());
+    }
     return WQ_OK;
 }
 
@@ -414,6 +684,11 @@ int copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_m
     ShardCtx& sc = *h->shard;
     const uint64_t M = sc.last_M, P = sc.last_P;
     hipStream_t s = h->stream;
+    if (sc.last_slots) {
+        if (int rc = slots_copy_out(h, d_offsets, d_peers, d_msgs, capacity)) return rc;
+        if (P > capacity) return set_error(h, WQ_E_CAPACITY, "sharded tick: output capacity too small (required size in *n_pairs)");
+        return WQ_OK;
+    }
     if (M) {
         WQ_ALLOC(h, sc.by_msg, M * 4);
         const unsigned g = (unsigned)((M + kBlock - 1) / kBlock);
@@ -441,8 +716,12 @@ void shard_release(wq_router* h) {
     if (!h->shard) return;
     ShardCtx* sc = h->shard;
     if (sc->kind == kXRccl && sc->comm) (void)rccl().CommDestroy(sc->comm);
-    DevBuf* bufs[] = {&sc->recs, &sc->recv, &sc->cnt2, &sc->pc, &sc->own_off, &sc->own_peers, &sc->own_e,
-                      &sc->ret_e, &sc->ret_off, &sc->ret_peers, &sc->by_msg, &sc->tmp, &sc->small};
+    DevBuf* bufs[] = {&sc->recs,     &sc->recv,      &sc->cnt2,     &sc->pc,        &sc->own_off,  &sc->own_peers,
+                      &sc->own_e,    &sc->ret_e,     &sc->ret_off,  &sc->ret_peers, &sc->by_msg,   &sc->tmp,
+                      &sc->small,    &sc->slots,     &sc->perm,     &sc->rslots,    &sc->ocnt,     &sc->hslot,
+                      &sc->plen,     &sc->poff,      &sc->claim,    &sc->lead,      &sc->self_ref, &sc->ref_send,
+                      &sc->ref_recv, &sc->pool_send, &sc->pool_recv, &sc->desc_fill, &sc->desc_msg, &sc->e_msg,
+                      &sc->self_w};
     for (DevBuf* b : bufs) b->release();
     delete sc;
     h->shard = nullptr;
@@ -552,6 +831,35 @@ int wq_sharded_apply_ops(wq_router* h, const wq_op* ops, size_t n) {
     return wq_apply_ops(h, mine.data(), mine.size());
 }
 
+// A receive buffer could not be allocated after the peers were told what they will send: the
+// collective cannot complete. The hub is marked broken (its peers fail at their next wait instead
+// of timing out); an RCCL or callback caller has to abandon its communicator.
+static int fatal_receive(wq_router* h, const char* what) {
+    ShardCtx& sc = *h->shard;
+    if (sc.kind == kXHub) {
+        std::lock_guard<std::mutex> lk(sc.hub->mu);
+        sc.hub->broken = true;
+        sc.hub->cv.notify_all();
+    }
+    return set_error(h, WQ_E_OOM, what);
+}
+
+// Status word of a failed local step as the exchanges carry it (the negated WQ_E_* code).
+static uint32_t status_of(int rc) { return (uint32_t)(-rc); }
+
+// The error a shard reports for a status word it received (its own or a peer's): counter bits
+// << 32 (4 spin, 2 > 2^32 pairs, 8 stale table) or a negated WQ_E_* code.
+static int status_error(wq_router* h, uint64_t st, uint32_t from) {
+    const uint32_t bits = (uint32_t)(st >> 32), code = (uint32_t)st;
+    std::string who = " (shard " + std::to_string(from) + ")";
+    if (code) return set_error(h, -(int)code, ("sharded tick: a shard's local step failed" + who).c_str());
+    if (bits & kErrStale)
+        return set_error(h, WQ_E_INVALID, ("sharded tick: a shard's table is still missing an incremental batch the "
+                                           "device could not apply" + who).c_str());
+    if (bits & 4u) return set_error(h, WQ_E_TIMEOUT, ("sharded tick: a bounded spin gave up" + who).c_str());
+    return set_error(h, WQ_E_CAPACITY, ("sharded tick: more than 2^32-1 pairs in one owner block" + who).c_str());
+}
+
 // Steps 1-3 of a sharded tick, shared by the origin and owner forms: shard this rank's messages,
 // exchange the counts (host read 1) and the records, route what this shard owns into
 // own_off / own_peers. *R_out = records received, *seg = their source segments. A local route
@@ -565,17 +873,31 @@ static int shard_exchange_route(wq_router* h, const double* d_pos, const int64_t
     const uint32_t G = sc.G;
     const size_t M = n_msgs;
     sc.last_ready = false;
+    sc.last_slots = false;
     int& late = *late_out;  // a local failure, reported once the tick's exchanges are complete
     std::string& late_msg = *late_msg_out;
+    auto fail = [&](int rc) {
+        if (rc && !late) {
+            late = rc;
+            late_msg = h->err;
+        }
+        return rc;
+    };
 
-    // 1. shard
-    WQ_ALLOC(h, sc.recs, (M ? M : 1) * sizeof(wq_msg_rec));
-    WQ_ALLOC(h, sc.cnt2, 2 * G * 4);
-    uint32_t* cnt_send = sc.cnt2.as<uint32_t>();
+    const int inject = h->shard_inject;
+    h->shard_inject = 0;
+    // 1. shard (a failure here: this shard sends nothing, and reports the error after the exchanges)
+    uint32_t* cnt_send = reinterpret_cast<uint32_t*>(sc.small.as<char>() + kSmallA);
     uint32_t* cnt_recv = cnt_send + G;
-    int rc = launch_shard_messages(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, sc.recs.as<wq_msg_rec>(),
-                                   cnt_send);
-    if (rc) return rc;  // nothing exchanged yet: every rank's failure here is local and symmetric-safe
+    WQ_HIP(h, hipMemsetAsync(cnt_send, 0, 4 * G, s));
+    if (inject == 1) fail(set_error(h, WQ_E_INVALID, "injected failure at step 1 (test hook)"));
+    int rc = late ? late : sc.recs.ensure((M ? M : 1) * sizeof(wq_msg_rec)) == hipSuccess
+                 ? WQ_OK
+                 : set_error(h, WQ_E_OOM, "hipMalloc of the sharded tick's records");
+    if (!fail(rc))
+        fail(launch_shard_messages(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, sc.recs.as<wq_msg_rec>(),
+                                   cnt_send));
+    if (late) WQ_HIP(h, hipMemsetAsync(cnt_send, 0, 4 * G, s));
     // 2. counts, then the records
     std::vector<size_t> four(G, 4);
     {
@@ -597,29 +919,305 @@ static int shard_exchange_route(wq_router* h, const double* d_pos, const int64_t
         R += sc.rc[d];
         seg.b[d + 1] = (uint32_t)R;
     }
-    if (R >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "more than 2^32 - 1024 records on one owner");
-    WQ_ALLOC(h, sc.recv, (R ? R : 1) * sizeof(wq_msg_rec));
+    if (R >= 0xFFFFFC00ull) return fatal_receive(h, "more than 2^32 - 1024 records on one owner");
+    if (sc.recv.ensure((R ? R : 1) * sizeof(wq_msg_rec)) != hipSuccess)
+        return fatal_receive(h, "hipMalloc of the received records");
     {
         Xfer x{{sc.recs.p}, {sb.data()}, {sc.recv.p}, {rb.data()}, 1};
         if ((rc = exchange(h, x))) return rc;
     }
-    // 3. route what this shard owns
-    WQ_ALLOC(h, sc.own_off, (R + 1) * 4);
+    // 3. route what this shard owns (a failure: empty results here, the error after the exchanges)
     if (!sc.own_cap) {
         sc.own_cap = 16 * R + 4096;
         if (sc.own_cap > 0xFFFFFFFFull) sc.own_cap = 0xFFFFFFFFull;
     }
-    WQ_ALLOC(h, sc.own_peers, sc.own_cap * 4);
-    rc = launch_route_records(h, sc.recv.as<wq_msg_rec>(), R, sc.own_off.as<uint32_t>(), sc.own_peers.as<uint32_t>(),
-                              nullptr, sc.own_cap);
-    if (rc) {  // keep the collective going with empty results
-        late = rc;
-        late_msg = h->err;
-        WQ_HIP(h, hipMemsetAsync(sc.own_off.p, 0, (R + 1) * 4, s));
-    }
+    const bool bufs = sc.own_off.ensure((R + 1) * 4) == hipSuccess && sc.own_peers.ensure(sc.own_cap * 4) == hipSuccess &&
+                      sc.own_e.ensure((R ? R : 1) * 4) == hipSuccess;
+    if (!bufs) fail(set_error(h, WQ_E_OOM, "hipMalloc of the owner's route buffers"));
+    if (inject == 3) fail(set_error(h, WQ_E_INVALID, "injected failure at step 3 (test hook)"));
+    if (!late)
+        fail(launch_route_records(h, sc.recv.as<wq_msg_rec>(), R, sc.own_off.as<uint32_t>(), sc.own_peers.as<uint32_t>(),
+                                  nullptr, sc.own_cap));
     *R_out = R;
     *seg_out = seg;
     return WQ_OK;
+}
+
+// The slot tick (radius filter off): wq_sharded_route_tick_device's result with
+//   A   {slots, status} per owner                                        (host read 1)
+//   B   the compact slots (20 B per regular message)
+//   C   {pool words, recipients, status} per source                     (host read 2)
+//   D   per slot a 12-byte row reference, and per source ONE copy of every cube its messages hit
+// so a long list crosses xGMI once per (tick, destination) instead of once per message; the
+// ingesting GPU gathers the CSR itself. G = 1 skips the exchanges and reads P back at the end.
+// Local failures keep the collective going: a failed shard step sends zero-sized segments with its
+// status, every shard sees every status and all of them return the error after exchange D.
+static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                              const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t* d_offsets,
+                              uint32_t* d_peers, uint32_t* d_msgs, size_t capacity, size_t* n_pairs) {
+    hipStream_t s = h->stream;
+    ShardCtx& sc = *h->shard;
+    const uint32_t G = sc.G, me = sc.rank;
+    sc.last_ready = false;
+    sc.last_slots = true;
+    int late = WQ_OK;
+    std::string late_msg;
+    auto fail = [&](int rc) {
+        if (rc && !late) {
+            late = rc;
+            late_msg = h->err;
+        }
+        return rc;
+    };
+    char* small = sc.small.as<char>();
+    uint32_t* a_send = reinterpret_cast<uint32_t*>(small + kSmallA);
+    uint32_t* a_recv = a_send + 2 * G;
+    unsigned long long* c_send = reinterpret_cast<unsigned long long*>(small + kSmallC);
+    unsigned long long* c_recv = c_send + 4 * G;
+    unsigned long long* seg_pairs = reinterpret_cast<unsigned long long*>(small + kSmallPairs);
+    auto alloc = [&](DevBuf& b, size_t bytes) -> int {
+        return b.ensure(bytes) == hipSuccess ? WQ_OK : set_error(h, WQ_E_OOM, "hipMalloc (sharded tick workspace)");
+    };
+
+    const int inject = h->shard_inject;
+    h->shard_inject = 0;
+    // ---- 1. the M-sized buffers, then the slots grouped by owner ----
+    const uint64_t slot_cap = 2 * (uint64_t)M + 1;
+    WQ_HIP(h, hipMemsetAsync(a_send, 0, 8 * G, s));
+    if (inject == 1) fail(set_error(h, WQ_E_INVALID, "injected failure at step 1 (test hook)"));
+    if (!late && !fail(alloc(sc.slots, slot_cap * kSlotWords * 4)) && !fail(alloc(sc.perm, slot_cap * 4)) &&
+        !fail(alloc(sc.desc_msg, (M + 1) * 16)) && !fail(alloc(sc.e_msg, (M + 1) * 4)) &&
+        !fail(alloc(sc.self_w, (M + 1) * 4)))
+        fail(launch_shard_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, sc.slots.as<uint32_t>(),
+                                sc.perm.as<uint32_t>(), a_send, 2));
+    if (late) {  // nothing to send: zero slots everywhere, and the status
+        std::vector<uint32_t> v(2 * G, 0);
+        for (uint32_t d = 0; d < G; ++d) v[2 * d + 1] = status_of(late);
+        WQ_HIP(h, hipMemcpyAsync(a_send, v.data(), 8 * G, hipMemcpyHostToDevice, s));
+    }
+    std::vector<size_t> eight(G, 8), thirty2(G, 32);
+    int rc;
+    if (G > 1) {
+        Xfer x{{a_send}, {eight.data()}, {a_recv}, {eight.data()}, 1};
+        if ((rc = exchange(h, x))) return rc;
+    }
+    std::vector<uint32_t> av(4 * G);
+    WQ_HIP(h, hipMemcpyAsync(av.data(), a_send, (G > 1 ? 16 : 8) * G, hipMemcpyDeviceToHost, s));
+    WQ_HIP(h, hipStreamSynchronize(s));  // host read 1
+    if (G == 1) av[2] = av[0], av[3] = av[1];
+    std::vector<uint64_t> n_out(G), n_in(G);
+    uint64_t peer_status = 0;
+    uint32_t peer_from = 0;
+    SegBounds sseg, rseg;
+    sseg.b[0] = rseg.b[0] = 0;
+    uint64_t R = 0, S = 0;
+    for (uint32_t d = 0; d < G; ++d) {
+        n_out[d] = av[2 * d];
+        n_in[d] = av[2 * G + 2 * d];
+        if (av[2 * G + 2 * d + 1] && !peer_status) {
+            peer_status = av[2 * G + 2 * d + 1];
+            peer_from = d;
+        }
+        S += n_out[d];
+        R += n_in[d];
+        sseg.b[d + 1] = (uint32_t)S;
+        rseg.b[d + 1] = (uint32_t)R;
+    }
+    if (R >= 0xFFFFFC00ull) return fatal_receive(h, "more than 2^32 - 1024 slots on one owner");
+    const uint64_t n_self = n_in[me], R_remote = R - n_self;
+
+    // ---- 2. the slots ----
+    const uint32_t* rslots = sc.slots.as<uint32_t>();
+    if (G > 1) {
+        if (alloc(sc.rslots, (R ? R : 1) * kSlotWords * 4)) return fatal_receive(h, "hipMalloc of the received slots");
+        std::vector<size_t> sb(G), rb(G);
+        for (uint32_t d = 0; d < G; ++d) {
+            sb[d] = n_out[d] * kSlotWords * 4;
+            rb[d] = n_in[d] * kSlotWords * 4;
+        }
+        Xfer x{{sc.slots.p}, {sb.data()}, {sc.rslots.p}, {rb.data()}, 1};
+        if ((rc = exchange(h, x))) return rc;
+        rslots = sc.rslots.as<uint32_t>();
+    }
+
+    // ---- 3. the owner: count (local_message.rs:52-86 per slot), claims, pool sizes ----
+    WQ_HIP(h, hipMemsetAsync(seg_pairs, 0, 8 * G, s));
+    if (inject == 3) fail(set_error(h, WQ_E_INVALID, "injected failure at step 3 (test hook)"));
+    // fold in a finished incremental batch first (it may rebuild the table the view points into)
+    if (!late) fail(table_resolve(h, false));
+    const TableView tv = table_view(h);
+    wq_route_counters *cur = nullptr, *nxt = nullptr;
+    if (!late && R) fail(route_counters(h, R, nullptr, &cur, &nxt));
+    if (!late && R) {
+        RouteWs& rw = h->rws;
+        const uint32_t nb = (uint32_t)((R + kBlock - 1) / kBlock);
+        if (!fail(alloc(rw.e, R * 4)) && !fail(alloc(rw.info, R * 8)) && !fail(alloc(rw.tiles, (uint64_t)nb * 12)) &&
+            !fail(alloc(sc.ocnt, R * 4)) && !fail(alloc(sc.hslot, R * 4)) && !fail(alloc(sc.plen, (R + 1) * 4)) &&
+            !fail(alloc(sc.poff, (R + 1) * 4)) && !fail(alloc(sc.desc_fill, R * 16)) &&
+            !fail(alloc(sc.self_ref, (n_self + 1) * 12)) && !fail(alloc(sc.ref_send, (R_remote + 1) * 12))) {
+            CountParams cp;
+            cp.in = RouteIn{nullptr, nullptr, nullptr, nullptr, nullptr, (uint32_t)R, (int64_t)h->cube_size};
+            cp.in.slots = rslots;
+            cp.t = tv;
+            cp.e = rw.e.as<uint32_t>();
+            cp.info = rw.info.as<uint2>();
+            cp.tile_total = rw.tiles.as<uint32_t>();
+            cp.tile_F = cp.tile_total + nb;
+            cp.cnt = cur;
+            cp.cnt_next = nxt;
+            cp.health = route_health(h);
+            hipLaunchKernelGGL((count_kernel<true, 1, 8, 0, false, true>), dim3(nb), dim3(kBlock), 0, s, cp);
+            if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "count launch (sharded tick)"));
+        }
+        uint64_t C = 0;
+        if (!late && R_remote) {  // claim table: load <= 1/2
+            C = 1024;
+            while (C < 2 * R_remote) C <<= 1;
+            if (C > sc.claim_cap) {
+                if (!fail(alloc(sc.claim, C * 8)) && !fail(alloc(sc.lead, C * 4))) {
+                    if (hipMemsetAsync(sc.claim.p, 0, C * 8, s) != hipSuccess) fail(set_error(h, WQ_E_HIP, "memset"));
+                    sc.claim_cap = C;
+                }
+            } else {
+                C = sc.claim_cap;
+            }
+        }
+        if (!late) {
+            const uint64_t period = (1ull << kRefClaimTagBits) - 1;
+            if (sc.ticks && sc.ticks % period == 0 && sc.claim_cap &&
+                hipMemsetAsync(sc.claim.p, 0, sc.claim_cap * 8, s) != hipSuccess)  // tags wrap: forget them all
+                fail(set_error(h, WQ_E_HIP, "memset"));
+            RefOwnerParams rp{};
+            rp.e = rw.e.as<uint32_t>();
+            rp.info = rw.info.as<uint2>();
+            rp.list = tv.list;
+            rp.recs = tv.recs;
+            rp.seg = rseg;
+            rp.G = G;
+            rp.me = me;
+            rp.R = (uint32_t)R;
+            rp.tag = (uint32_t)(sc.ticks % period) + 1u;
+            rp.claim = sc.claim.as<unsigned long long>();
+            rp.lead = sc.lead.as<uint32_t>();
+            rp.cmask = C ? C - 1 : 0;
+            rp.cnt = sc.ocnt.as<uint32_t>();
+            rp.hslot = sc.hslot.as<uint32_t>();
+            rp.plen = sc.plen.as<uint32_t>();
+            rp.seg_pairs = seg_pairs;
+            rp.poff = sc.poff.as<uint32_t>();
+            rp.ref_send = sc.ref_send.as<uint3>();
+            rp.self_ref = sc.self_ref.as<uint3>();
+            rp.desc_fill = sc.desc_fill.as<uint4>();
+            sc.ticks++;
+            hipLaunchKernelGGL(k_ref_claim, dim3((unsigned)((R + kBlock) / kBlock)), dim3(kBlock), 0, s, rp);
+            if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "claim launch (sharded tick)"));
+            if (!late) fail(scan_excl(h, sc.tmp, sc.plen.as<uint32_t>(), sc.poff.as<uint32_t>(), R + 1));
+            if (!late) {
+                hipLaunchKernelGGL(k_ref_make, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rp);
+                hipLaunchKernelGGL(k_ref_sizes, dim3(1), dim3(64), 0, s, sc.poff.as<uint32_t>(), rseg, G, me,
+                                   (const unsigned long long*)seg_pairs, cur, tv.stale, c_send);
+                if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "reference launch (sharded tick)"));
+            }
+        }
+    }
+    if (late || !R) {  // nothing routed here: zero sizes (and the status, if a step failed)
+        std::vector<unsigned long long> v(4 * G, 0);
+        if (late)
+            for (uint32_t d = 0; d < G; ++d) v[4 * d + 2] = status_of(late);
+        WQ_HIP(h, hipMemcpyAsync(c_send, v.data(), 32 * G, hipMemcpyHostToDevice, s));
+    }
+    if (G > 1) {
+        Xfer x{{c_send}, {thirty2.data()}, {c_recv}, {thirty2.data()}, 1};
+        if ((rc = exchange(h, x))) return rc;
+    }
+    std::vector<unsigned long long> cv(8 * G);
+    WQ_HIP(h, hipMemcpyAsync(cv.data(), c_send, (G > 1 ? 64 : 32) * G, hipMemcpyDeviceToHost, s));
+    WQ_HIP(h, hipStreamSynchronize(s));  // host read 2
+    if (G == 1)
+        for (int q = 0; q < 4; ++q) cv[4 + q] = cv[q];
+    std::vector<uint64_t> pool_out(G), pool_in(G);
+    uint64_t P = 0, pool_out_total = 0, pool_in_total = 0;
+    std::vector<uint64_t> pbase(G + 1, 0);
+    for (uint32_t d = 0; d < G; ++d) {
+        pool_out[d] = cv[4 * d];
+        pool_in[d] = cv[4 * G + 4 * d];
+        P += cv[4 * G + 4 * d + 1];
+        const uint64_t st = cv[4 * G + 4 * d + 2];
+        if (st && !peer_status) {
+            peer_status = st;
+            peer_from = d;
+        }
+        pool_out_total += pool_out[d];
+        pbase[d] = pool_in_total;
+        pool_in_total += pool_in[d];
+    }
+    pbase[G] = pool_in_total;
+
+    // ---- 4. references and pools, then the ingesting side's exchange ----
+    if (alloc(sc.pool_send, (pool_out_total + 1) * 4)) return fatal_receive(h, "hipMalloc of the pools to send");
+    if (alloc(sc.pool_recv, (pool_in_total + 1) * 4) || alloc(sc.ref_recv, (S - n_out[me] + 1) * 12))
+        return fatal_receive(h, "hipMalloc of the references / pools to receive");
+    if (!late && R_remote && pool_out_total) {
+        GatherParams gp{sc.poff.as<uint32_t>(), sc.desc_fill.as<uint4>(), (uint32_t)R, sc.pool_send.as<uint32_t>(),
+                        nullptr, pool_out_total};
+        hipLaunchKernelGGL(gather_rows_kernel<16>, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, gp);
+        if (hipGetLastError() != hipSuccess) return fatal_receive(h, "pool gather launch");
+    }
+    uint64_t sent = 0, recvd = 0;
+    if (G > 1) {
+        std::vector<size_t> rs(G), rr(G), ps(G), pr(G);
+        for (uint32_t d = 0; d < G; ++d) {
+            rs[d] = d == me || late ? 0 : n_in[d] * 12;  // references for the slots d sent here
+            // a shard whose local step failed (a WQ_E_* code in its status) sends no references
+            rr[d] = d == me || (uint32_t)cv[4 * G + 4 * d + 2] != 0 ? 0 : n_out[d] * 12;
+            ps[d] = late ? 0 : pool_out[d] * 4;
+            pr[d] = pool_in[d] * 4;
+            if (d != me) {
+                sent += n_out[d] * kSlotWords * 4 + rs[d] + ps[d];
+                recvd += n_in[d] * kSlotWords * 4 + rr[d] + pr[d];
+            }
+        }
+        Xfer x{{sc.ref_send.p, sc.pool_send.p}, {rs.data(), ps.data()}, {sc.ref_recv.p, sc.pool_recv.p},
+               {rr.data(), pr.data()}, 2};
+        if ((rc = exchange(h, x))) return rc;
+    }
+    sc.last_sent = sent;
+    sc.last_recv = recvd;
+    if (late) {
+        h->err = late_msg;
+        return late;
+    }
+    if (peer_status) return status_error(h, peer_status, peer_from);
+
+    // ---- 5. the ingesting side: descriptors in message order, offsets, rows ----
+    if (S) {
+        ResolveParams rp{};
+        rp.perm = sc.perm.as<uint32_t>();
+        rp.sender = d_sender;
+        rp.ref_recv = sc.ref_recv.as<uint3>();
+        rp.self_ref = sc.self_ref.as<uint3>();
+        rp.self_a = sseg.b[me];
+        rp.self_b = sseg.b[me + 1];
+        rp.sseg = sseg;
+        rp.G = G;
+        rp.n = (uint32_t)S;
+        rp.pool = sc.pool_recv.as<uint32_t>();
+        for (uint32_t d = 0; d <= G; ++d) rp.pbase[d] = pbase[d];
+        rp.list = tv.list;
+        rp.recs = tv.recs;
+        rp.desc_msg = sc.desc_msg.as<uint4>();
+        rp.e_msg = sc.e_msg.as<uint32_t>();
+        rp.self_w = sc.self_w.as<uint32_t>();
+        hipLaunchKernelGGL(k_ref_resolve, dim3((unsigned)((S + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rp);
+        WQ_HIP(h, hipGetLastError());
+    }
+    WQ_HIP(h, hipMemsetAsync(sc.e_msg.as<uint32_t>() + M, 0, 4, s));
+    sc.last_M = M;
+    sc.last_P = P;
+    sc.last_ready = true;
+    *n_pairs = P;
+    if (P > 0xFFFFFFFFull) return set_error(h, WQ_E_CAPACITY, "more than 2^32-1 pairs in one tick");
+    return copy_out(h, d_offsets, d_peers, d_msgs, capacity);
 }
 
 int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
@@ -633,6 +1231,9 @@ int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_
     if (capacity > 0xFFFFFFFFull) capacity = 0xFFFFFFFFull;
     hipStream_t s = h->stream;
     *n_pairs = 0;
+    if (h->shard && !(h->radius > 0.0) && !h->shard_expanded)
+        return sharded_tick_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs,
+                                  capacity, n_pairs);
     if (!h->shard) {  // G = 1 without an exchange: the single-GPU tick, P read back
         int rc = launch_route(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs, capacity);
         if (rc) return rc;
@@ -650,59 +1251,72 @@ int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_
     const size_t M = n_msgs;
     int late = WQ_OK;  // a local failure, reported once the tick's exchanges are complete
     std::string late_msg;
+    auto fail = [&](int code) {
+        if (code && !late) {
+            late = code;
+            late_msg = h->err;
+        }
+        return code;
+    };
     uint64_t R = 0;
     SegBounds seg;
     int rc = shard_exchange_route(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, &R, &seg, &late, &late_msg);
     if (rc) return rc;
-    std::vector<size_t> eight(G, 8);
-    // 4. per-record counts, per-source pair counts, exchanged
-    WQ_ALLOC(h, sc.own_e, (R ? R : 1) * 4);
-    WQ_ALLOC(h, sc.pc, 2 * G * 8 + sizeof(wq_route_counters));
-    uint64_t* pc_send = sc.pc.as<uint64_t>();
-    uint64_t* pc_recv = pc_send + G;
-    wq_route_counters* cnt_copy = reinterpret_cast<wq_route_counters*>(pc_recv + G);
-    hipLaunchKernelGGL(k_owner_counts, dim3((unsigned)((R + kBlock - 1) / kBlock) + 1), dim3(kBlock), 0, s,
-                       sc.own_off.as<uint32_t>(), (uint32_t)R, seg, G, sc.own_e.as<uint32_t>(), pc_send);
-    WQ_HIP(h, hipGetLastError());
-    if (!late && R) WQ_HIP(h, hipMemcpyAsync(cnt_copy, h->rws.last, sizeof(wq_route_counters), hipMemcpyDeviceToDevice, s));
-    else WQ_HIP(h, hipMemsetAsync(cnt_copy, 0, sizeof(wq_route_counters), s));
+    std::vector<size_t> sixteen(G, 16);
+    // 4. per-record counts; per source {pair count, status}, exchanged before any pair moves
+    unsigned long long* pc_send = reinterpret_cast<unsigned long long*>(sc.small.as<char>() + kSmallC);
+    unsigned long long* pc_recv = pc_send + 2 * G;
+    if (!late) {
+        hipLaunchKernelGGL(k_owner_counts, dim3((unsigned)((R + kBlock - 1) / kBlock) + 1), dim3(kBlock), 0, s,
+                           sc.own_off.as<uint32_t>(), (uint32_t)R, seg, G, sc.own_e.as<uint32_t>(), pc_send,
+                           R ? h->rws.last : nullptr, h->tab.stale.as<uint32_t>());
+        if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "owner counts launch"));
+    }
+    if (late) {
+        std::vector<unsigned long long> v(2 * G, 0);
+        for (uint32_t d = 0; d < G; ++d) v[2 * d + 1] = status_of(late);
+        WQ_HIP(h, hipMemcpyAsync(pc_send, v.data(), 16 * G, hipMemcpyHostToDevice, s));
+    }
     {
-        Xfer x{{pc_send}, {eight.data()}, {pc_recv}, {eight.data()}, 1};
+        Xfer x{{pc_send}, {sixteen.data()}, {pc_recv}, {sixteen.data()}, 1};
         if ((rc = exchange(h, x))) return rc;
     }
-    std::vector<uint64_t> hp(2 * G + 3);
-    WQ_HIP(h, hipMemcpyAsync(hp.data(), pc_send, 2 * G * 8 + sizeof(wq_route_counters), hipMemcpyDeviceToHost, s));
+    std::vector<unsigned long long> hp(4 * G);
+    WQ_HIP(h, hipMemcpyAsync(hp.data(), pc_send, 32 * G, hipMemcpyDeviceToHost, s));
     WQ_HIP(h, hipStreamSynchronize(s));  // host read 2
-    wq_route_counters oc;
-    memcpy(&oc, hp.data() + 2 * G, sizeof(oc));
-    if (!late && oc.error) {
-        late = (oc.error & 4u) ? WQ_E_TIMEOUT : WQ_E_CAPACITY;
-        late_msg = (oc.error & 4u) ? "owner route: look-back spin gave up" : "owner route: more than 2^32-1 pairs";
+    uint64_t peer_status = 0, P_own = 0;
+    uint32_t peer_from = 0;
+    for (uint32_t d = 0; d < G; ++d) {
+        P_own += hp[2 * d];
+        const uint64_t st = hp[2 * G + 2 * d + 1];
+        if (st && !peer_status) {
+            peer_status = st;
+            peer_from = d;
+        }
     }
-    const uint64_t P_own = R ? oc.n_pairs : 0;
     if (!late && P_own > sc.own_cap) {  // the pair buffer was short: offsets are right, route again
         sc.own_cap = P_own + P_own / 4 + 4096;
         if (sc.own_cap > 0xFFFFFFFFull) sc.own_cap = 0xFFFFFFFFull;
-        WQ_ALLOC(h, sc.own_peers, sc.own_cap * 4);
-        rc = launch_route_records(h, sc.recv.as<wq_msg_rec>(), R, sc.own_off.as<uint32_t>(),
-                                  sc.own_peers.as<uint32_t>(), nullptr, sc.own_cap);
-        if (rc) {
-            late = rc;
-            late_msg = h->err;
-        }
+        // the sizes are promised: a shard that cannot keep the promise breaks the collective
+        if (sc.own_peers.ensure(sc.own_cap * 4) != hipSuccess) return fatal_receive(h, "hipMalloc of the owner's pairs");
+        if ((rc = launch_route_records(h, sc.recv.as<wq_msg_rec>(), R, sc.own_off.as<uint32_t>(),
+                                       sc.own_peers.as<uint32_t>(), nullptr, sc.own_cap)))
+            return fatal_receive(h, "owner re-route");
     }
-    // 5. recipient counts and peers back to the ingesting shards (one exchange group)
+    // 5. recipient counts and peers back to the ingesting shards (one exchange group); a shard whose
+    // local step failed sends none of either, as its status said
     std::vector<size_t> eb_s(G), eb_r(G), pb_s(G), pb_r(G);
     uint64_t P = 0;
     for (uint32_t d = 0; d < G; ++d) {
-        eb_s[d] = (size_t)sc.rc[d] * 4;  // to source d: e of the records it sent here
-        eb_r[d] = (size_t)sc.sc[d] * 4;  // from owner d: e of the records sent there
-        pb_s[d] = (size_t)hp[d] * 4;
-        pb_r[d] = (size_t)hp[G + d] * 4;
-        P += hp[G + d];
+        const bool d_failed = (uint32_t)hp[2 * G + 2 * d + 1] != 0;
+        eb_s[d] = late ? 0 : (size_t)sc.rc[d] * 4;      // to source d: e of the records it sent here
+        eb_r[d] = d_failed ? 0 : (size_t)sc.sc[d] * 4;  // from owner d: e of the records sent there
+        pb_s[d] = (size_t)hp[2 * d] * 4;
+        pb_r[d] = (size_t)hp[2 * G + 2 * d] * 4;
+        P += hp[2 * G + 2 * d];
     }
-    WQ_ALLOC(h, sc.ret_e, (M ? M : 1) * 4);
-    WQ_ALLOC(h, sc.ret_peers, (P ? P : 1) * 4);
+    if (sc.ret_e.ensure((M ? M : 1) * 4) != hipSuccess || sc.ret_peers.ensure((P ? P : 1) * 4) != hipSuccess)
+        return fatal_receive(h, "hipMalloc of the returned pairs");
     {
         Xfer x{{sc.own_e.p, sc.own_peers.p}, {eb_s.data(), pb_s.data()}, {sc.ret_e.p, sc.ret_peers.p},
                {eb_r.data(), pb_r.data()}, 2};
@@ -713,6 +1327,7 @@ int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_
         h->err = late_msg;
         return late;
     }
+    if (peer_status) return status_error(h, peer_status, peer_from);
     *n_pairs = P;
     if (P > 0xFFFFFFFFull) return set_error(h, WQ_E_CAPACITY, "more than 2^32-1 pairs in one tick");
     // 6. unshard into the caller's CSR, message order
@@ -773,6 +1388,25 @@ int wq_sharded_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, ui
     if (!h->shard || !h->shard->last_ready) return set_error(h, WQ_E_INVALID, "no sharded tick to copy out");
     WQ_HIP(h, hipSetDevice(h->device));
     return copy_out(h, d_offsets, d_peers, d_msgs, capacity > 0xFFFFFFFFull ? 0xFFFFFFFFull : capacity);
+}
+
+int wq_shard_last_bytes(wq_router* h, uint64_t* sent, uint64_t* received) {
+    if (!h || !sent || !received) return WQ_E_INVALID;
+    *sent = h->shard ? h->shard->last_sent : 0;
+    *received = h->shard ? h->shard->last_recv : 0;
+    return WQ_OK;
+}
+
+int wq_debug_inject_shard_failure(wq_router* h, int step) {
+    if (!h || step < 0 || step > 3) return WQ_E_INVALID;
+    h->shard_inject = step;
+    return WQ_OK;
+}
+
+int wq_debug_set_shard_form(wq_router* h, int expanded) {
+    if (!h) return WQ_E_INVALID;
+    h->shard_expanded = expanded != 0;
+    return WQ_OK;
 }
 
 }  // extern "C"

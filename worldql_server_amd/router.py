@@ -99,6 +99,9 @@ def load_library(build_if_missing: bool = True):
         "wq_sharded_route_tick_device": ([vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, ctypes.POINTER(sz)], i32),
         "wq_sharded_copy_out": ([vp, vp, vp, vp, sz], i32),
         "wq_sharded_route_owner_device": ([vp, vp, vp, vp, vp, vp, sz, ctypes.POINTER(abi.OwnerView)], i32),
+        "wq_shard_last_bytes": ([vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], i32),
+        "wq_debug_set_shard_form": ([vp, i32], i32),
+        "wq_debug_inject_shard_failure": ([vp, i32], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -357,6 +360,21 @@ class Router:
 
     def sharded_copy_out(self, offsets_ptr, peers_ptr, msgs_ptr, capacity) -> None:
         self._check(self.lib.wq_sharded_copy_out(self.h, offsets_ptr, peers_ptr or None, msgs_ptr or None, capacity))
+
+    def shard_last_bytes(self):
+        """(bytes sent to, bytes received from) OTHER shards in this shard's latest sharded tick."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self.lib.wq_shard_last_bytes(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def inject_shard_failure(self, step: int) -> None:
+        """Test hook: the next sharded tick fails locally at step 1 or 3 (wq_debug_inject_shard_failure)."""
+        self._check(self.lib.wq_debug_inject_shard_failure(self.h, step))
+
+    def set_shard_form(self, expanded: bool) -> None:
+        """True: the sharded tick returns expanded (message, peer) pairs (the radius filter's form);
+        False (default): row references + one pool of cube lists per destination."""
+        self._check(self.lib.wq_debug_set_shard_form(self.h, int(expanded)))
 
     # ---- C5 radius filter (include/wq_router.h) ----
     def set_peer_positions(self, pos) -> None:
