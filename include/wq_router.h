@@ -97,6 +97,22 @@ int wq_host_free(void* p);
 
 /* ---- lifetime: replaces WorldMap::new (world_map.rs:17-22) ---- */
 int wq_router_create(uint16_t cube_size, int device, wq_router** out);
+/* The same table over n_gpus GPUs behind ONE handle (SURVEY.md §8(b) wq_router_create(cube_size,
+ * n_gpus, devices, out)); the reference's single owner (thread.rs:119) keeps its one WorldMap.
+ * Inside: one cube-hash shard per device (devices may repeat), attached to an in-process exchange,
+ * driven by one worker thread each; every call below gives the one-table result:
+ *   wq_apply_ops[_device], wq_remove_peers   the whole op stream to every shard (each keeps its cubes)
+ *   wq_route_tick[_device]                   the sharded tick over G slices of the messages, CSR
+ *                                            concatenated in message order (n_candidates = P)
+ *   wq_is_subscribed[_any], wq_world_peers,  shard answers combined (any-keys merged on devices[0])
+ *   wq_route_global[_device], wq_get_stats
+ *   wq_set_radius, wq_set_peer_positions[_device], wq_set_fanout_hint, wq_route_health: every shard
+ * Device-pointer calls take arrays on devices[0], ordered after the handle's stream (wq_set_stream),
+ * and are synchronous on return. The sharded entry points (wq_shard_*, wq_sharded_*) and the
+ * instrumentation hooks are for single-device handles. */
+int wq_router_create_multi(uint16_t cube_size, int n_gpus, const int* devices, wq_router** out);
+/* Shards behind a handle (1 for wq_router_create). */
+int wq_multi_info(wq_router* h, uint32_t* n_gpus);
 int wq_router_destroy(wq_router* h);
 const char* wq_last_error(const wq_router* h);
 /* Use the caller's HIP stream (hipStream_t as void*); NULL restores the handle's own stream. */

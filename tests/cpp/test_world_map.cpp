@@ -4,7 +4,9 @@
 // Built and run by tests/test_cpp_mirror.py (the run needs a gfx950 GPU; exit code 0 = pass).
 #include <cstdio>
 #include <cstdlib>
+#include <memory>
 #include <string>
+#include <vector>
 
 #include "world_map.hpp"
 
@@ -19,8 +21,14 @@ static int g_fail = 0;
         }                                                              \
     } while (0)
 
-static void area_subscriptions() {
-    WorldMap wm(16);
+// devs empty: one GPU (wq_router_create); else one handle over those devices (wq_router_create_multi)
+static WorldMap* make_map(const std::vector<int>& devs) {
+    return devs.empty() ? new WorldMap(16) : new WorldMap(16, devs);
+}
+
+static void area_subscriptions(const std::vector<int>& devs) {
+    std::unique_ptr<WorldMap> wmp(make_map(devs));
+    WorldMap& wm = *wmp;
     AreaMap& map = wm.get_mut("world");
     const uint32_t uuid = 7;
     const CubeArea cube_1{0, 0, 0}, cube_2{16, 16, 16};
@@ -54,10 +62,11 @@ static void area_subscriptions() {
     CHECK(!map.is_peer_subscribed(uuid, vec_1));
 }
 
-static void world_subscriptions() {
+static void world_subscriptions(const std::vector<int>& devs) {
     const uint32_t uuid_1 = 1, uuid_2 = 2;
     const CubeArea cube_1{0, 0, 0}, cube_2{16, 16, 16};
-    WorldMap wm(16);
+    std::unique_ptr<WorldMap> wmp(make_map(devs));
+    WorldMap& wm = *wmp;
     AreaMap& map = wm.get_mut("world");
     CHECK(!map.is_peer_subscribed_any(uuid_1));
     CHECK(!map.is_peer_subscribed_any(uuid_2));
@@ -82,6 +91,53 @@ static void world_subscriptions() {
     map.remove_peer(uuid_2);
     CHECK(!map.is_peer_subscribed_any(uuid_1));
     CHECK(!map.is_peer_subscribed_any(uuid_2));
+}
+
+// The batch path over the same map: messages to the neighbourhood of subscribed peers, every
+// replication mode, routed through wq_route_tick; per message the recipients must be what the
+// map's own membership queries say (get_subscribed_peers, then the replication filter).
+static void multi_route(const std::vector<int>& devs) {
+    std::unique_ptr<WorldMap> wmp(make_map(devs));
+    WorldMap& wm = *wmp;
+    AreaMap& map = wm.get_mut("world");
+    std::vector<wq_op> ops;
+    uint64_t x = 12345;
+    auto rnd = [&]() { x = x * 6364136223846793005ull + 1442695040888963407ull; return (double)(x >> 11) * 0x1p-53; };
+    for (uint32_t p = 0; p < 400; ++p)
+        for (int k = 0; k < 3; ++k) {
+            wq_op op{};
+            op.world = map.world_id();
+            op.peer = p;
+            op.kind = WQ_OP_SUBSCRIBE;
+            op.u.pos[0] = rnd() * 96 - 48, op.u.pos[1] = rnd() * 96 - 48, op.u.pos[2] = rnd() * 96 - 48;
+            ops.push_back(op);
+        }
+    wm.apply_ops(ops);
+    const size_t M = 3000;
+    std::vector<double> pos(3 * M);
+    std::vector<uint32_t> world(M, map.world_id()), sender(M);
+    std::vector<uint8_t> repl(M);
+    for (size_t i = 0; i < M; ++i) {
+        for (int d = 0; d < 3; ++d) pos[3 * i + d] = rnd() * 96 - 48;
+        sender[i] = (uint32_t)(rnd() * 400);
+        repl[i] = (uint8_t)(rnd() * 3);
+    }
+    WorldMap::Routed r = wm.route(pos, world, sender, repl);
+    CHECK(r.offsets.size() == M + 1 && r.offsets[M] == r.peers.size());
+    size_t bad = 0;
+    for (size_t i = 0; i < M && bad < 5; ++i) {
+        std::vector<uint32_t> want;
+        for (uint32_t p : map.get_subscribed_peers(Vector3{pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]})) {
+            const bool keep = repl[i] == WQ_REPL_INCLUDING_SELF ? true
+                              : repl[i] == WQ_REPL_ONLY_SELF    ? p == sender[i]
+                                                                : p != sender[i];
+            if (keep) want.push_back(p);
+        }
+        const std::vector<uint32_t> got(r.peers.begin() + r.offsets[i], r.peers.begin() + r.offsets[i + 1]);
+        if (got != want) ++bad;
+    }
+    CHECK(bad == 0);
+    CHECK(r.peers.size() > M);  // the neighbourhoods overlap: plenty of recipients
 }
 
 static void sanitize() {
@@ -118,8 +174,13 @@ int main(int argc, char** argv) {
         std::printf(g_fail ? "FAILED\n" : "host ok\n");
         return g_fail ? 1 : 0;
     }
-    area_subscriptions();
-    world_subscriptions();
+    // one GPU, then one handle over G = 1, 2, 3 shards (all on device 0 here)
+    const std::vector<std::vector<int>> configs = {{}, {0}, {0, 0}, {0, 0, 0}};
+    for (const auto& devs : configs) {
+        area_subscriptions(devs);
+        world_subscriptions(devs);
+        multi_route(devs);
+    }
     std::printf(g_fail ? "FAILED (%d)\n" : "ok\n", g_fail);
     return g_fail ? 1 : 0;
 }

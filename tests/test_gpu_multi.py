@@ -1,0 +1,121 @@
+"""One handle over G GPUs (wq_router_create_multi, csrc/wq_multi.hip) against the oracle: the
+reference keeps ONE WorldMap in one task (worldql_server/src/processing/thread.rs:119), and the
+multi handle must answer every call with that one table's result. G in {1, 2, 3} shards, all on
+cuda:0 here (the box has one GPU; devices may repeat)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from worldql_server_amd import abi, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _workload():
+    w = synth.uniform_box(31, 2500, 12000, 80.0, neighbourhood=True, repl_mode="mixed", n_worlds=3)
+    rng = np.random.default_rng(31)
+    un = w.ops[rng.choice(len(w.ops), 3000, replace=False)].copy()
+    un["kind"] = abi.OP_UNSUBSCRIBE
+    rm = abi.ops_array(np.full(30, abi.WORLD_INVALID, np.uint32), rng.choice(2500, 30, replace=False),
+                       np.full(30, abi.OP_REMOVE_PEER, np.uint8), pos=np.zeros((30, 3)))
+    return w, abi.concat_ops([un, rm])
+
+
+@pytest.mark.parametrize("G", [1, 2, 3])
+def test_multi_handle_is_one_table(G):
+    import torch
+    from worldql_server_amd.router import Router
+    w, churn = _workload()
+    M = len(w.world)
+    r = Router.multi(16, [0] * G)
+    assert r.n_gpus() == G
+    o = orc.COracle(16)
+    r.apply_ops(w.ops)
+    o.apply_ops(w.ops)
+    r.apply_ops(churn)
+    o.apply_ops(churn)
+    r.remove_peers(np.array([3, 4, 5], np.uint32))
+    o.apply_ops(abi.ops_array(np.full(3, abi.WORLD_INVALID, np.uint32), np.array([3, 4, 5]),
+                              np.full(3, abi.OP_REMOVE_PEER, np.uint8), pos=np.zeros((3, 3))))
+
+    # the hot path, host arrays (twice: the second reuses the shards' staging)
+    want_offs, want_peers, _ = o.route(w.pos, w.world, w.sender, w.repl)
+    for _ in range(2):
+        offs, peers, msgs = r.route(w.pos, w.world, w.sender, w.repl, with_msgs=True)
+        assert (offs == want_offs).all() and (peers == want_peers).all()
+        assert (msgs == np.repeat(np.arange(M, dtype=np.uint32), np.diff(want_offs.astype(np.int64)))).all()
+    # a capacity too small: WQ_E_CAPACITY with the size, then the retry inside route()
+    offs, peers, _ = r.route(w.pos, w.world, w.sender, w.repl, capacity=None)
+    assert (peers == want_peers).all()
+
+    # device pointers on devices[0]
+    dev = torch.device("cuda:0")
+    pos = torch.from_numpy(w.pos).to(dev)
+    wo = torch.from_numpy(w.world.view(np.int32)).to(dev)
+    se = torch.from_numpy(w.sender.view(np.int32)).to(dev)
+    rp = torch.from_numpy(w.repl).to(dev)
+    d_off = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    cap = len(want_peers) + 100
+    d_peers = torch.empty(cap, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    r.route_device(pos.data_ptr(), wo.data_ptr(), se.data_ptr(), rp.data_ptr(), M, d_off.data_ptr(), d_peers.data_ptr(),
+                   None, cap, cnt.data_ptr())
+    torch.cuda.synchronize()
+    c = cnt.cpu().numpy().view(abi.COUNTERS_DTYPE)[0]
+    assert int(c["n_pairs"]) == len(want_peers) and c["overflow"] == 0 and c["error"] == 0
+    assert (d_off.cpu().numpy().view(np.uint32) == want_offs).all()
+    assert (d_peers[:len(want_peers)].cpu().numpy().view(np.uint32) == want_peers).all()
+
+    # queries (area_map.rs:33-67)
+    idx = np.arange(0, len(w.ops), 37)
+    ops = w.ops[idx]
+    got = r.is_subscribed(ops["world"], ops["peer"], False, ops["pos"])
+    want = np.array([o.is_subscribed(int(x["world"]), int(x["peer"]), False, x["pos"]) for x in ops])
+    assert (got == want).all() and want.any() and not want.all()
+    peers_q = np.arange(0, 2500, 7, dtype=np.uint32)
+    for world in range(3):
+        got = r.is_subscribed_any(np.full(len(peers_q), world, np.uint32), peers_q)
+        want = np.array([o.is_subscribed_any(world, int(p)) for p in peers_q])
+        assert (got == want).all()
+        assert (r.world_peers(world) == o.world_peers(world)).all()
+    st = r.stats()
+    e, cubes = o.counts()
+    assert st["n_entries"] == e and st["n_cubes"] == cubes
+    assert st["n_any"] == sum(len(o.world_peers(x)) for x in range(3))
+
+    # GlobalMessage to a world (global_message.rs:36-84) on the merged any-keys
+    gw = np.array([0, 1, 2, 7, 1], np.uint32)
+    gs = np.array([10, 11, 12, 13, 6], np.uint32)
+    gr = np.array([0, 1, 2, 0, 2], np.uint8)
+    g_offs, g_peers, _ = r.route_global(gw, gs, gr)
+    wo_, wp_ = o.route_global(gw, gs, gr)
+    assert (g_offs == wo_).all() and (g_peers == wp_).all()
+
+    # after more ops the merged any-keys follow
+    more = abi.ops_array(np.zeros(5, np.uint32), np.arange(5000, 5005), np.zeros(5, np.uint8),
+                         pos=np.ones((5, 3)) * 7.0)
+    r.apply_ops(more)
+    o.apply_ops(more)
+    assert (r.world_peers(0) == o.world_peers(0)).all()
+    assert r.route_health()[0] == 0  # no error bits (overflow holds route()'s capacity retries)
+    r.close()
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_multi_handle_radius_filter(G):
+    """C5's exact radius filter through the multi handle: positions and radius go to every shard."""
+    from worldql_server_amd.router import Router
+    w = synth.uniform_box(33, 3000, 9000, 64.0, neighbourhood=True, repl_mode="mixed")
+    rng = np.random.default_rng(33)
+    peer_pos = rng.uniform(-64, 64, (3000, 3))
+    r = Router.multi(16, [0] * G)
+    r.apply_ops(w.ops)
+    r.set_peer_positions(peer_pos)
+    r.set_radius(14.0)
+    o = orc.COracle(16)
+    o.apply_ops(w.ops)
+    offs, peers, _ = r.route(w.pos, w.world, w.sender, w.repl)
+    wo_, wp_ = o.route_radius(w.pos, w.world, w.sender, w.repl, peer_pos, 14.0)[:2]
+    assert (offs == wo_).all() and (peers == wp_).all() and len(peers) > 0
+    r.close()

@@ -17,11 +17,11 @@ BUILD = os.path.join(PKG, "_build")
 LIB = os.path.join(PKG, "libwq_router.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["wq_route.hip", "wq_global.hip", "wq_query.hip", "wq_table.hip", "wq_delta.hip", "wq_shard.hip", "wq_sharded.hip", "wq_peers.hip", "wq_router.hip"]
+SOURCES = ["wq_route.hip", "wq_global.hip", "wq_query.hip", "wq_table.hip", "wq_delta.hip", "wq_shard.hip", "wq_sharded.hip", "wq_peers.hip", "wq_multi.hip", "wq_router.hip"]
 HOST_SOURCES = ["wq_codec.cpp"]
 CXX = os.environ.get("CXX", "g++")
 HOST_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-pthread", "-Wall"]
-HEADERS = ["lane_xchg.hpp", "wq_device.hpp", "wq_internal.hpp", "route_common.hpp", "route_count.hpp", "route_scan.hpp", "route_emit.hpp", "route_tick.hpp", "route_radius.hpp", "route_spill.hpp", "table_prims.hpp"]
+HEADERS = ["lane_xchg.hpp", "wq_device.hpp", "wq_internal.hpp", "route_common.hpp", "route_count.hpp", "route_scan.hpp", "route_emit.hpp", "route_tick.hpp", "route_radius.hpp", "route_spill.hpp", "route_gather.hpp", "table_prims.hpp"]
 # No fast-math and no FMA contraction: coord_clamp must reproduce Rust's f64 op sequence.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
          "-fno-fast-math", "-Wall", "-Wno-unused-function", "-Wno-unused-result"]

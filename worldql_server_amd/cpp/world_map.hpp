@@ -101,6 +101,11 @@ class WorldMap {
         int rc = wq_router_create(cube_size, device, &h_);
         if (rc) throw Error(rc, std::string("wq_router_create: ") + wq_last_error(nullptr));
     }
+    // The same map over several GPUs behind one handle (wq_router_create_multi; devices may repeat).
+    WorldMap(uint16_t cube_size, const std::vector<int>& devices) {
+        int rc = wq_router_create_multi(cube_size, (int)devices.size(), devices.data(), &h_);
+        if (rc) throw Error(rc, std::string("wq_router_create_multi: ") + wq_last_error(nullptr));
+    }
     ~WorldMap() {
         for (auto& kv : maps_) delete kv.second;
         if (h_) wq_router_destroy(h_);

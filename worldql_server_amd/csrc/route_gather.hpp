@@ -4,23 +4,32 @@
 // owner ships to another GPU, as a row descriptor {len, skip, pointer}: output word k of the row
 // is src[k + (k >= skip)] — the cube's list or a record's inline peers with the sender's own
 // entry skipped (ExceptSelf), a list copied into a received pool, or the sender itself
-// (OnlySelf). gather_rows_kernel writes rows i = 0 .. n-1 at out[start[i] ..) with the owner-map
-// windows of emit_map_kernel (route_emit.hpp): per block 256 rows; each row marks where its range
-// enters a window of W = R * 256 outputs in a u16 map, a block-wide max-scan carries each owner
-// over its outputs, and thread t writes outputs t, t + 256, ... (one contiguous 256-word run per
-// store instruction), so the stores stream whatever the row lengths.
+// (OnlySelf). gather_rows_kernel writes rows i = 0 .. n-1 contiguously with the owner-map windows
+// of emit_map_kernel (route_emit.hpp): per block 256 rows; each row marks where its range enters a
+// window of W = R * 256 outputs in a u16 map, a block-wide max-scan carries each owner over its
+// outputs, and thread t writes outputs t, t + 256, ... (one contiguous 256-word run per store
+// instruction), so the stores stream whatever the row lengths. Two ways to place the rows:
+//   CSR = false  row i at start[i] (an exclusive prefix with start[n] = total; its length is
+//                start[i + 1] - start[i], so rows of length 0 need no descriptor at all);
+//   CSR = true   the message-major CSR: row lengths e[i], the block's first output from the tile
+//                scan of the per-256-row totals (route_scan.hpp), the in-block prefix by a row
+//                scan; the kernel writes offsets[i] as well (offsets[n] comes from the tile scan).
 #pragma once
 #include "route_common.hpp"
 
 namespace wq {
 
 struct GatherParams {
-    const uint32_t* start;  // exclusive prefix of the row lengths, n + 1 entries (start[n] = total)
+    const uint32_t* start;  // CSR = false: exclusive prefix of the row lengths, n + 1 entries
     const uint4* desc;      // {len, skip (kNone: none), pointer lo, pointer hi} per row
     uint32_t n;
     uint32_t* out;
     uint32_t* out_row;      // nullable: the row index of every output word (the CSR's msgs[])
     uint64_t capacity;      // outputs at or beyond it are not written
+    // CSR = true
+    const uint32_t* e = nullptr;            // row lengths
+    const uint32_t* tile_prefix = nullptr;  // exclusive prefix of the 256-row totals
+    uint32_t* offsets = nullptr;            // out: offsets[0 .. n)
 };
 
 template <int R>
@@ -28,9 +37,26 @@ struct GatherSmem {
     alignas(16) uint4 desc[kBlock];
     alignas(16) uint16_t map[R * kBlock];
     uint32_t wave_max[kWaves];
+    uint32_t wave_tot[kWaves];
 };
 
-template <int R>
+// Per-256-row totals of e (the tile scan's input), for gather_rows_kernel<R, true>.
+__global__ __launch_bounds__(kBlock) void row_tile_sums_kernel(const uint32_t* __restrict__ e, uint32_t n,
+                                                               uint32_t* __restrict__ tile_total) {
+    __shared__ uint64_t part[kWaves];
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t s = wave_sum_u64(i < n ? e[i] : 0u);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) t += part[w];
+        tile_total[blockIdx.x] = t > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)t;
+    }
+}
+
+template <int R, bool CSR = false>
 __global__ __launch_bounds__(kBlock) void gather_rows_kernel(GatherParams p) {
     static_assert(R % 8 == 0, "map rows of whole 16-byte words");
     constexpr uint32_t W = R * kBlock;
@@ -38,13 +64,33 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(GatherParams p) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t i0 = blockIdx.x * kBlock;
     const uint32_t i = i0 + tid;
-    const uint32_t g = p.start[i0];
-    const uint32_t T = p.start[i0 + kBlock < p.n ? i0 + kBlock : p.n] - g;
-    if (T == 0) return;  // block-uniform
-    const uint4 d = i < p.n ? p.desc[i] : make_uint4(0, kNone, 0, 0);
-    const uint32_t e = d.x;
-    const uint32_t st = i < p.n ? p.start[i] - g : T;
-    sm.desc[tid] = make_uint4(st, d.y, d.z, d.w);
+    uint32_t g, T, e, st;
+    // the descriptor is loaded first, so its latency hides behind the row scan
+    const uint4 d0 = i < p.n ? p.desc[i] : make_uint4(0, kNone, 0, 0);
+    if (CSR) {
+        e = i < p.n ? p.e[i] : 0u;
+        const uint32_t incl = wave_incl_scan_add(e, lane);
+        if (lane == 63) sm.wave_tot[wave] = incl;
+        lds_barrier();
+        uint32_t before = 0;
+        T = 0;
+#pragma unroll
+        for (int u = 0; u < kWaves; ++u) {
+            const uint32_t t = sm.wave_tot[u];
+            if (u < wave) before += t;
+            T += t;
+        }
+        st = before + incl - e;
+        g = p.tile_prefix[blockIdx.x];
+        if (i < p.n) p.offsets[i] = g + st;
+    } else {
+        g = p.start[i0];
+        T = p.start[i0 + kBlock < p.n ? i0 + kBlock : p.n] - g;
+        e = i < p.n ? p.start[i + 1] - p.start[i] : 0u;
+        st = i < p.n ? p.start[i] - g : T;
+    }
+    if (T == 0 || !p.out) return;  // block-uniform
+    sm.desc[tid] = make_uint4(st, d0.y, d0.z, d0.w);  // (rows of length 0 are never read)
     uint4* my_map = reinterpret_cast<uint4*>(sm.map) + tid * (R / 8);
     for (uint32_t w0 = 0; w0 < T; w0 += W) {
 #pragma unroll

@@ -114,6 +114,7 @@ struct ProfileEvents {
 };
 
 struct ShardCtx;  // wq_sharded.hip: the exchange a sharded tick uses, and its workspace
+struct MultiCtx;  // wq_multi.hip: a handle over G GPUs (wq_router_create_multi)
 
 }  // namespace wq
 
@@ -163,6 +164,7 @@ struct wq_router {
     wq::ShardCtx* shard = nullptr;  // wq_shard_attach_*: this handle is one shard of G
     bool shard_expanded = false;    // wq_debug_set_shard_form: expanded pairs back instead of row references
     int shard_inject = 0;           // wq_debug_inject_shard_failure: fail the next sharded tick's step 1 or 3
+    wq::MultiCtx* multi = nullptr;  // wq_router_create_multi: this handle drives G shard handles
 };
 
 namespace wq {
@@ -221,6 +223,22 @@ int table_ensure_any(wq_router* h);
 int set_error(wq_router* h, int code, const char* what, hipError_t e = hipSuccess);
 // wq_sharded.hip: frees the exchange and its workspace (destroys an RCCL communicator).
 void shard_release(wq_router* h);
+// wq_multi.hip: the multi-GPU handle's side of the entry points (h->multi != nullptr)
+int multi_merge_any(wq_router* h);
+int multi_apply_ops(wq_router* h, const wq_op* ops, size_t n);
+int multi_apply_ops_device(wq_router* h, const wq_op* d_ops, size_t n);
+int multi_remove_peers(wq_router* h, const uint32_t* peers, size_t n);
+int multi_route_tick(wq_router* h, const double* pos, const int64_t* keys, const uint32_t* world,
+                     const uint32_t* sender, const uint8_t* repl, size_t M, uint32_t* offsets, uint32_t* peers,
+                     uint32_t* msgs, size_t capacity, size_t* n_pairs, bool on_device);
+int multi_is_subscribed(wq_router* h, size_t n, const uint32_t* world, const uint32_t* peer, int raw,
+                        const void* kp, uint8_t* out);
+int multi_stats(wq_router* h, wq_stats* out);
+int multi_health(wq_router* h, uint32_t* error_bits, uint32_t* overflow);
+int multi_set_positions(wq_router* h, const double* pos, size_t n, bool on_device);
+int multi_set_radius(wq_router* h, double radius);
+int multi_set_hint(wq_router* h, double pairs_per_message);
+void multi_release(wq_router* h);
 }  // namespace wq
 
 #define WQ_HIP(h, call)                                                    \

@@ -128,6 +128,7 @@ int wq_router_create(uint16_t cube_size, int device, wq_router** out) {
 
 int wq_router_destroy(wq_router* h) {
     if (!h) return WQ_E_INVALID;
+    multi_release(h);
     (void)hipSetDevice(h->device);
     (void)hipStreamSynchronize(h->stream);
     shard_release(h);
@@ -162,6 +163,7 @@ int wq_set_stream(wq_router* h, void* stream) {
 int wq_get_stats(wq_router* h, wq_stats* out) {
     if (!h || !out) return WQ_E_INVALID;
     WQ_HIP(h, hipSetDevice(h->device));
+    if (h->multi) return multi_stats(h, out);
     int rc = table_ensure_any(h);
     if (rc) return rc;
     if ((rc = table_sync_delta_stats(h))) return rc;
@@ -195,6 +197,7 @@ static __global__ void k_pos_f32(const double* __restrict__ pos, uint64_t n, flo
 static int set_peer_positions(wq_router* h, const double* pos, size_t n, hipMemcpyKind kind) {
     if (!h || (n && !pos) || n > 0xFFFFFFFFull) return WQ_E_INVALID;
     WQ_HIP(h, hipSetDevice(h->device));
+    if (h->multi) return multi_set_positions(h, pos, n, kind == hipMemcpyDeviceToDevice);
     WQ_ALLOC(h, h->ppos, (n ? n : 1) * 24);
     WQ_ALLOC(h, h->ppos4, (n ? n : 1) * 16);
     const bool d2d = kind == hipMemcpyDeviceToDevice;
@@ -221,11 +224,13 @@ int wq_set_peer_positions_device(wq_router* h, const double* d_pos, size_t n_pee
 int wq_set_radius(wq_router* h, double radius) {
     if (!h) return WQ_E_INVALID;
     h->radius = (radius > 0.0) ? radius : 0.0;  // NaN compares false: off
+    if (h->multi) return multi_set_radius(h, radius);
     return WQ_OK;
 }
 
 int wq_set_fanout_hint(wq_router* h, double pairs_per_message) {
     if (!h) return WQ_E_INVALID;
+    if (h->multi) return multi_set_hint(h, pairs_per_message);
     if (!(pairs_per_message >= 0.0)) {  // negative or NaN: back to the automatic choice
         h->fanout_auto = true;
         return WQ_OK;
@@ -247,7 +252,10 @@ int wq_route_health(wq_router* h, uint32_t* error_bits, uint32_t* overflow) {
     WQ_HIP(h, hipSetDevice(h->device));
     *error_bits = 0;
     *overflow = 0;
-    if (!h->rws.buf.p) return WQ_OK;  // no route call yet
+    if (h->multi) {
+        if (int rc = multi_health(h, error_bits, overflow)) return rc;
+    }
+    if (!h->rws.buf.p) return WQ_OK;  // no route call yet (the multi handle's own: global routes)
     uint32_t w[2];
     WQ_HIP(h, hipMemcpyAsync(w, h->rws.buf.p, 8, hipMemcpyDeviceToHost, h->stream));
     WQ_HIP(h, hipMemsetAsync(h->rws.buf.p, 0, 8, h->stream));
@@ -299,6 +307,7 @@ int wq_apply_ops(wq_router* h, const wq_op* ops, size_t n) {
         if (ops[i].kind > WQ_OP_REMOVE_PEER ||
             (ops[i].kind != WQ_OP_REMOVE_PEER && ops[i].world == WQ_WORLD_INVALID))
             return set_error(h, WQ_E_INVALID, "bad op (kind or reserved world id)");
+    if (h->multi) return multi_apply_ops(h, ops, n);
     // Split at REMOVE_PEER runs so the reference's sequential order is kept (thread.rs:122-146).
     size_t i = 0;
     std::vector<uint64_t> rm;
@@ -325,12 +334,14 @@ int wq_apply_ops(wq_router* h, const wq_op* ops, size_t n) {
 int wq_apply_ops_device(wq_router* h, const wq_op* d_ops, size_t n) {
     if (!h || (n && !d_ops)) return WQ_E_INVALID;
     WQ_HIP(h, hipSetDevice(h->device));
+    if (h->multi) return multi_apply_ops_device(h, d_ops, n);
     return table_apply_segment(h, d_ops, n, true);
 }
 
 int wq_remove_peers(wq_router* h, const uint32_t* peers, size_t n) {
     if (!h || (n && !peers)) return WQ_E_INVALID;
     WQ_HIP(h, hipSetDevice(h->device));
+    if (h->multi) return multi_remove_peers(h, peers, n);
     std::vector<uint64_t> rm(n);
     for (size_t i = 0; i < n; ++i) rm[i] = ((uint64_t)WQ_WORLD_INVALID << 32) | peers[i];
     std::sort(rm.begin(), rm.end());
@@ -347,6 +358,17 @@ int wq_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_key
     if (n_msgs >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
     if (capacity > 0xFFFFFFFFull) capacity = 0xFFFFFFFFull;  // u32 CSR offsets
     WQ_HIP(h, hipSetDevice(h->device));
+    if (h->multi) {
+        size_t P = 0;
+        const int rc = multi_route_tick(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs,
+                                        capacity, &P, true);
+        if ((rc == WQ_OK || rc == WQ_E_CAPACITY) && d_counters) {  // P (F reported as P), overflow
+            wq_route_counters c{P, P, P > capacity ? 1u : 0u, 0u};
+            WQ_HIP(h, hipMemcpyAsync(d_counters, &c, sizeof(c), hipMemcpyHostToDevice, h->stream));
+            WQ_HIP(h, hipStreamSynchronize(h->stream));
+        }
+        return rc == WQ_E_CAPACITY ? WQ_OK : rc;  // as the single-GPU form: the counters report overflow
+    }
     int rc = launch_route(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs, capacity);
     if (rc) return rc;
     if (d_counters)
@@ -362,6 +384,11 @@ int wq_route_tick(wq_router* h, const double* pos, const int64_t* keys, const ui
         (capacity && !peers))
         return WQ_E_INVALID;
     WQ_HIP(h, hipSetDevice(h->device));
+    if (h->multi) {
+        if (M >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
+        return multi_route_tick(h, pos, keys, world, sender, repl, M, offsets, peers, msgs,
+                                std::min<size_t>(capacity, 0xFFFFFFFFull), n_pairs, false);
+    }
     const size_t b_pos = keys ? M * 24 : (pos ? M * 24 : 0);
     const size_t o_pos = 0, o_w = align256(o_pos + b_pos), o_s = align256(o_w + M * 4),
                  o_r = align256(o_s + M * 4), n_in = align256(o_r + M + 1);
@@ -402,7 +429,7 @@ int wq_route_global_device(wq_router* h, const uint32_t* d_world, const uint32_t
     if (n_msgs >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
     if (capacity > 0xFFFFFFFFull) capacity = 0xFFFFFFFFull;
     WQ_HIP(h, hipSetDevice(h->device));
-    int rc = table_ensure_any(h);
+    int rc = h->multi ? multi_merge_any(h) : table_ensure_any(h);
     if (rc) return rc;
     rc = launch_route_global(h, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs, capacity);
     if (rc) return rc;
@@ -420,7 +447,7 @@ int wq_route_global(wq_router* h, const uint32_t* world, const uint32_t* sender,
     for (size_t i = 0; i < M; ++i)
         if (world[i] == WQ_WORLD_INVALID) return set_error(h, WQ_E_INVALID, "reserved world id in a GlobalMessage");
     WQ_HIP(h, hipSetDevice(h->device));
-    int rc0 = table_ensure_any(h);
+    int rc0 = h->multi ? multi_merge_any(h) : table_ensure_any(h);
     if (rc0) return rc0;
     const size_t o_w = 0, o_s = align256(M * 4), o_r = align256(o_s + M * 4), n_in = align256(o_r + M + 1);
     WQ_ALLOC(h, h->h_in, n_in);
@@ -503,6 +530,7 @@ int wq_is_subscribed(wq_router* h, size_t n, const uint32_t* world, const uint32
     if (n == 0) return WQ_OK;
     if (n >= 0xFFFFFFFFull) return WQ_E_INVALID;
     WQ_HIP(h, hipSetDevice(h->device));
+    if (h->multi) return multi_is_subscribed(h, n, world, peer, key_is_raw, key_or_pos, out);
     if (int rc0 = table_resolve(h, true)) return rc0;
     const size_t o_w = 0, o_p = align256(n * 4), o_k = align256(o_p + n * 4), o_o = align256(o_k + n * 24);
     WQ_ALLOC(h, h->h_in, o_o + n);
@@ -524,7 +552,7 @@ int wq_is_subscribed_any(wq_router* h, size_t n, const uint32_t* world, const ui
     if (n == 0) return WQ_OK;
     if (n >= 0xFFFFFFFFull) return WQ_E_INVALID;
     WQ_HIP(h, hipSetDevice(h->device));
-    int rc0 = table_ensure_any(h);
+    int rc0 = h->multi ? multi_merge_any(h) : table_ensure_any(h);
     if (rc0) return rc0;
     const size_t o_w = 0, o_p = align256(n * 4), o_o = align256(o_p + n * 4);
     WQ_ALLOC(h, h->h_in, o_o + n);
@@ -543,7 +571,7 @@ int wq_is_subscribed_any(wq_router* h, size_t n, const uint32_t* world, const ui
 int wq_world_peers(wq_router* h, uint32_t world, uint32_t* out, size_t capacity, size_t* n_out) {
     if (!h || !n_out || (capacity && !out)) return WQ_E_INVALID;
     WQ_HIP(h, hipSetDevice(h->device));
-    int rc0 = table_ensure_any(h);
+    int rc0 = h->multi ? multi_merge_any(h) : table_ensure_any(h);
     if (rc0) return rc0;
     WQ_ALLOC(h, h->small, 64);
     hipStream_t s = h->stream;

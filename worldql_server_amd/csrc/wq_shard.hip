@@ -75,14 +75,28 @@ __global__ void __launch_bounds__(kBlock) shard_count_kernel(ShardIn in, uint32_
     for (uint32_t d = threadIdx.x; d < in.G; d += kBlock) cnt[d] = 0;
     __syncthreads();
     const uint32_t m0 = blockIdx.x * kShardTile + threadIdx.x;
+    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int i = 0; i < kShardIPT; ++i) {
         const uint32_t m = m0 + i * kBlock;
-        if (m < in.M) {
+        const bool valid = m < in.M;
+        uint32_t own = 0xFFFFFFFFu, wt = 0;
+        if (valid) {
             int64_t x, y, z;
             msg_key<RAW>(in, m, x, y, z);
             const uint32_t w = in.world[m];
-            atomicAdd(&cnt[shard_of(w, x, y, z, in.G)], msg_weight<RAW, COMPACT>(in, w, x, y, z));
+            own = shard_of(w, x, y, z, in.G);
+            wt = msg_weight<RAW, COMPACT>(in, w, x, y, z);
+        }
+        // one LDS add per distinct owner in the wave (G = 1: one per wave, not 64 on one word)
+        const uint64_t wide = __ballot(wt == 2);
+        uint64_t todo = __ballot(valid);
+        while (todo) {
+            const int leader = __ffsll((unsigned long long)todo) - 1;
+            const uint32_t d = __shfl(own, leader, 64);
+            const uint64_t mask = __ballot(own == d);
+            if (lane == leader) atomicAdd(&cnt[d], (uint32_t)(__popcll(mask) + __popcll(mask & wide)));
+            todo &= ~mask;
         }
     }
     __syncthreads();

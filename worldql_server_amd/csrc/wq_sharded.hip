@@ -38,6 +38,7 @@
 
 #include "route_count.hpp"
 #include "route_gather.hpp"
+#include "route_scan.hpp"
 
 namespace wq {
 int launch_shard_messages(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
@@ -151,11 +152,14 @@ constexpr int kXNone = 0, kXHub = 1, kXRccl = 2, kXCallback = 3;
 constexpr double kHubTimeoutS = 120.0;
 // The small exchange vectors (ShardCtx::small, allocated at attach): the slot counts exchange
 // {slots, status} u32 x 2 per shard (send at kSmallA, receive after it), the pool-size exchange
-// {pool words, recipients, status, 0} u64 x 4 per shard (send at kSmallC, receive after it), and
-// the per-source recipient sums of the owner (u64 per shard at kSmallPairs).
-constexpr size_t kSmallA = 0, kSmallC = 1024, kSmallPairs = 6144, kSmallBytes = 8192;
-static_assert(kSmallA + 4 * WQ_MAX_SHARDS * 4 <= kSmallC && kSmallC + 8 * WQ_MAX_SHARDS * 8 <= kSmallPairs &&
-                  kSmallPairs + WQ_MAX_SHARDS * 8 <= kSmallBytes,
+// {pool words, recipients, status, 0} u64 x 4 per shard (send at kSmallC, receive after it), the
+// message-side counters of a slot tick (kSmallCnt), and the owner's per-source recipient sums, 64
+// partial words per source (kSmallPairs: blocks add to word blockIdx % 64 — one shared word would
+// take ~40k same-address atomics per C3 tick at ~90 per microsecond).
+constexpr size_t kSmallA = 0, kSmallC = 1024, kSmallCnt = 5120, kSmallPairs = 8192, kPairLanes = 64;
+constexpr size_t kSmallBytes = kSmallPairs + WQ_MAX_SHARDS * kPairLanes * 8;
+static_assert(kSmallA + 4 * WQ_MAX_SHARDS * 4 <= kSmallC && kSmallC + 8 * WQ_MAX_SHARDS * 8 <= kSmallCnt &&
+                  kSmallCnt + sizeof(wq_route_counters) <= kSmallPairs,
               "small exchange vector layout");
 
 }  // namespace
@@ -189,7 +193,7 @@ struct ShardCtx {
     std::vector<uint64_t> ps, pr;
     // workspace of the slot tick (compact slots out, row references + cube-list pools back)
     DevBuf slots, perm, rslots, ocnt, hslot, plen, poff, claim, lead, self_ref, ref_send, ref_recv, pool_send,
-        pool_recv, desc_fill, desc_msg, e_msg, self_w;
+        pool_recv, desc_fill, desc_msg, e_msg, self_w, mtiles;
     uint64_t claim_cap = 0;  // claim table entries (power of two); 0 = not allocated
     uint64_t ticks = 0;      // slot ticks run: the claim table's tag
     // bytes this shard sent to / received from OTHER shards in its latest tick (xGMI volume)
@@ -469,11 +473,17 @@ struct RefOwnerParams {
     uint32_t* cnt;         // per slot: the cube's peer count (OnlySelf: e)
     uint32_t* hslot;       // per slot: its claim slot
     uint32_t* plen;        // per slot: words it adds to its source's pool (R + 1 entries, last 0)
-    unsigned long long* seg_pairs;  // per source: recipients of its slots
+    unsigned long long* seg_pairs;  // per source: kPairLanes partial recipient sums
     const uint32_t* poff;  // exclusive scan of plen
     uint3* ref_send;       // references of the remote sources' slots (own segment left out)
-    uint3* self_ref;       // references of this shard's own slots
     uint4* desc_fill;      // pool rows: the claiming slot copies its cube's peers
+    // this shard's own slots resolve here, straight into the message-order descriptors
+    const uint32_t* perm;  // sent slot -> message (kNone: a tail)
+    uint32_t self_sent;    // first sent slot of this shard's own segment
+    const uint32_t* sender;
+    uint4* desc_msg;
+    uint32_t* e_msg;
+    uint32_t* self_w;
 };
 
 __device__ __forceinline__ uint32_t slot_cnt(const uint2 inf, uint32_t e, const uint32_t* list) {
@@ -482,9 +492,10 @@ __device__ __forceinline__ uint32_t slot_cnt(const uint2 inf, uint32_t e, const 
     return inf.y == kNone ? 0u : inf.y >> 24;  // inline record, or no subscriber at all
 }
 
-// (owner) per received slot: the cube's peer count, and for a remote source's slot the claim of its
-// (source, cube) pair — the first claimer ships the cube's peers in that source's pool, the others
-// point at them. Per-source recipient sums go to seg_pairs (LDS first, a few global atomics per block).
+// (owner, G > 1) per received slot: the cube's peer count, and for a remote source's slot the claim
+// of its (source, cube) pair — the first claimer ships the cube's peers in that source's pool, the
+// others point at them. Per-source recipient sums: LDS, then one global atomic per (block, source)
+// spread over kPairLanes words.
 __global__ __launch_bounds__(kBlock) void k_ref_claim(RefOwnerParams p) {
     __shared__ unsigned long long acc[WQ_MAX_SHARDS];
     const int tid = threadIdx.x;
@@ -524,7 +535,6 @@ __global__ __launch_bounds__(kBlock) void k_ref_claim(RefOwnerParams p) {
         p.plen[i] = leader ? cnt : 0u;
     }
     if (i == p.R) p.plen[i] = 0;
-    // per-source recipient sums
     const uint32_t s0 = __shfl(s, 0, 64);
     if (__all(i >= p.R || s == s0)) {
         const uint64_t w = wave_sum_u64(ei);
@@ -534,56 +544,79 @@ __global__ __launch_bounds__(kBlock) void k_ref_claim(RefOwnerParams p) {
     }
     __syncthreads();
     for (uint32_t d = tid; d < p.G; d += kBlock)
-        if (acc[d]) atomicAdd(p.seg_pairs + d, acc[d]);
+        if (acc[d]) atomicAdd(p.seg_pairs + d * kPairLanes + (blockIdx.x & (kPairLanes - 1)), acc[d]);
 }
 
-// (owner) per received slot: its reference (own slots: straight into the table; remote: into the
-// source's pool) and, for a claiming slot, the pool row copying its cube's peers.
+// The row of a slot from its count-pass locator: kind, source offset (list word / record slot) and
+// skipped index (local_message.rs:60-86 as finish_message encoded it).
+__device__ __forceinline__ void slot_row(const uint2 inf, uint32_t* kind, uint32_t* off, uint32_t* skip) {
+    *kind = kRefSelf;
+    *off = 0;
+    *skip = kRefSkipNone;
+    if (inf.x & kLocSelf) return;
+    if (inf.x & kLocGlobal) {
+        *kind = kRefList;
+        *off = (inf.x & ~kLocGlobal) + 1;
+        *skip = inf.y == kNone ? kRefSkipNone : inf.y;
+    } else if (inf.y != kNone) {
+        *kind = kRefInline;
+        *off = inf.x;
+        const uint32_t s24 = inf.y & kSkipNone24;
+        *skip = s24 == kSkipNone24 ? kRefSkipNone : s24;
+    }  // else: no subscriber — an empty SELF row
+}
+
+__device__ __forceinline__ const uint32_t* row_src(uint32_t kind, uint32_t off, const uint32_t* list, const Record* recs) {
+    return kind == kRefList ? list + off : reinterpret_cast<const uint32_t*>(recs) + ((uint64_t)off * 32 + kInlineWord0);
+}
+
+__device__ __forceinline__ void put_desc(uint4* desc_msg, uint32_t* e_msg, uint32_t m, uint32_t e, uint32_t skip,
+                                         const uint32_t* src) {
+    const uint64_t a = reinterpret_cast<uint64_t>(src);
+    desc_msg[m] = make_uint4(e, skip, (uint32_t)a, (uint32_t)(a >> 32));
+    e_msg[m] = e;
+}
+
+// (owner) per received slot: this shard's own slots resolve at once into their messages'
+// descriptors (pointers into the table); a remote source's slot becomes its reference into the
+// source's pool and, for the claiming slot, the pool row copying its cube's peers.
 __global__ __launch_bounds__(kBlock) void k_ref_make(RefOwnerParams p) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= p.R) return;
-    const uint32_t s = seg_find(p.seg, p.G, i);
+    const uint32_t s = p.G > 1 ? seg_find(p.seg, p.G, i) : 0u;
     const uint2 inf = p.info[i];
-    const uint32_t cnt = p.cnt[i];
-    uint32_t kind = kRefSelf, off = 0, skip = kRefSkipNone;
-    if (inf.x & kLocSelf) {
-        kind = kRefSelf;
-    } else if (inf.x & kLocGlobal) {
-        kind = kRefList;
-        off = (inf.x & ~kLocGlobal) + 1;
-        skip = inf.y == kNone ? kRefSkipNone : inf.y;
-    } else if (inf.y != kNone) {
-        kind = kRefInline;
-        off = inf.x;
-        const uint32_t s24 = inf.y & kSkipNone24;
-        skip = s24 == kSkipNone24 ? kRefSkipNone : s24;
-    }  // else: no subscriber — an empty SELF row
+    uint32_t kind, off, skip;
+    slot_row(inf, &kind, &off, &skip);
     if (s == p.me) {
-        p.self_ref[i - p.seg.b[s]] = make_uint3(off, cnt, (kind << 30) | skip);
-        p.desc_fill[i] = make_uint4(0, kNone, 0, 0);
+        const uint32_t m = p.perm[p.self_sent + (i - p.seg.b[s])];
+        if (m == kNone) return;  // a tail slot
+        const uint32_t e = p.e[i];
+        if (kind == kRefSelf) {
+            if (e) p.self_w[m] = p.sender[m];
+            put_desc(p.desc_msg, p.e_msg, m, e, kNone, p.self_w + m);
+        } else {
+            put_desc(p.desc_msg, p.e_msg, m, e, skip == kRefSkipNone ? kNone : skip, row_src(kind, off, p.list, p.recs));
+        }
         return;
     }
-    uint4 fill = make_uint4(0, kNone, 0, 0);
+    const uint32_t cnt = p.cnt[i];
     uint3 ref;
     if (kind == kRefList || kind == kRefInline) {
         const uint32_t j = p.lead[p.hslot[i]];
         ref = make_uint3(p.poff[j] - p.poff[p.seg.b[s]], cnt, (kRefPool << 30) | skip);
         if (j == i) {
-            const uint32_t* src = kind == kRefList ? p.list + off
-                                                   : reinterpret_cast<const uint32_t*>(p.recs) + ((uint64_t)off * 32 + kInlineWord0);
-            const uint64_t a = reinterpret_cast<uint64_t>(src);
-            fill = make_uint4(cnt, kNone, (uint32_t)a, (uint32_t)(a >> 32));
+            const uint64_t a = reinterpret_cast<uint64_t>(row_src(kind, off, p.list, p.recs));
+            p.desc_fill[i] = make_uint4(cnt, kNone, (uint32_t)a, (uint32_t)(a >> 32));
         }
     } else {
         ref = make_uint3(0, cnt, (kRefSelf << 30) | kRefSkipNone);
     }
-    p.desc_fill[i] = fill;
     const uint32_t a = p.seg.b[p.me], nself = p.seg.b[p.me + 1] - a;
     p.ref_send[i < a ? i : i - nself] = ref;
 }
 
-// (owner) the per-destination words of the pool-size exchange: {pool words, recipients, status, 0}.
-// status = error bits of the count pass (2: > 2^32 pairs in a block, 8: stale table) << 32.
+// (owner, G > 1) the per-destination words of the pool-size exchange: {pool words, recipients,
+// status, 0}. status = error bits of the count pass (2: > 2^32 pairs in a block, 8: stale table) << 32.
 __global__ void k_ref_sizes(const uint32_t* __restrict__ poff, SegBounds seg, uint32_t G, uint32_t me,
                             const unsigned long long* __restrict__ seg_pairs, const wq_route_counters* __restrict__ cnt,
                             const uint32_t* __restrict__ stale, unsigned long long* __restrict__ out) {
@@ -591,8 +624,10 @@ __global__ void k_ref_sizes(const uint32_t* __restrict__ poff, SegBounds seg, ui
     if (d >= G) return;
     uint32_t err = cnt->error;
     if (stale && *stale) err |= kErrStale;
-    out[4 * d] = d == me ? 0ull : (unsigned long long)(poff[seg.b[d + 1]] - poff[seg.b[d]]);
-    out[4 * d + 1] = seg_pairs[d];
+    unsigned long long pairs = 0;
+    for (uint32_t k = 0; k < kPairLanes; ++k) pairs += seg_pairs[d * kPairLanes + k];
+    out[4 * d] = (d == me || !poff) ? 0ull : (unsigned long long)(poff[seg.b[d + 1]] - poff[seg.b[d]]);
+    out[4 * d + 1] = pairs;
     out[4 * d + 2] = (unsigned long long)err << 32;
     out[4 * d + 3] = 0;
 }
@@ -601,45 +636,33 @@ struct ResolveParams {
     const uint32_t* perm;     // sent slot -> message (kNone: a tail slot)
     const uint32_t* sender;   // the caller's d_sender
     const uint3* ref_recv;    // references from the remote owners, in sent-slot order (own segment left out)
-    const uint3* self_ref;    // references of this shard's own slots
     uint32_t self_a, self_b;  // this shard's own segment of the sent slots
     SegBounds sseg;           // sent slots per owner
-    uint32_t G, n;
+    uint32_t G, n;            // n = remote slots
     const uint32_t* pool;     // the pools received, owner after owner
     uint64_t pbase[WQ_MAX_SHARDS + 1];
-    const uint32_t* list;
-    const Record* recs;
     uint4* desc_msg;          // per message: {recipients, skip, pointer}
-    uint32_t* e_msg;          // per message: recipients (M + 1 entries, last 0)
+    uint32_t* e_msg;          // per message: recipients
     uint32_t* self_w;         // per message: the sender, for OnlySelf rows
 };
 
-// (ingesting GPU) per sent slot: the message's row descriptor, in message order.
+// (ingesting GPU) per slot sent to a remote owner: the message's row descriptor, in message order.
 __global__ __launch_bounds__(kBlock) void k_ref_resolve(ResolveParams p) {
-    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
-    if (k >= p.n) return;
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= p.n) return;
+    const uint32_t k = t < p.self_a ? t : t + (p.self_b - p.self_a);  // the sent slot
     const uint32_t m = p.perm[k];
     if (m == kNone) return;  // the tail of a two-slot message
-    const bool own = k >= p.self_a && k < p.self_b;
-    const uint3 ref = own ? p.self_ref[k - p.self_a] : p.ref_recv[k < p.self_a ? k : k - (p.self_b - p.self_a)];
+    const uint3 ref = p.ref_recv[t];
     const uint32_t kind = ref.z >> 30, sk = ref.z & kRefSkipNone;
-    uint32_t skip = sk == kRefSkipNone ? kNone : sk;
-    const uint32_t* src;
-    uint32_t e;
     if (kind == kRefSelf) {
-        e = ref.y;
-        skip = kNone;
-        if (e) p.self_w[m] = p.sender[m];
-        src = p.self_w + m;
-    } else {
-        e = ref.y - (skip != kNone ? 1u : 0u);
-        if (kind == kRefPool) src = p.pool + p.pbase[seg_find(p.sseg, p.G, k)] + ref.x;
-        else if (kind == kRefList) src = p.list + ref.x;
-        else src = reinterpret_cast<const uint32_t*>(p.recs) + ((uint64_t)ref.x * 32 + kInlineWord0);
+        if (ref.y) p.self_w[m] = p.sender[m];
+        put_desc(p.desc_msg, p.e_msg, m, ref.y, kNone, p.self_w + m);
+        return;
     }
-    const uint64_t a = reinterpret_cast<uint64_t>(src);
-    p.desc_msg[m] = make_uint4(e, skip, (uint32_t)a, (uint32_t)(a >> 32));
-    p.e_msg[m] = e;
+    const uint32_t skip = sk == kRefSkipNone ? kNone : sk;
+    const uint32_t e = ref.y - (skip != kNone ? 1u : 0u);
+    put_desc(p.desc_msg, p.e_msg, m, e, skip, p.pool + p.pbase[seg_find(p.sseg, p.G, k)] + ref.x);
 }
 
 int attach(wq_router* h, uint32_t G, uint32_t rank) {
@@ -659,23 +682,44 @@ int attach(wq_router* h, uint32_t G, uint32_t rank) {
     return WQ_OK;
 }
 
-// The slot tick's CSR from its message-order descriptors: offsets = exclusive scan of e_msg (whose
-// last entry is 0, so offsets[M] = P), then the rows gathered (outputs beyond capacity not written).
+// The slot tick's CSR from its message-order descriptors (e_msg, desc_msg): per-256-message
+// totals, the tile scan (offsets[M] = P, the counters at kSmallCnt: P, the overflow / error bits),
+// then the rows gathered with their offsets (outputs beyond capacity are not written).
 int slots_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity) {
     ShardCtx& sc = *h->shard;
     const uint64_t M = sc.last_M;
     hipStream_t s = h->stream;
-    size_t bytes = 0;
-    WQ_HIP(h, rocprim::exclusive_scan(nullptr, bytes, sc.e_msg.as<uint32_t>(), d_offsets, 0u, M + 1,
-                                      rocprim::plus<uint32_t>(), s));
-    WQ_ALLOC(h, sc.tmp, bytes);
-    WQ_HIP(h, rocprim::exclusive_scan(sc.tmp.p, bytes, sc.e_msg.as<uint32_t>(), d_offsets, 0u, M + 1,
-                                      rocprim::plus<uint32_t>(), s));
-    if (M && capacity) {
-        GatherParams gp{d_offsets, sc.desc_msg.as<uint4>(), (uint32_t)M, d_peers, d_msgs, capacity};
-        hipLaunchKernelGGL(gather_rows_kernel<16>, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, gp);
-        WQ_HIP(h, hipGetLastError());
+    wq_route_counters* cnt = reinterpret_cast<wq_route_counters*>(sc.small.as<char>() + kSmallCnt);
+    WQ_HIP(h, hipMemsetAsync(cnt, 0, sizeof(*cnt), s));
+    if (M == 0) {
+        WQ_HIP(h, hipMemsetAsync(d_offsets, 0, 4, s));
+        return WQ_OK;
     }
+    const uint32_t nt = (uint32_t)((M + kBlock - 1) / kBlock);
+    WQ_ALLOC(h, sc.mtiles, (uint64_t)nt * 8);
+    uint32_t* tile_total = sc.mtiles.as<uint32_t>();
+    uint32_t* tile_prefix = tile_total + nt;
+    hipLaunchKernelGGL(row_tile_sums_kernel, dim3(nt), dim3(kBlock), 0, s, sc.e_msg.as<uint32_t>(), (uint32_t)M,
+                       tile_total);
+    WQ_HIP(h, hipGetLastError());
+    TileScanParams tp;
+    tp.tile_total = tile_total;
+    tp.tile_F = tile_total;  // no candidate count on this path: F is reported as P
+    tp.tile_prefix = tile_prefix;
+    tp.n_tiles = nt;
+    tp.offsets = d_offsets;
+    tp.M = (uint32_t)M;
+    tp.capacity = capacity;
+    tp.cnt = cnt;
+    tp.health = h->rws.buf.p ? route_health(h) : nullptr;
+    tp.stale = h->tab.stale.as<uint32_t>();  // error bit 8: the table still misses a device batch
+    if (int rc = launch_tile_scan(h, tp)) return rc;
+    GatherParams gp{nullptr, sc.desc_msg.as<uint4>(), (uint32_t)M, capacity ? d_peers : nullptr, d_msgs, capacity};
+    gp.e = sc.e_msg.as<uint32_t>();
+    gp.tile_prefix = tile_prefix;
+    gp.offsets = d_offsets;
+    hipLaunchKernelGGL((gather_rows_kernel<16, true>), dim3(nt), dim3(kBlock), 0, s, gp);
+    WQ_HIP(h, hipGetLastError());
     return WQ_OK;
 }
 
@@ -721,7 +765,7 @@ void shard_release(wq_router* h) {
                       &sc->small,    &sc->slots,     &sc->perm,     &sc->rslots,    &sc->ocnt,     &sc->hslot,
                       &sc->plen,     &sc->poff,      &sc->claim,    &sc->lead,      &sc->self_ref, &sc->ref_send,
                       &sc->ref_recv, &sc->pool_send, &sc->pool_recv, &sc->desc_fill, &sc->desc_msg, &sc->e_msg,
-                      &sc->self_w};
+                      &sc->self_w,   &sc->mtiles};
     for (DevBuf* b : bufs) b->release();
     delete sc;
     h->shard = nullptr;
@@ -960,6 +1004,8 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
     const uint32_t G = sc.G, me = sc.rank;
     sc.last_ready = false;
     sc.last_slots = true;
+    const int inject = h->shard_inject;
+    h->shard_inject = 0;
     int late = WQ_OK;
     std::string late_msg;
     auto fail = [&](int rc) {
@@ -979,11 +1025,9 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
         return b.ensure(bytes) == hipSuccess ? WQ_OK : set_error(h, WQ_E_OOM, "hipMalloc (sharded tick workspace)");
     };
 
-    const int inject = h->shard_inject;
-    h->shard_inject = 0;
     // ---- 1. the M-sized buffers, then the slots grouped by owner ----
     const uint64_t slot_cap = 2 * (uint64_t)M + 1;
-    WQ_HIP(h, hipMemsetAsync(a_send, 0, 8 * G, s));
+    WQ_HIP(h, hipMemsetAsync(small, 0, kSmallPairs + (size_t)G * kPairLanes * 8, s));  // counts, statuses, sums
     if (inject == 1) fail(set_error(h, WQ_E_INVALID, "injected failure at step 1 (test hook)"));
     if (!late && !fail(alloc(sc.slots, slot_cap * kSlotWords * 4)) && !fail(alloc(sc.perm, slot_cap * 4)) &&
         !fail(alloc(sc.desc_msg, (M + 1) * 16)) && !fail(alloc(sc.e_msg, (M + 1) * 4)) &&
@@ -1024,7 +1068,7 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
         rseg.b[d + 1] = (uint32_t)R;
     }
     if (R >= 0xFFFFFC00ull) return fatal_receive(h, "more than 2^32 - 1024 slots on one owner");
-    const uint64_t n_self = n_in[me], R_remote = R - n_self;
+    const uint64_t n_self = n_in[me], R_remote = R - n_self, S_remote = S - n_out[me];
 
     // ---- 2. the slots ----
     const uint32_t* rslots = sc.slots.as<uint32_t>();
@@ -1040,8 +1084,7 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
         rslots = sc.rslots.as<uint32_t>();
     }
 
-    // ---- 3. the owner: count (local_message.rs:52-86 per slot), claims, pool sizes ----
-    WQ_HIP(h, hipMemsetAsync(seg_pairs, 0, 8 * G, s));
+    // ---- 3. the owner: count (local_message.rs:52-86 per slot), own slots resolved, claims ----
     if (inject == 3) fail(set_error(h, WQ_E_INVALID, "injected failure at step 3 (test hook)"));
     // fold in a finished incremental batch first (it may rebuild the table the view points into)
     if (!late) fail(table_resolve(h, false));
@@ -1052,9 +1095,9 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
         RouteWs& rw = h->rws;
         const uint32_t nb = (uint32_t)((R + kBlock - 1) / kBlock);
         if (!fail(alloc(rw.e, R * 4)) && !fail(alloc(rw.info, R * 8)) && !fail(alloc(rw.tiles, (uint64_t)nb * 12)) &&
-            !fail(alloc(sc.ocnt, R * 4)) && !fail(alloc(sc.hslot, R * 4)) && !fail(alloc(sc.plen, (R + 1) * 4)) &&
-            !fail(alloc(sc.poff, (R + 1) * 4)) && !fail(alloc(sc.desc_fill, R * 16)) &&
-            !fail(alloc(sc.self_ref, (n_self + 1) * 12)) && !fail(alloc(sc.ref_send, (R_remote + 1) * 12))) {
+            (G == 1 || (!fail(alloc(sc.ocnt, R * 4)) && !fail(alloc(sc.hslot, R * 4)) &&
+                        !fail(alloc(sc.plen, (R + 1) * 4)) && !fail(alloc(sc.poff, (R + 1) * 4)) &&
+                        !fail(alloc(sc.desc_fill, (R + 1) * 16)) && !fail(alloc(sc.ref_send, (R_remote + 1) * 12))))) {
             CountParams cp;
             cp.in = RouteIn{nullptr, nullptr, nullptr, nullptr, nullptr, (uint32_t)R, (int64_t)h->cube_size};
             cp.in.slots = rslots;
@@ -1084,7 +1127,7 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
         }
         if (!late) {
             const uint64_t period = (1ull << kRefClaimTagBits) - 1;
-            if (sc.ticks && sc.ticks % period == 0 && sc.claim_cap &&
+            if (R_remote && sc.ticks && sc.ticks % period == 0 &&
                 hipMemsetAsync(sc.claim.p, 0, sc.claim_cap * 8, s) != hipSuccess)  // tags wrap: forget them all
                 fail(set_error(h, WQ_E_HIP, "memset"));
             RefOwnerParams rp{};
@@ -1106,65 +1149,73 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
             rp.seg_pairs = seg_pairs;
             rp.poff = sc.poff.as<uint32_t>();
             rp.ref_send = sc.ref_send.as<uint3>();
-            rp.self_ref = sc.self_ref.as<uint3>();
             rp.desc_fill = sc.desc_fill.as<uint4>();
+            rp.perm = sc.perm.as<uint32_t>();
+            rp.self_sent = sseg.b[me];
+            rp.sender = d_sender;
+            rp.desc_msg = sc.desc_msg.as<uint4>();
+            rp.e_msg = sc.e_msg.as<uint32_t>();
+            rp.self_w = sc.self_w.as<uint32_t>();
             sc.ticks++;
-            hipLaunchKernelGGL(k_ref_claim, dim3((unsigned)((R + kBlock) / kBlock)), dim3(kBlock), 0, s, rp);
-            if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "claim launch (sharded tick)"));
-            if (!late) fail(scan_excl(h, sc.tmp, sc.plen.as<uint32_t>(), sc.poff.as<uint32_t>(), R + 1));
+            if (G > 1) {  // claims and per-source recipient sums (G = 1: P comes from the tile scan)
+                hipLaunchKernelGGL(k_ref_claim, dim3((unsigned)((R + kBlock) / kBlock)), dim3(kBlock), 0, s, rp);
+                if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "claim launch (sharded tick)"));
+                if (!late && R_remote) fail(scan_excl(h, sc.tmp, sc.plen.as<uint32_t>(), sc.poff.as<uint32_t>(), R + 1));
+            }
             if (!late) {
                 hipLaunchKernelGGL(k_ref_make, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rp);
-                hipLaunchKernelGGL(k_ref_sizes, dim3(1), dim3(64), 0, s, sc.poff.as<uint32_t>(), rseg, G, me,
-                                   (const unsigned long long*)seg_pairs, cur, tv.stale, c_send);
+                if (G > 1)
+                    hipLaunchKernelGGL(k_ref_sizes, dim3(1), dim3(64), 0, s, R_remote ? sc.poff.as<uint32_t>() : nullptr,
+                                       rseg, G, me, (const unsigned long long*)seg_pairs, cur, tv.stale, c_send);
                 if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "reference launch (sharded tick)"));
             }
         }
     }
-    if (late || !R) {  // nothing routed here: zero sizes (and the status, if a step failed)
-        std::vector<unsigned long long> v(4 * G, 0);
-        if (late)
-            for (uint32_t d = 0; d < G; ++d) v[4 * d + 2] = status_of(late);
-        WQ_HIP(h, hipMemcpyAsync(c_send, v.data(), 32 * G, hipMemcpyHostToDevice, s));
-    }
-    if (G > 1) {
-        Xfer x{{c_send}, {thirty2.data()}, {c_recv}, {thirty2.data()}, 1};
-        if ((rc = exchange(h, x))) return rc;
-    }
-    std::vector<unsigned long long> cv(8 * G);
-    WQ_HIP(h, hipMemcpyAsync(cv.data(), c_send, (G > 1 ? 64 : 32) * G, hipMemcpyDeviceToHost, s));
-    WQ_HIP(h, hipStreamSynchronize(s));  // host read 2
-    if (G == 1)
-        for (int q = 0; q < 4; ++q) cv[4 + q] = cv[q];
-    std::vector<uint64_t> pool_out(G), pool_in(G);
-    uint64_t P = 0, pool_out_total = 0, pool_in_total = 0;
-    std::vector<uint64_t> pbase(G + 1, 0);
-    for (uint32_t d = 0; d < G; ++d) {
-        pool_out[d] = cv[4 * d];
-        pool_in[d] = cv[4 * G + 4 * d];
-        P += cv[4 * G + 4 * d + 1];
-        const uint64_t st = cv[4 * G + 4 * d + 2];
-        if (st && !peer_status) {
-            peer_status = st;
-            peer_from = d;
-        }
-        pool_out_total += pool_out[d];
-        pbase[d] = pool_in_total;
-        pool_in_total += pool_in[d];
-    }
-    pbase[G] = pool_in_total;
 
-    // ---- 4. references and pools, then the ingesting side's exchange ----
-    if (alloc(sc.pool_send, (pool_out_total + 1) * 4)) return fatal_receive(h, "hipMalloc of the pools to send");
-    if (alloc(sc.pool_recv, (pool_in_total + 1) * 4) || alloc(sc.ref_recv, (S - n_out[me] + 1) * 12))
-        return fatal_receive(h, "hipMalloc of the references / pools to receive");
-    if (!late && R_remote && pool_out_total) {
-        GatherParams gp{sc.poff.as<uint32_t>(), sc.desc_fill.as<uint4>(), (uint32_t)R, sc.pool_send.as<uint32_t>(),
-                        nullptr, pool_out_total};
-        hipLaunchKernelGGL(gather_rows_kernel<16>, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, gp);
-        if (hipGetLastError() != hipSuccess) return fatal_receive(h, "pool gather launch");
-    }
+    // ---- 4. pool sizes, then the references and pools (G > 1) ----
+    std::vector<unsigned long long> cv(8 * G, 0);
+    std::vector<uint64_t> pbase(G + 1, 0);
+    uint64_t P = 0;
     uint64_t sent = 0, recvd = 0;
     if (G > 1) {
+        if (late || !R) {  // nothing routed here: zero sizes (and the status, if a step failed)
+            std::vector<unsigned long long> v(4 * G, 0);
+            if (late)
+                for (uint32_t d = 0; d < G; ++d) v[4 * d + 2] = status_of(late);
+            WQ_HIP(h, hipMemcpyAsync(c_send, v.data(), 32 * G, hipMemcpyHostToDevice, s));
+        }
+        {
+            Xfer x{{c_send}, {thirty2.data()}, {c_recv}, {thirty2.data()}, 1};
+            if ((rc = exchange(h, x))) return rc;
+        }
+        WQ_HIP(h, hipMemcpyAsync(cv.data(), c_send, 64 * G, hipMemcpyDeviceToHost, s));
+        WQ_HIP(h, hipStreamSynchronize(s));  // host read 2
+        std::vector<uint64_t> pool_out(G), pool_in(G);
+        uint64_t pool_out_total = 0, pool_in_total = 0;
+        for (uint32_t d = 0; d < G; ++d) {
+            pool_out[d] = cv[4 * d];
+            pool_in[d] = cv[4 * G + 4 * d];
+            P += cv[4 * G + 4 * d + 1];
+            const uint64_t st = cv[4 * G + 4 * d + 2];
+            if (st && !peer_status) {
+                peer_status = st;
+                peer_from = d;
+            }
+            pool_out_total += pool_out[d];
+            pbase[d] = pool_in_total;
+            pool_in_total += pool_in[d];
+        }
+        pbase[G] = pool_in_total;
+        if (alloc(sc.pool_send, (pool_out_total + 1) * 4)) return fatal_receive(h, "hipMalloc of the pools to send");
+        if (alloc(sc.pool_recv, (pool_in_total + 1) * 4) || alloc(sc.ref_recv, (S_remote + 1) * 12))
+            return fatal_receive(h, "hipMalloc of the references / pools to receive");
+        if (!late && R_remote && pool_out_total) {
+            GatherParams gp{sc.poff.as<uint32_t>(), sc.desc_fill.as<uint4>(), (uint32_t)R, sc.pool_send.as<uint32_t>(),
+                            nullptr, pool_out_total};
+            hipLaunchKernelGGL((gather_rows_kernel<16, false>), dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock),
+                               0, s, gp);
+            if (hipGetLastError() != hipSuccess) return fatal_receive(h, "pool gather launch");
+        }
         std::vector<size_t> rs(G), rr(G), ps(G), pr(G);
         for (uint32_t d = 0; d < G; ++d) {
             rs[d] = d == me || late ? 0 : n_in[d] * 12;  // references for the slots d sent here
@@ -1173,8 +1224,8 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
             ps[d] = late ? 0 : pool_out[d] * 4;
             pr[d] = pool_in[d] * 4;
             if (d != me) {
-                sent += n_out[d] * kSlotWords * 4 + rs[d] + ps[d];
-                recvd += n_in[d] * kSlotWords * 4 + rr[d] + pr[d];
+                sent += 8 + n_out[d] * kSlotWords * 4 + 32 + rs[d] + ps[d];
+                recvd += 8 + n_in[d] * kSlotWords * 4 + 32 + rr[d] + pr[d];
             }
         }
         Xfer x{{sc.ref_send.p, sc.pool_send.p}, {rs.data(), ps.data()}, {sc.ref_recv.p, sc.pool_recv.p},
@@ -1189,35 +1240,48 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
     }
     if (peer_status) return status_error(h, peer_status, peer_from);
 
-    // ---- 5. the ingesting side: descriptors in message order, offsets, rows ----
-    if (S) {
+    // ---- 5. the ingesting side: remote references -> descriptors, then the CSR ----
+    if (S_remote) {
         ResolveParams rp{};
         rp.perm = sc.perm.as<uint32_t>();
         rp.sender = d_sender;
         rp.ref_recv = sc.ref_recv.as<uint3>();
-        rp.self_ref = sc.self_ref.as<uint3>();
         rp.self_a = sseg.b[me];
         rp.self_b = sseg.b[me + 1];
         rp.sseg = sseg;
         rp.G = G;
-        rp.n = (uint32_t)S;
+        rp.n = (uint32_t)S_remote;
         rp.pool = sc.pool_recv.as<uint32_t>();
         for (uint32_t d = 0; d <= G; ++d) rp.pbase[d] = pbase[d];
-        rp.list = tv.list;
-        rp.recs = tv.recs;
         rp.desc_msg = sc.desc_msg.as<uint4>();
         rp.e_msg = sc.e_msg.as<uint32_t>();
         rp.self_w = sc.self_w.as<uint32_t>();
-        hipLaunchKernelGGL(k_ref_resolve, dim3((unsigned)((S + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rp);
+        hipLaunchKernelGGL(k_ref_resolve, dim3((unsigned)((S_remote + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rp);
         WQ_HIP(h, hipGetLastError());
     }
-    WQ_HIP(h, hipMemsetAsync(sc.e_msg.as<uint32_t>() + M, 0, 4, s));
     sc.last_M = M;
-    sc.last_P = P;
     sc.last_ready = true;
+    if (G > 1) {
+        sc.last_P = P;
+        *n_pairs = P;
+        if (P > 0xFFFFFFFFull) return set_error(h, WQ_E_CAPACITY, "more than 2^32-1 pairs in one tick");
+        return copy_out(h, d_offsets, d_peers, d_msgs, capacity);
+    }
+    // G = 1: P and the error bits from the tile scan's counters, read once the tick has run
+    if ((rc = slots_copy_out(h, d_offsets, d_peers, d_msgs, capacity))) return rc;
+    wq_route_counters c[2];
+    WQ_HIP(h, hipMemcpyAsync(&c[0], small + kSmallCnt, sizeof(c[0]), hipMemcpyDeviceToHost, s));
+    if (cur) WQ_HIP(h, hipMemcpyAsync(&c[1], cur, sizeof(c[1]), hipMemcpyDeviceToHost, s));
+    else c[1] = wq_route_counters{};
+    WQ_HIP(h, hipStreamSynchronize(s));
+    const uint32_t err = c[0].error | c[1].error;
+    P = M ? c[0].n_pairs : 0;
+    sc.last_P = P;
     *n_pairs = P;
-    if (P > 0xFFFFFFFFull) return set_error(h, WQ_E_CAPACITY, "more than 2^32-1 pairs in one tick");
-    return copy_out(h, d_offsets, d_peers, d_msgs, capacity);
+    if (err & kErrStale) return status_error(h, (uint64_t)kErrStale << 32, me);
+    if (err) return status_error(h, (uint64_t)err << 32, me);
+    if (P > capacity) return set_error(h, WQ_E_CAPACITY, "sharded tick: output capacity too small (required size in *n_pairs)");
+    return WQ_OK;
 }
 
 int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,

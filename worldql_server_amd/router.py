@@ -51,6 +51,8 @@ def load_library(build_if_missing: bool = True):
     vp, sz, u32, u16, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_int
     sig = {
         "wq_router_create": ([u16, i32, ctypes.POINTER(vp)], i32),
+        "wq_router_create_multi": ([u16, i32, vp, ctypes.POINTER(vp)], i32),
+        "wq_multi_info": ([vp, ctypes.POINTER(u32)], i32),
         "wq_router_destroy": ([vp], i32),
         "wq_last_error": ([vp], ctypes.c_char_p),
         "wq_set_stream": ([vp, vp], i32),
@@ -174,6 +176,27 @@ class Router:
         self.device = device
         if hash_bits != 64:
             self._check(self.lib.wq_debug_set_hash_bits(self.h, hash_bits))
+
+    @classmethod
+    def multi(cls, cube_size: int = 16, devices=(0,)) -> "Router":
+        """One handle over len(devices) GPUs (wq_router_create_multi): the same API, the one-table
+        result, the table sharded by cube hash over the devices (they may repeat)."""
+        self = cls.__new__(cls)
+        self.lib = load_library()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        rc = self.lib.wq_router_create_multi(cube_size, len(devices), devs, ctypes.byref(h))
+        if rc != 0:
+            raise WQError(rc, self.lib.wq_last_error(None).decode())
+        self.h = h
+        self.cube_size = cube_size
+        self.device = devices[0]
+        return self
+
+    def n_gpus(self) -> int:
+        n = ctypes.c_uint32()
+        self._check(self.lib.wq_multi_info(self.h, ctypes.byref(n)))
+        return n.value
 
     def _check(self, rc: int):
         if rc != 0:
