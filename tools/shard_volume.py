@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""What the sharded tick moves between GPUs, measured at any G on ONE GPU (the in-process hub:
+G router handles on cuda:0, one thread each — the collective runs for real, only the links are
+local copies). Full C3 by default: every shard ingests M/G of the 10M messages; per shard the
+bytes sent to / received from the other shards (wq_shard_last_bytes) in both return forms:
+
+  slots     20-byte slots out; 12-byte row references + one pool of cube lists per
+            (owner, destination) back (the default)
+  expanded  40-byte records out; per-record counts + expanded peer ids back (the radius form)
+
+    python tools/shard_volume.py [--G 8] [--scale 1.0] [--out profiles/r03_c3_xgmi_g8.json]
+
+The bench's C3 line quotes the result as its modelled xGMI volume per GPU (bench_configs.py)."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--G", type=int, default=8)
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import torch
+    from worldql_server_amd import synth_ext
+    from worldql_server_amd.router import Hub, Router
+
+    w = synth_ext.config_c3(scale=a.scale)
+    M, G = len(w.world), a.G
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    res = {"slots": [None] * G, "expanded": [None] * G}
+    errors = []
+
+    def body(rank):
+        try:
+            r = routers[rank]
+            r.attach_hub(hub, rank)
+            r.set_fanout_hint(40.0)
+            lo, hi = rank * M // G, (rank + 1) * M // G
+            n = hi - lo
+            r.sharded_apply_ops(w.ops)
+            pos = torch.from_numpy(np.ascontiguousarray(w.pos[lo:hi])).to(dev)
+            wo = torch.from_numpy(np.ascontiguousarray(w.world[lo:hi]).view(np.int32)).to(dev)
+            se = torch.from_numpy(np.ascontiguousarray(w.sender[lo:hi]).view(np.int32)).to(dev)
+            rp = torch.from_numpy(np.ascontiguousarray(w.repl[lo:hi])).to(dev)
+            offs = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            cap = 64 * n + 1024
+            peers = torch.empty(cap, dtype=torch.int32, device=dev)
+            torch.cuda.synchronize(dev)
+            for form in ("slots", "expanded"):
+                r.set_shard_form(form == "expanded")
+                rc, P = r.sharded_route_device(pos.data_ptr(), wo.data_ptr(), se.data_ptr(), rp.data_ptr(), n,
+                                               offs.data_ptr(), peers.data_ptr(), None, cap)
+                assert rc == 0, rc
+                sent, recvd = r.shard_last_bytes()
+                res[form][rank] = {"messages": n, "pairs": int(P), "sent_bytes": int(sent), "recv_bytes": int(recvd)}
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=body, args=(k,)) for k in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    out = {"workload": f"C3 (scale {a.scale}): {M} messages, {len(w.ops)} subscriptions, G = {G} shards as hub "
+                       f"threads on one GPU (the bytes are those an {G}-GPU run moves over xGMI)",
+           "G": G, "messages_per_tick": M, "pairs_per_tick": sum(x["pairs"] for x in res["slots"]),
+           "wall_s": round(time.perf_counter() - t0, 1)}
+    for form in ("slots", "expanded"):
+        s = [x["sent_bytes"] for x in res[form]]
+        r_ = [x["recv_bytes"] for x in res[form]]
+        out[form] = {"sent_bytes_per_gpu_mean": float(np.mean(s)), "sent_bytes_per_gpu_max": int(max(s)),
+                     "recv_bytes_per_gpu_mean": float(np.mean(r_)), "recv_bytes_per_gpu_max": int(max(r_)),
+                     "per_shard": res[form]}
+    out["slots_vs_expanded"] = out["slots"]["sent_bytes_per_gpu_mean"] / out["expanded"]["sent_bytes_per_gpu_mean"]
+    print(json.dumps({k: v for k, v in out.items() if k not in ("slots", "expanded")}))
+    print(json.dumps({f: {k: v for k, v in out[f].items() if k != "per_shard"} for f in ("slots", "expanded")}))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+    for r in routers:
+        r.close()
+    hub.close()
+
+
+if __name__ == "__main__":
+    main()

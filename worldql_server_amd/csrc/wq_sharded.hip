@@ -152,14 +152,11 @@ constexpr int kXNone = 0, kXHub = 1, kXRccl = 2, kXCallback = 3;
 constexpr double kHubTimeoutS = 120.0;
 // The small exchange vectors (ShardCtx::small, allocated at attach): the slot counts exchange
 // {slots, status} u32 x 2 per shard (send at kSmallA, receive after it), the pool-size exchange
-// {pool words, recipients, status, 0} u64 x 4 per shard (send at kSmallC, receive after it), the
-// message-side counters of a slot tick (kSmallCnt), and the owner's per-source recipient sums, 64
-// partial words per source (kSmallPairs: blocks add to word blockIdx % 64 — one shared word would
-// take ~40k same-address atomics per C3 tick at ~90 per microsecond).
-constexpr size_t kSmallA = 0, kSmallC = 1024, kSmallCnt = 5120, kSmallPairs = 8192, kPairLanes = 64;
-constexpr size_t kSmallBytes = kSmallPairs + WQ_MAX_SHARDS * kPairLanes * 8;
+// {pool words, 0, status, 0} u64 x 4 per shard (send at kSmallC, receive after it), and the
+// message-side counters of a slot tick (kSmallCnt: P and the error bits, from its tile scan).
+constexpr size_t kSmallA = 0, kSmallC = 1024, kSmallCnt = 5120, kSmallBytes = 8192;
 static_assert(kSmallA + 4 * WQ_MAX_SHARDS * 4 <= kSmallC && kSmallC + 8 * WQ_MAX_SHARDS * 8 <= kSmallCnt &&
-                  kSmallCnt + sizeof(wq_route_counters) <= kSmallPairs,
+                  kSmallCnt + sizeof(wq_route_counters) <= kSmallBytes,
               "small exchange vector layout");
 
 }  // namespace
@@ -461,29 +458,23 @@ __device__ __forceinline__ uint32_t seg_find(const SegBounds& sb, uint32_t G, ui
 }
 
 struct RefOwnerParams {
-    const uint32_t* e;     // count pass: filtered recipients per slot
-    const uint2* info;     // count pass: locator per slot (route_count.hpp finish_message)
+    const uint32_t* e;     // count pass: filtered recipients per received slot (remote slots)
+    const uint2* info;     // count pass: locator per received slot (route_count.hpp finish_message)
     const uint32_t* list;
     const Record* recs;
-    SegBounds seg;         // received slots per source shard
-    uint32_t G, me, R, tag;
+    SegBounds rrem;        // the remote slots per source shard, in remote index (own segment empty)
+    uint32_t G, n_rem;     // remote slots
+    uint32_t self_lo, n_self;  // the own segment of the received slots (skipped)
+    uint32_t tag;
     unsigned long long* claim;  // (cube, source) claims of this tick, open addressing
-    uint32_t* lead;             // claim slot -> the slot that claimed it
+    uint32_t* lead;             // claim slot -> the remote slot that claimed it
     uint64_t cmask;
-    uint32_t* cnt;         // per slot: the cube's peer count (OnlySelf: e)
-    uint32_t* hslot;       // per slot: its claim slot
-    uint32_t* plen;        // per slot: words it adds to its source's pool (R + 1 entries, last 0)
-    unsigned long long* seg_pairs;  // per source: kPairLanes partial recipient sums
+    uint32_t* cnt;         // per remote slot: the cube's peer count (OnlySelf: e)
+    uint32_t* hslot;       // per remote slot: its claim slot
+    uint32_t* plen;        // per remote slot: words it adds to its source's pool (n_rem + 1 entries)
     const uint32_t* poff;  // exclusive scan of plen
-    uint3* ref_send;       // references of the remote sources' slots (own segment left out)
+    uint3* ref_send;       // per remote slot: its reference
     uint4* desc_fill;      // pool rows: the claiming slot copies its cube's peers
-    // this shard's own slots resolve here, straight into the message-order descriptors
-    const uint32_t* perm;  // sent slot -> message (kNone: a tail)
-    uint32_t self_sent;    // first sent slot of this shard's own segment
-    const uint32_t* sender;
-    uint4* desc_msg;
-    uint32_t* e_msg;
-    uint32_t* self_w;
 };
 
 __device__ __forceinline__ uint32_t slot_cnt(const uint2 inf, uint32_t e, const uint32_t* list) {
@@ -492,59 +483,41 @@ __device__ __forceinline__ uint32_t slot_cnt(const uint2 inf, uint32_t e, const 
     return inf.y == kNone ? 0u : inf.y >> 24;  // inline record, or no subscriber at all
 }
 
-// (owner, G > 1) per received slot: the cube's peer count, and for a remote source's slot the claim
-// of its (source, cube) pair — the first claimer ships the cube's peers in that source's pool, the
-// others point at them. Per-source recipient sums: LDS, then one global atomic per (block, source)
-// spread over kPairLanes words.
+// (owner, remote slots) the cube's peer count and the claim of the slot's (source, cube) pair: the
+// first claimer ships the cube's peers in that source's pool, the others point at them.
 __global__ __launch_bounds__(kBlock) void k_ref_claim(RefOwnerParams p) {
-    __shared__ unsigned long long acc[WQ_MAX_SHARDS];
-    const int tid = threadIdx.x;
-    for (uint32_t d = tid; d < p.G; d += kBlock) acc[d] = 0;
-    __syncthreads();
-    const uint32_t i = blockIdx.x * kBlock + tid;
-    uint32_t s = 0, ei = 0;
-    if (i < p.R) {
-        s = seg_find(p.seg, p.G, i);
-        const uint2 inf = p.info[i];
-        ei = p.e[i];
-        const uint32_t cnt = slot_cnt(inf, ei, p.list);
-        bool leader = false;
-        uint64_t hs = 0;
-        if (s != p.me && !(inf.x & kLocSelf) && cnt) {
-            const unsigned long long key = ((unsigned long long)p.tag << 38) | ((unsigned long long)s << 32) | inf.x;
-            uint64_t hv = ((uint64_t)inf.x | ((uint64_t)s << 32)) * 0x9E3779B97F4A7C15ull;
-            hv ^= hv >> 29;
-            hs = hv & p.cmask;
-            for (;;) {
-                unsigned long long v = __hip_atomic_load(p.claim + hs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((v >> 38) != p.tag) {  // a previous tick's word: free
-                    const unsigned long long old = atomicCAS(p.claim + hs, v, key);
-                    if (old == v) {
-                        leader = true;
-                        break;
-                    }
-                    v = old;
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t == p.n_rem) p.plen[t] = 0;
+    if (t >= p.n_rem) return;
+    const uint32_t i = t < p.self_lo ? t : t + p.n_self;  // the received slot
+    const uint32_t s = seg_find(p.rrem, p.G, t);
+    const uint2 inf = p.info[i];
+    const uint32_t cnt = slot_cnt(inf, p.e[i], p.list);
+    bool leader = false;
+    uint64_t hs = 0;
+    if (!(inf.x & kLocSelf) && cnt) {
+        const unsigned long long key = ((unsigned long long)p.tag << 38) | ((unsigned long long)s << 32) | inf.x;
+        uint64_t hv = ((uint64_t)inf.x | ((uint64_t)s << 32)) * 0x9E3779B97F4A7C15ull;
+        hv ^= hv >> 29;
+        hs = hv & p.cmask;
+        for (;;) {
+            unsigned long long v = __hip_atomic_load(p.claim + hs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((v >> 38) != p.tag) {  // a previous tick's word: free
+                const unsigned long long old = atomicCAS(p.claim + hs, v, key);
+                if (old == v) {
+                    leader = true;
+                    break;
                 }
-                if (v == key) break;
-                if ((v >> 38) == p.tag) hs = (hs + 1) & p.cmask;
+                v = old;
             }
-            if (leader) p.lead[hs] = i;
+            if (v == key) break;
+            if ((v >> 38) == p.tag) hs = (hs + 1) & p.cmask;
         }
-        p.cnt[i] = cnt;
-        p.hslot[i] = (uint32_t)hs;
-        p.plen[i] = leader ? cnt : 0u;
+        if (leader) p.lead[hs] = t;
     }
-    if (i == p.R) p.plen[i] = 0;
-    const uint32_t s0 = __shfl(s, 0, 64);
-    if (__all(i >= p.R || s == s0)) {
-        const uint64_t w = wave_sum_u64(ei);
-        if ((tid & 63) == 0 && w) atomicAdd(&acc[s0], (unsigned long long)w);
-    } else if (i < p.R && ei) {
-        atomicAdd(&acc[s], (unsigned long long)ei);
-    }
-    __syncthreads();
-    for (uint32_t d = tid; d < p.G; d += kBlock)
-        if (acc[d]) atomicAdd(p.seg_pairs + d * kPairLanes + (blockIdx.x & (kPairLanes - 1)), acc[d]);
+    p.cnt[t] = cnt;
+    p.hslot[t] = (uint32_t)hs;
+    p.plen[t] = leader ? cnt : 0u;
 }
 
 // The row of a slot from its count-pass locator: kind, source offset (list word / record slot) and
@@ -577,57 +550,90 @@ __device__ __forceinline__ void put_desc(uint4* desc_msg, uint32_t* e_msg, uint3
     e_msg[m] = e;
 }
 
-// (owner) per received slot: this shard's own slots resolve at once into their messages'
-// descriptors (pointers into the table); a remote source's slot becomes its reference into the
-// source's pool and, for the claiming slot, the pool row copying its cube's peers.
-__global__ __launch_bounds__(kBlock) void k_ref_make(RefOwnerParams p) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= p.R) return;
-    const uint32_t s = p.G > 1 ? seg_find(p.seg, p.G, i) : 0u;
-    const uint2 inf = p.info[i];
-    uint32_t kind, off, skip;
-    slot_row(inf, &kind, &off, &skip);
-    if (s == p.me) {
-        const uint32_t m = p.perm[p.self_sent + (i - p.seg.b[s])];
+// (owner) the count pass over the received slots (route_count.hpp count_rows, one slot per lane).
+// This shard's own slots — all of them at G = 1 — resolve right here into their messages'
+// descriptors (pointers into the table): the ingesting side is this GPU, so nothing is staged and
+// the record lines the count just read are still in the caches when the gather follows. A remote
+// source's slot leaves its count and locator for the claim / reference kernels.
+struct SlotCountParams {
+    CountParams c;
+    uint32_t self_lo, self_hi;  // this shard's own segment of the received slots
+    const uint32_t* perm;       // sent slot -> message
+    uint32_t self_sent;         // first sent slot of the own segment
+    const uint32_t* sender;
+    uint4* desc_msg;
+    uint32_t* e_msg;
+    uint32_t* self_w;
+};
+
+__global__ __launch_bounds__(kBlock, 8) void k_count_slots(SlotCountParams p) {
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0 && tid == 0) {
+        p.c.cnt_next->n_pairs = 0;
+        p.c.cnt_next->n_candidates = 0;
+        p.c.cnt_next->overflow = 0;
+        p.c.cnt_next->error = 0;
+    }
+    const uint32_t m0 = blockIdx.x * kBlock;
+    uint64_t F_local = 0;
+    uint32_t E_local = 0;
+    uint32_t e_out[1];
+    uint2 inf_out[1];
+    count_rows<true, 1, 0, false, true>(p.c.in, p.c.t, m0, e_out, inf_out, F_local, E_local);
+    const uint32_t i = m0 + tid;
+    if (i >= p.c.in.M) return;
+    if (i >= p.self_lo && i < p.self_hi) {
+        const uint32_t m = p.perm[p.self_sent + (i - p.self_lo)];
         if (m == kNone) return;  // a tail slot
-        const uint32_t e = p.e[i];
+        uint32_t kind, off, skip;
+        slot_row(inf_out[0], &kind, &off, &skip);
+        const uint32_t e = e_out[0];
         if (kind == kRefSelf) {
             if (e) p.self_w[m] = p.sender[m];
             put_desc(p.desc_msg, p.e_msg, m, e, kNone, p.self_w + m);
         } else {
-            put_desc(p.desc_msg, p.e_msg, m, e, skip == kRefSkipNone ? kNone : skip, row_src(kind, off, p.list, p.recs));
+            put_desc(p.desc_msg, p.e_msg, m, e, skip == kRefSkipNone ? kNone : skip,
+                     row_src(kind, off, p.c.t.list, p.c.t.recs));
         }
         return;
     }
-    const uint32_t cnt = p.cnt[i];
+    p.c.e[i] = e_out[0];
+    p.c.info[i] = inf_out[0];
+}
+
+// (owner, remote slots) a remote source's slot becomes its reference into the source's pool and,
+// for the claiming slot, the pool row copying its cube's peers.
+__global__ __launch_bounds__(kBlock) void k_ref_make(RefOwnerParams p) {
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= p.n_rem) return;
+    const uint32_t i = t < p.self_lo ? t : t + p.n_self;  // the received slot
+    const uint32_t s = seg_find(p.rrem, p.G, t);
+    uint32_t kind, off, skip;
+    slot_row(p.info[i], &kind, &off, &skip);
+    const uint32_t cnt = p.cnt[t];
     uint3 ref;
     if (kind == kRefList || kind == kRefInline) {
-        const uint32_t j = p.lead[p.hslot[i]];
-        ref = make_uint3(p.poff[j] - p.poff[p.seg.b[s]], cnt, (kRefPool << 30) | skip);
-        if (j == i) {
+        const uint32_t j = p.lead[p.hslot[t]];
+        ref = make_uint3(p.poff[j] - p.poff[p.rrem.b[s]], cnt, (kRefPool << 30) | skip);
+        if (j == t) {
             const uint64_t a = reinterpret_cast<uint64_t>(row_src(kind, off, p.list, p.recs));
-            p.desc_fill[i] = make_uint4(cnt, kNone, (uint32_t)a, (uint32_t)(a >> 32));
+            p.desc_fill[t] = make_uint4(cnt, kNone, (uint32_t)a, (uint32_t)(a >> 32));
         }
     } else {
         ref = make_uint3(0, cnt, (kRefSelf << 30) | kRefSkipNone);
     }
-    const uint32_t a = p.seg.b[p.me], nself = p.seg.b[p.me + 1] - a;
-    p.ref_send[i < a ? i : i - nself] = ref;
+    p.ref_send[t] = ref;
 }
 
-// (owner, G > 1) the per-destination words of the pool-size exchange: {pool words, recipients,
-// status, 0}. status = error bits of the count pass (2: > 2^32 pairs in a block, 8: stale table) << 32.
-__global__ void k_ref_sizes(const uint32_t* __restrict__ poff, SegBounds seg, uint32_t G, uint32_t me,
-                            const unsigned long long* __restrict__ seg_pairs, const wq_route_counters* __restrict__ cnt,
+// (owner, G > 1) the per-destination words of the pool-size exchange: {pool words, 0, status, 0}.
+// status = error bits of the count pass (8: stale table) << 32.
+__global__ void k_ref_sizes(const uint32_t* __restrict__ poff, SegBounds rrem, uint32_t G,
                             const uint32_t* __restrict__ stale, unsigned long long* __restrict__ out) {
     const uint32_t d = threadIdx.x;
     if (d >= G) return;
-    uint32_t err = cnt->error;
-    if (stale && *stale) err |= kErrStale;
-    unsigned long long pairs = 0;
-    for (uint32_t k = 0; k < kPairLanes; ++k) pairs += seg_pairs[d * kPairLanes + k];
-    out[4 * d] = (d == me || !poff) ? 0ull : (unsigned long long)(poff[seg.b[d + 1]] - poff[seg.b[d]]);
-    out[4 * d + 1] = pairs;
+    const uint32_t err = (stale && *stale) ? kErrStale : 0u;
+    out[4 * d] = poff ? (unsigned long long)(poff[rrem.b[d + 1]] - poff[rrem.b[d]]) : 0ull;
+    out[4 * d + 1] = 0;
     out[4 * d + 2] = (unsigned long long)err << 32;
     out[4 * d + 3] = 0;
 }
@@ -1020,14 +1026,13 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
     uint32_t* a_recv = a_send + 2 * G;
     unsigned long long* c_send = reinterpret_cast<unsigned long long*>(small + kSmallC);
     unsigned long long* c_recv = c_send + 4 * G;
-    unsigned long long* seg_pairs = reinterpret_cast<unsigned long long*>(small + kSmallPairs);
     auto alloc = [&](DevBuf& b, size_t bytes) -> int {
         return b.ensure(bytes) == hipSuccess ? WQ_OK : set_error(h, WQ_E_OOM, "hipMalloc (sharded tick workspace)");
     };
 
     // ---- 1. the M-sized buffers, then the slots grouped by owner ----
     const uint64_t slot_cap = 2 * (uint64_t)M + 1;
-    WQ_HIP(h, hipMemsetAsync(small, 0, kSmallPairs + (size_t)G * kPairLanes * 8, s));  // counts, statuses, sums
+    WQ_HIP(h, hipMemsetAsync(small, 0, kSmallCnt, s));  // counts and statuses
     if (inject == 1) fail(set_error(h, WQ_E_INVALID, "injected failure at step 1 (test hook)"));
     if (!late && !fail(alloc(sc.slots, slot_cap * kSlotWords * 4)) && !fail(alloc(sc.perm, slot_cap * 4)) &&
         !fail(alloc(sc.desc_msg, (M + 1) * 16)) && !fail(alloc(sc.e_msg, (M + 1) * 4)) &&
@@ -1052,9 +1057,9 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
     std::vector<uint64_t> n_out(G), n_in(G);
     uint64_t peer_status = 0;
     uint32_t peer_from = 0;
-    SegBounds sseg, rseg;
-    sseg.b[0] = rseg.b[0] = 0;
-    uint64_t R = 0, S = 0;
+    SegBounds sseg, rseg, rrem;
+    sseg.b[0] = rseg.b[0] = rrem.b[0] = 0;
+    uint64_t R = 0, S = 0, Rr = 0;
     for (uint32_t d = 0; d < G; ++d) {
         n_out[d] = av[2 * d];
         n_in[d] = av[2 * G + 2 * d];
@@ -1064,8 +1069,10 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
         }
         S += n_out[d];
         R += n_in[d];
+        if (d != me) Rr += n_in[d];
         sseg.b[d + 1] = (uint32_t)S;
         rseg.b[d + 1] = (uint32_t)R;
+        rrem.b[d + 1] = (uint32_t)Rr;  // the remote slots, own segment left out
     }
     if (R >= 0xFFFFFC00ull) return fatal_receive(h, "more than 2^32 - 1024 slots on one owner");
     const uint64_t n_self = n_in[me], R_remote = R - n_self, S_remote = S - n_out[me];
@@ -1084,7 +1091,8 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
         rslots = sc.rslots.as<uint32_t>();
     }
 
-    // ---- 3. the owner: count (local_message.rs:52-86 per slot), own slots resolved, claims ----
+    // ---- 3. the owner: count (local_message.rs:52-86 per slot; own slots resolved in place),
+    //         then the remote slots' claims, pools and references ----
     if (inject == 3) fail(set_error(h, WQ_E_INVALID, "injected failure at step 3 (test hook)"));
     // fold in a finished incremental batch first (it may rebuild the table the view points into)
     if (!late) fail(table_resolve(h, false));
@@ -1093,23 +1101,29 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
     if (!late && R) fail(route_counters(h, R, nullptr, &cur, &nxt));
     if (!late && R) {
         RouteWs& rw = h->rws;
-        const uint32_t nb = (uint32_t)((R + kBlock - 1) / kBlock);
-        if (!fail(alloc(rw.e, R * 4)) && !fail(alloc(rw.info, R * 8)) && !fail(alloc(rw.tiles, (uint64_t)nb * 12)) &&
-            (G == 1 || (!fail(alloc(sc.ocnt, R * 4)) && !fail(alloc(sc.hslot, R * 4)) &&
-                        !fail(alloc(sc.plen, (R + 1) * 4)) && !fail(alloc(sc.poff, (R + 1) * 4)) &&
-                        !fail(alloc(sc.desc_fill, (R + 1) * 16)) && !fail(alloc(sc.ref_send, (R_remote + 1) * 12))))) {
-            CountParams cp;
-            cp.in = RouteIn{nullptr, nullptr, nullptr, nullptr, nullptr, (uint32_t)R, (int64_t)h->cube_size};
-            cp.in.slots = rslots;
-            cp.t = tv;
-            cp.e = rw.e.as<uint32_t>();
-            cp.info = rw.info.as<uint2>();
-            cp.tile_total = rw.tiles.as<uint32_t>();
-            cp.tile_F = cp.tile_total + nb;
-            cp.cnt = cur;
-            cp.cnt_next = nxt;
-            cp.health = route_health(h);
-            hipLaunchKernelGGL((count_kernel<true, 1, 8, 0, false, true>), dim3(nb), dim3(kBlock), 0, s, cp);
+        if (!fail(alloc(rw.e, R * 4)) && !fail(alloc(rw.info, R * 8)) &&
+            (!R_remote || (!fail(alloc(sc.ocnt, R_remote * 4)) && !fail(alloc(sc.hslot, R_remote * 4)) &&
+                           !fail(alloc(sc.plen, (R_remote + 1) * 4)) && !fail(alloc(sc.poff, (R_remote + 1) * 4)) &&
+                           !fail(alloc(sc.desc_fill, (R_remote + 1) * 16)) &&
+                           !fail(alloc(sc.ref_send, (R_remote + 1) * 12))))) {
+            SlotCountParams cp{};
+            cp.c.in = RouteIn{nullptr, nullptr, nullptr, nullptr, nullptr, (uint32_t)R, (int64_t)h->cube_size};
+            cp.c.in.slots = rslots;
+            cp.c.t = tv;
+            cp.c.e = rw.e.as<uint32_t>();
+            cp.c.info = rw.info.as<uint2>();
+            cp.c.cnt = cur;
+            cp.c.cnt_next = nxt;
+            cp.c.health = route_health(h);
+            cp.self_lo = rseg.b[me];
+            cp.self_hi = rseg.b[me + 1];
+            cp.perm = sc.perm.as<uint32_t>();
+            cp.self_sent = sseg.b[me];
+            cp.sender = d_sender;
+            cp.desc_msg = sc.desc_msg.as<uint4>();
+            cp.e_msg = sc.e_msg.as<uint32_t>();
+            cp.self_w = sc.self_w.as<uint32_t>();
+            hipLaunchKernelGGL(k_count_slots, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, cp);
             if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "count launch (sharded tick)"));
         }
         uint64_t C = 0;
@@ -1125,48 +1139,36 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
                 C = sc.claim_cap;
             }
         }
-        if (!late) {
+        if (!late && R_remote) {
             const uint64_t period = (1ull << kRefClaimTagBits) - 1;
-            if (R_remote && sc.ticks && sc.ticks % period == 0 &&
-                hipMemsetAsync(sc.claim.p, 0, sc.claim_cap * 8, s) != hipSuccess)  // tags wrap: forget them all
-                fail(set_error(h, WQ_E_HIP, "memset"));
+            if (sc.ticks && sc.ticks % period == 0 && hipMemsetAsync(sc.claim.p, 0, sc.claim_cap * 8, s) != hipSuccess)
+                fail(set_error(h, WQ_E_HIP, "memset"));  // the tags wrap: forget them all
             RefOwnerParams rp{};
             rp.e = rw.e.as<uint32_t>();
             rp.info = rw.info.as<uint2>();
             rp.list = tv.list;
             rp.recs = tv.recs;
-            rp.seg = rseg;
+            rp.rrem = rrem;
             rp.G = G;
-            rp.me = me;
-            rp.R = (uint32_t)R;
+            rp.n_rem = (uint32_t)R_remote;
+            rp.self_lo = rseg.b[me];
+            rp.n_self = (uint32_t)n_self;
             rp.tag = (uint32_t)(sc.ticks % period) + 1u;
             rp.claim = sc.claim.as<unsigned long long>();
             rp.lead = sc.lead.as<uint32_t>();
-            rp.cmask = C ? C - 1 : 0;
+            rp.cmask = C - 1;
             rp.cnt = sc.ocnt.as<uint32_t>();
             rp.hslot = sc.hslot.as<uint32_t>();
             rp.plen = sc.plen.as<uint32_t>();
-            rp.seg_pairs = seg_pairs;
             rp.poff = sc.poff.as<uint32_t>();
             rp.ref_send = sc.ref_send.as<uint3>();
             rp.desc_fill = sc.desc_fill.as<uint4>();
-            rp.perm = sc.perm.as<uint32_t>();
-            rp.self_sent = sseg.b[me];
-            rp.sender = d_sender;
-            rp.desc_msg = sc.desc_msg.as<uint4>();
-            rp.e_msg = sc.e_msg.as<uint32_t>();
-            rp.self_w = sc.self_w.as<uint32_t>();
             sc.ticks++;
-            if (G > 1) {  // claims and per-source recipient sums (G = 1: P comes from the tile scan)
-                hipLaunchKernelGGL(k_ref_claim, dim3((unsigned)((R + kBlock) / kBlock)), dim3(kBlock), 0, s, rp);
-                if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "claim launch (sharded tick)"));
-                if (!late && R_remote) fail(scan_excl(h, sc.tmp, sc.plen.as<uint32_t>(), sc.poff.as<uint32_t>(), R + 1));
-            }
+            hipLaunchKernelGGL(k_ref_claim, dim3((unsigned)((R_remote + kBlock) / kBlock)), dim3(kBlock), 0, s, rp);
+            if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "claim launch (sharded tick)"));
+            if (!late) fail(scan_excl(h, sc.tmp, sc.plen.as<uint32_t>(), sc.poff.as<uint32_t>(), R_remote + 1));
             if (!late) {
-                hipLaunchKernelGGL(k_ref_make, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rp);
-                if (G > 1)
-                    hipLaunchKernelGGL(k_ref_sizes, dim3(1), dim3(64), 0, s, R_remote ? sc.poff.as<uint32_t>() : nullptr,
-                                       rseg, G, me, (const unsigned long long*)seg_pairs, cur, tv.stale, c_send);
+                hipLaunchKernelGGL(k_ref_make, dim3((unsigned)((R_remote + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rp);
                 if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "reference launch (sharded tick)"));
             }
         }
@@ -1175,13 +1177,16 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
     // ---- 4. pool sizes, then the references and pools (G > 1) ----
     std::vector<unsigned long long> cv(8 * G, 0);
     std::vector<uint64_t> pbase(G + 1, 0);
-    uint64_t P = 0;
     uint64_t sent = 0, recvd = 0;
     if (G > 1) {
-        if (late || !R) {  // nothing routed here: zero sizes (and the status, if a step failed)
+        if (!late) {
+            hipLaunchKernelGGL(k_ref_sizes, dim3(1), dim3(64), 0, s, R_remote ? sc.poff.as<uint32_t>() : nullptr, rrem,
+                               G, tv.stale, c_send);
+            if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "size launch (sharded tick)"));
+        }
+        if (late) {  // nothing routed here: zero sizes and the status
             std::vector<unsigned long long> v(4 * G, 0);
-            if (late)
-                for (uint32_t d = 0; d < G; ++d) v[4 * d + 2] = status_of(late);
+            for (uint32_t d = 0; d < G; ++d) v[4 * d + 2] = status_of(late);
             WQ_HIP(h, hipMemcpyAsync(c_send, v.data(), 32 * G, hipMemcpyHostToDevice, s));
         }
         {
@@ -1195,7 +1200,6 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
         for (uint32_t d = 0; d < G; ++d) {
             pool_out[d] = cv[4 * d];
             pool_in[d] = cv[4 * G + 4 * d];
-            P += cv[4 * G + 4 * d + 1];
             const uint64_t st = cv[4 * G + 4 * d + 2];
             if (st && !peer_status) {
                 peer_status = st;
@@ -1210,10 +1214,10 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
         if (alloc(sc.pool_recv, (pool_in_total + 1) * 4) || alloc(sc.ref_recv, (S_remote + 1) * 12))
             return fatal_receive(h, "hipMalloc of the references / pools to receive");
         if (!late && R_remote && pool_out_total) {
-            GatherParams gp{sc.poff.as<uint32_t>(), sc.desc_fill.as<uint4>(), (uint32_t)R, sc.pool_send.as<uint32_t>(),
-                            nullptr, pool_out_total};
-            hipLaunchKernelGGL((gather_rows_kernel<16, false>), dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock),
-                               0, s, gp);
+            GatherParams gp{sc.poff.as<uint32_t>(), sc.desc_fill.as<uint4>(), (uint32_t)R_remote,
+                            sc.pool_send.as<uint32_t>(), nullptr, pool_out_total};
+            hipLaunchKernelGGL((gather_rows_kernel<16, false>), dim3((unsigned)((R_remote + kBlock - 1) / kBlock)),
+                               dim3(kBlock), 0, s, gp);
             if (hipGetLastError() != hipSuccess) return fatal_receive(h, "pool gather launch");
         }
         std::vector<size_t> rs(G), rr(G), ps(G), pr(G);
@@ -1261,24 +1265,18 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
     }
     sc.last_M = M;
     sc.last_ready = true;
-    if (G > 1) {
-        sc.last_P = P;
-        *n_pairs = P;
-        if (P > 0xFFFFFFFFull) return set_error(h, WQ_E_CAPACITY, "more than 2^32-1 pairs in one tick");
-        return copy_out(h, d_offsets, d_peers, d_msgs, capacity);
-    }
-    // G = 1: P and the error bits from the tile scan's counters, read once the tick has run
     if ((rc = slots_copy_out(h, d_offsets, d_peers, d_msgs, capacity))) return rc;
+    // P and the error bits: the message-side tile scan's counters and the count pass's, read once
+    // the tick has run (the one host wait after the exchanges)
     wq_route_counters c[2];
     WQ_HIP(h, hipMemcpyAsync(&c[0], small + kSmallCnt, sizeof(c[0]), hipMemcpyDeviceToHost, s));
     if (cur) WQ_HIP(h, hipMemcpyAsync(&c[1], cur, sizeof(c[1]), hipMemcpyDeviceToHost, s));
     else c[1] = wq_route_counters{};
     WQ_HIP(h, hipStreamSynchronize(s));
     const uint32_t err = c[0].error | c[1].error;
-    P = M ? c[0].n_pairs : 0;
+    const uint64_t P = M ? c[0].n_pairs : 0;
     sc.last_P = P;
     *n_pairs = P;
-    if (err & kErrStale) return status_error(h, (uint64_t)kErrStale << 32, me);
     if (err) return status_error(h, (uint64_t)err << 32, me);
     if (P > capacity) return set_error(h, WQ_E_CAPACITY, "sharded tick: output capacity too small (required size in *n_pairs)");
     return WQ_OK;
@@ -1381,6 +1379,12 @@ int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_
     }
     if (sc.ret_e.ensure((M ? M : 1) * 4) != hipSuccess || sc.ret_peers.ensure((P ? P : 1) * 4) != hipSuccess)
         return fatal_receive(h, "hipMalloc of the returned pairs");
+    sc.last_sent = sc.last_recv = 0;
+    for (uint32_t d = 0; d < G; ++d)
+        if (d != me) {
+            sc.last_sent += 4 + (uint64_t)sc.sc[d] * sizeof(wq_msg_rec) + 16 + eb_s[d] + pb_s[d];
+            sc.last_recv += 4 + (uint64_t)sc.rc[d] * sizeof(wq_msg_rec) + 16 + eb_r[d] + pb_r[d];
+        }
     {
         Xfer x{{sc.own_e.p, sc.own_peers.p}, {eb_s.data(), pb_s.data()}, {sc.ret_e.p, sc.ret_peers.p},
                {eb_r.data(), pb_r.data()}, 2};
