@@ -229,7 +229,35 @@ def run_c3(a, rank, world_size, local_rank, dev):
                 "synthetic (splitmix64, SURVEY.md §8(d) C3 generator)")
     if not a.no_cpu_baseline:
         out["cpu_baseline"] = _cpu_route_sample(w, a.cpu_seconds, "C3")
+        threads = min(16, os.cpu_count() or 1)
+        if threads > 1:  # SURVEY.md §8(d) cpu_ref_mt: the same restatement on the host's cores
+            out["cpu_baseline_mt"] = bench.cpu_baseline_mt(w, threads)
+    out["xgmi_model"] = _xgmi_model()
     r.close()
+    return out
+
+
+XGMI_G8 = "r03_c3_xgmi_g8.json"  # tools/shard_volume.py --G 8: full C3 as 8 hub shards on one GPU
+XGMI_LINK_GBS = 64.0  # one xGMI link, one direction, sustained (MI355X_MICROARCH.md: ~153 GB/s per link both ways)
+
+
+def _xgmi_model():
+    """What an 8-GPU cube-hash tick of this workload moves between GPUs, per GPU — measured, not
+    estimated: tools/shard_volume.py runs the sharded tick with G = 8 hub shards on one GPU and
+    reads wq_shard_last_bytes (the bytes each shard sends to / receives from the other seven).
+    link_us: that volume spread over the 7 links of a GPU at XGMI_LINK_GBS each (a lower bound on
+    the exchange time; the exchanges themselves are not overlapped with compute)."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", XGMI_G8)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    out = {"n_gpus": d["G"], "source": "profiles/" + XGMI_G8 + " (tools/shard_volume.py)"}
+    for form in ("slots", "expanded"):
+        b = d[form]["sent_bytes_per_gpu_max"]
+        out[form] = {"xgmi_bytes_per_gpu": b, "link_us": round(b / (7 * XGMI_LINK_GBS * 1e3), 1)}
+    out["note"] = ("slots = the sharded tick's default (20-byte slots out, row references + one pool of cube lists "
+                   "per destination back); expanded = 40-byte records out, expanded pairs back")
     return out
 
 
@@ -285,19 +313,23 @@ def _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s):
         tick()
     t_ms = timed_ticks(tick, a.steps, stream, dev, world_size, [r])
     t_max_ms, pairs_all = reduce_over_ranks(t_ms, state["P"], dev, world_size)
+    sent, _ = r.shard_last_bytes()  # the last timed tick's bytes to the other GPUs (xGMI)
+    sent_max, _ = reduce_over_ranks(float(sent), 0, dev, world_size)
     out = _line(a, world_size, pairs_all * a.steps / (t_max_ms / 1e3), t_max_ms / a.steps, "strong",
                 f"C3 over {world_size} GPUs by cube hash: 1M peers x 3x3x3, 10M LocalMessages/tick in total, "
                 "256 Zipf(1) Gaussian hotspots + 10% uniform, cube_size 16, ExceptSelf"
                 + ("" if a.scale == 1.0 else f" (scaled {a.scale})"),
                 {"messages_per_tick": M_all, "messages_per_gpu": M, "peers": w.n_peers,
                  "subscriptions_this_shard": int(st["n_entries"]), "pairs_per_tick": int(pairs_all),
-                 "parallelism": f"cube-hash x{world_size} (wq_sharded_route_tick_device, RCCL all-to-all: records "
-                                "out, pairs back)",
-                 "table_build_s": round(build_s, 3), "generate_s": round(gen_s, 1)},
+                 "parallelism": f"cube-hash x{world_size} (wq_sharded_route_tick_device over RCCL: 20-byte slots "
+                                "out, row references + per-destination cube-list pools back)",
+                 "xgmi_bytes_per_gpu": int(sent_max), "table_build_s": round(build_s, 3),
+                 "generate_s": round(gen_s, 1)},
                 roofline(algorithmic_bytes(M_all, int(pairs_all), int(pairs_all)) // world_size, t_max_ms / a.steps / 1e3,
                          "whole sharded tick per GPU (shard + exchanges + owner route + unshard); bytes = the "
                          "tick's SURVEY §8(d) bytes / N"),
                 "synthetic (splitmix64, SURVEY.md §8(d) C3 generator)")
+    out["xgmi_model"] = _xgmi_model()
     if not a.no_extra:
         # SURVEY.md §8(e) step 5's other option: the same collective tick with the pairs left on the
         # owner that routed them (wq_sharded_route_owner_device) — no return exchange
@@ -600,7 +632,8 @@ def _cpu_c5_sample(init, tick_ops, pos_after, radius, seconds):
         done += len(chunk)
     faith.close()
     t_tick = t_route + n_ops * (t_ops / done)
-    return {"value": P / t_tick, "unit": "pairs/s", "cores": 1, "kind": "port",
+    # an estimate, not a measured tick: the churn part is a sample scaled to the whole tick
+    return {"value": P / t_tick, "unit": "pairs/s", "cores": 1, "kind": "estimate",
             "sample": f"C5 tick estimate: {M} messages routed with the radius filter in {t_route:.2f} s "
                       f"({P} pairs) + {done} of the tick's {n_ops} churn ops (every {stride}th) applied with the "
                       f"reference's O(#cubes) unsubscribe scan in {t_ops:.2f} s, scaled to all {n_ops} ops: "
