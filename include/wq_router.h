@@ -136,8 +136,9 @@ int wq_apply_ops(wq_router* h, const wq_op* ops, size_t n);
  * (an op whose key has no packed form — NaN / huge coordinates, off-grid raw keys, world ids
  * >= 2^24 - 1 — or list space exhausted) is re-applied from it by the rebuild then, and routes
  * issued in between report error bit 8 (WQ stale table) in their counters and in
- * wq_route_health. An invalid op (REMOVE_PEER kind, reserved world) in such a batch is reported
- * as WQ_E_INVALID by that next call, with the table left as before the batch. */
+ * wq_route_health. A batch holding an invalid op (REMOVE_PEER kind, reserved world) is not applied at
+ * all (the table stays as before it); the next call on the handle still does its own work in full
+ * and leaves the rejection in wq_last_error and as error bit 16 of wq_route_health. */
 int wq_apply_ops_device(wq_router* h, const wq_op* d_ops, size_t n);
 /* WorldMap::remove_peer for n peers (every world), world_map.rs:41-61. */
 int wq_remove_peers(wq_router* h, const uint32_t* peers, size_t n);
@@ -355,7 +356,8 @@ int wq_peer_major_device(wq_router* h, const uint32_t* d_offsets, const uint32_t
  * normal tick never writes them, so a caller that runs many _device ticks without reading their
  * counters checks the whole run here: error bit 4 = a bounded spin gave up (WQ_E_TIMEOUT), 2 =
  * more than 2^32-1 pairs in one tick, 8 = a tick ran on a table still missing an incremental
- * batch (wq_apply_ops_device); overflow = some tick's pairs exceeded its capacity. */
+ * batch (wq_apply_ops_device), 16 = a device op batch held an invalid op and was not applied;
+ * overflow = some tick's pairs exceeded its capacity. */
 int wq_route_health(wq_router* h, uint32_t* error_bits, uint32_t* overflow);
 
 /* ---- instrumentation ----

@@ -292,3 +292,39 @@ def test_device_batch_without_packed_key_is_reapplied():
     _check(r, o, pos, world, sender, repl)
     assert r.route_health() == (0, 0)
     del d_ops
+
+
+def test_invalid_device_batch_does_not_drop_the_next_call():
+    """A device batch holding an invalid op (REMOVE_PEER kind) is not applied; the next call on the
+    handle — a valid host batch here — still does its own work, and the rejection shows as error
+    bit 16 of wq_route_health."""
+    import torch
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(37)
+    r, o = mk_router(), orc.COracle(16)
+    r.set_stream(torch.cuda.current_stream().cuda_stream)
+    base = _random_ops(rng, 40000, 2, 3000, 128.0, 1.0)
+    r.apply_ops(base)
+    o.apply_ops(base)
+    bad = abi.concat_ops([_random_ops(rng, 500, 2, 3000, 128.0, 1.0),
+                          abi.ops_array(np.zeros(1, np.uint32), np.array([9], np.uint32),
+                                        np.full(1, abi.OP_REMOVE_PEER, np.uint8), pos=np.zeros((1, 3)))])
+    d_ops = torch.from_numpy(np.ascontiguousarray(bad).view(np.uint8).copy()).to(dev)
+    r.apply_ops_device(d_ops.data_ptr(), len(bad))  # rejected on the device: nothing of it applies
+    good = _random_ops(rng, 800, 2, 3000, 128.0, 1.0)
+    r.apply_ops(good)  # folds the rejected batch in, then applies its own ops in full
+    o.apply_ops(good)
+    got = r.is_subscribed(good["world"], good["peer"], False, good["pos"])
+    want = np.array([o.is_subscribed(int(x["world"]), int(x["peer"]), False, x["pos"]) for x in good])
+    assert (got == want).all() and got.any()
+    assert r.stats()["n_entries"] == o.counts()[0]
+    e, _ = r.route_health()
+    assert e & 16
+    M = 2000
+    pos = rng.uniform(-130, 130, (M, 3))
+    world = rng.integers(0, 2, M).astype(np.uint32)
+    sender = rng.integers(0, 3000, M).astype(np.uint32)
+    repl = rng.integers(0, 3, M).astype(np.uint8)
+    _check(r, o, pos, world, sender, repl)
+    assert r.route_health() == (0, 0)
+    del d_ops

@@ -1327,8 +1327,24 @@ int table_resolve(wq_router* h, bool blocking) {
     h->n_delta_applies--;
     WQ_HIP(h, hipMemsetAsync(t.stale.p, 0, 4, h->stream));
     if (hs.flags & 2u) {
+        // the batch held an invalid op and was not applied (the table is as before it). The call
+        // folding it in goes on with its own work; the rejection stays visible in wq_last_error and
+        // as error bit 16 of wq_route_health (no silently dropped call)
         WQ_HIP(h, hipStreamSynchronize(h->stream));
-        return set_error(h, WQ_E_INVALID, "bad op (kind or reserved world id) in an earlier device batch");
+        RouteWs& rw = h->rws;
+        if (!rw.buf.p) {  // as route_counters lays it out: health words first
+            WQ_ALLOC(h, rw.buf, 128);
+            WQ_HIP(h, hipMemsetAsync(rw.buf.p, 0, 128, h->stream));
+            rw.calls = 0;
+        }
+        uint32_t w = 0;
+        WQ_HIP(h, hipMemcpyAsync(&w, rw.buf.p, 4, hipMemcpyDeviceToHost, h->stream));
+        WQ_HIP(h, hipStreamSynchronize(h->stream));
+        w |= kErrBadBatch;
+        WQ_HIP(h, hipMemcpyAsync(rw.buf.p, &w, 4, hipMemcpyHostToDevice, h->stream));
+        WQ_HIP(h, hipStreamSynchronize(h->stream));
+        h->err = "bad op (kind or reserved world id) in an earlier device batch: that batch was not applied";
+        return WQ_OK;
     }
     h->n_delta_fallbacks++;
     h->cur_ops = pd.ops;

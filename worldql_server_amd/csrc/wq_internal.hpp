@@ -12,6 +12,9 @@
 
 namespace wq {
 
+// wq_route_health error bit 16: a device op batch held an invalid op and was not applied.
+constexpr uint32_t kErrBadBatch = 16u;
+
 // Grow-only device buffer.
 struct DevBuf {
     void* p = nullptr;

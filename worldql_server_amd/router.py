@@ -431,6 +431,9 @@ class Router:
     def check_health(self) -> None:
         """Raises WQError when any tick since the last check reported an error or an overflow."""
         e, o = self.route_health()
+        if e & 16:
+            raise WQError(abi.WQ_E_INVALID, f"a device op batch held an invalid op and was not applied "
+                                            f"(error bits {e:#x})")
         if e & 8:
             raise WQError(abi.WQ_E_INVALID, f"a tick ran on a table still missing an incremental batch the "
                                             f"device could not apply (error bits {e:#x})")

@@ -154,6 +154,9 @@ class DeviceShard:
     def check_counters(words) -> None:
         """Raises when a route call reported an error (host copy of counters_i64)."""
         err = (int(words[2]) >> 32) & 0xFFFFFFFF
+        if err & 8:  # as Router.check_health: the table still misses a batch the device could not apply
+            raise RuntimeError(f"wq error {abi.WQ_E_INVALID}: a tick ran on a table still missing an incremental "
+                               f"batch the device could not apply (error bits {err:#x})")
         if err:
             code = abi.WQ_E_TIMEOUT if err & 4 else abi.WQ_E_CAPACITY
             raise RuntimeError(f"wq error {code}: route counters report error bits {err:#x}")
