@@ -18,11 +18,15 @@ It restates, with a bytearray that grows at the front:
   are written last element first, `push_slot` skips a scalar equal to its default, `write_vtable`
   writes the soffset, then the vtable right below the table, and erases it again when a
   byte-identical vtable was already written in this buffer; `finish` aligns to the largest
-  alignment seen and writes the root uoffset.
+  alignment seen and writes the root uoffset. A struct is pushed under its Push::alignment(), whose
+  default is align_of::<Output>(): Vec3d (WorldQLFB_generated.rs:254-298) is a repr(transparent)
+  [u8; 24] with that default, so positions are pushed with alignment 1 — no padding, min_align
+  unchanged — despite the schema's "aligned to 8" comment.
 
 Parity: UNPINNED at the byte level — the reference is Rust, cannot be built here,
-and holds no serialized frames. The layout is pinned only by this restatement, by a hand-derived
-known-answer frame (tests/test_codec_serialize.py) and semantically by decoding every frame back
+and holds no serialized frames. The layout is pinned only by this restatement, by two hand-derived
+known-answer frames (tests/test_codec_serialize.py: a Handshake, and a LocalMessage with a position,
+one Record and one Entity) and semantically by decoding every frame back
 with the verifier restatement in fbs_oracle.py.
 """
 from __future__ import annotations

@@ -42,6 +42,66 @@ def _handshake_kat() -> bytes:
     return struct.pack("<I", 24) + b"\0\0" + vt + table + tail
 
 
+def _local_message_kat() -> bytes:
+    """LocalMessage { sender 0…0, world "w", position (1, 2, 3), records [Record { uuid 0…0, world "w",
+    data "d" }], entities [Entity { uuid 0…0, world "w", position (4, 5, 6) }] }, laid out by hand in
+    MessageT::pack order (WorldQLFB_generated.rs:1133-1173; RecordT/EntityT::pack :619-645, :838-864)
+    — 328 bytes. Vec3d (:254-298) is `#[repr(transparent)] struct Vec3d([u8; 24])` and its Push impl
+    keeps the trait's default alignment, align_of::<Vec3d>() = 1 (flatbuffers 2.0.0 src/push.rs), so a
+    position is pushed with NO padding and does not raise min_align: the message position lands at
+    byte 48 and the entity's at byte 100 (not 8-aligned), although the schema comment says "aligned
+    to 8". revloc = bytes used from the end after each step:
+      sender : pad 3, NUL, 36, len                                     -> 44
+      world  : pad 2, "w" NUL, len                                     -> 52
+      record : uuid str -> 96, world str -> 104, data str -> 112 (table start);
+               data @116 (4), world @120 (16), uuid @124 (28), soffset -> 128 (size 16);
+               vtable 12 bytes (slots 4, 6 = 0, 8, 10) -> 140, soffset 12
+      records: uoffset 16 -> 144, len 1 -> 148
+      entity : uuid str -> 192, world str -> 200 (table start);
+               world @204 (4), position 24 bytes @228 (no pad), uuid @232 (40), soffset -> 236 (size 36);
+               vtable 10 bytes (slots 4, 6, 8) -> 246, soffset 10
+      entities: pad 2 -> 248, uoffset 16 -> 252, len 1 -> 256 (message table start)
+      message: position @280, entities @284 (28), records @288 (140), world @292 (240),
+               sender @296 (252), replication 0 = default (omitted), instruction 7 @297,
+               pad 3, soffset -> 304 (size 48); vtable 20 bytes (slot 18) -> 324, soffset 20
+      finish : min_align 4, no pad; root uoffset 328 - 304 = 24
+    """
+    zero = str(uuid.UUID(int=0)).encode()
+
+    def s(raw):  # len, bytes, NUL, zero pad to 4
+        b = struct.pack("<I", len(raw)) + raw + b"\0"
+        return b + b"\0" * (-len(b) % 4)
+
+    msg_vt = struct.pack("<10H", 20, 48, 7, 0, 8, 12, 0, 16, 20, 24)
+    msg_table = struct.pack("<i", 20) + b"\0\0\0\x07" + struct.pack("<4I", 252, 240, 140, 28) + \
+        struct.pack("<3d", 1.0, 2.0, 3.0)
+    ents = struct.pack("<2I", 1, 16) + b"\0\0"
+    ent_vt = struct.pack("<5H", 10, 36, 4, 8, 32)
+    ent_table = struct.pack("<iI", 10, 40) + struct.pack("<3d", 4.0, 5.0, 6.0) + struct.pack("<I", 4)
+    recs = struct.pack("<2I", 1, 16)
+    rec_vt = struct.pack("<6H", 12, 16, 4, 0, 8, 12)
+    rec_table = struct.pack("<i3I", 12, 28, 16, 4)
+    out = struct.pack("<I", 24) + msg_vt + msg_table + ents + ent_vt + ent_table + s(b"w") + s(zero) + \
+        recs + rec_vt + rec_table + s(b"d") + s(b"w") + s(zero) + s(b"w") + s(zero)
+    assert struct.unpack_from("<3d", out, 48) == (1.0, 2.0, 3.0) and struct.unpack_from("<3d", out, 100) == (4.0, 5.0, 6.0)
+    return out
+
+
+def test_local_message_known_answer():
+    want = _local_message_kat()
+    assert len(want) == 328
+    z = bytes(16)
+    m = dict(instruction=7, sender_uuid=z, world_name="w", position=(1.0, 2.0, 3.0),
+             records=[dict(uuid=z, world_name="w", data="d")],
+             entities=[dict(uuid=z, world_name="w", position=(4.0, 5.0, 6.0))])
+    assert fbs_serialize.serialize(m) == want
+    assert codec.serialize_message(m) == want
+    assert read_back(want) == _normal(m)
+    d = fbs_oracle.decode(want)
+    assert d["status"] == 0 and d["instruction"] == 7 and d["world"] == b"w"
+    assert d["n_records"] == 1 and d["n_entities"] == 1
+
+
 def test_handshake_known_answer():
     want = _handshake_kat()
     assert len(want) == 108
