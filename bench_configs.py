@@ -582,7 +582,7 @@ def run_c5(a, rank, world_size, local_rank, dev):
                  "parallelism": "1 GPU", "table_build_s": round(build_s, 3), "generate_s": round(gen_s, 1)},
                 {"bound": "hbm", "achieved": B / (res["t_ms"] / steps / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
                  "unit": "GB/s", "frac": B / (res["t_ms"] / steps / 1e3) / 1e9 / HBM_PEAK_GBS,
-                 "traffic": _pmc_tick_traffic("r02_pmc_c5.json", a.scale),
+                 "traffic": _pmc_tick_traffic("r03_pmc_c5.json", a.scale),
                  "kernel": "whole tick (incremental update + positions + radius route); route launches alone below",
                  "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
                 "synthetic (splitmix64, SURVEY.md §8(d) C5 generator)")

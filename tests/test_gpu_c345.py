@@ -176,3 +176,46 @@ def test_c4_churn_ticks_vs_oracle():
         assert P > 0
     for wid in (0, 4, 60):
         assert (r.world_peers(wid) == o.world_peers(wid)).all()
+
+
+def test_radius_position_code_edges():
+    """The first radius test reads a 4-byte code per peer (x, y on 11 bits, z on 10, over the
+    positions' bounding box) and decides only when the reference's f64 result is certain; the
+    rest go to the f32 and f64 tests. Peers in a 64-unit box (steps of ~0.03 / 0.06) at distances
+    straddling the code's uncertainty band and the exact sphere, on a long list and an inline cube,
+    every replication mode; then the same peers in a 1e6-unit box (steps ~500: every code defers)."""
+    rng = synth.SplitMix64(41)
+    n_a, n_b = 70, 22
+    centre_a, centre_b = np.array([3.3, -2.1, 5.7]), np.array([-20.5, 14.25, -9.0])
+    peer = np.arange(n_a + n_b, dtype=np.uint32)
+    sub = np.concatenate([np.tile(centre_a, (n_a, 1)), np.tile(centre_b, (n_b, 1))])
+    ops = abi.ops_array(np.zeros(len(peer), np.uint32), peer, np.zeros(len(peer), np.uint8), pos=sub)
+    radius = 5.0
+    u = rng.uniform(-1.0, 1.0, 3 * (n_a + n_b)).reshape(-1, 3)
+    u /= np.linalg.norm(u, axis=1)[:, None]
+    d = radius + rng.uniform(-0.12, 0.12, n_a + n_b)   # across the code's band (~0.05 wide here)
+    d[::7] = radius                                     # on the sphere (to rounding)
+    pp = np.concatenate([centre_a + d[:n_a, None] * u[:n_a], centre_b + d[n_a:, None] * u[n_a:]])
+    pp[3] = centre_a + [radius, 0.0, 0.0]               # d2 == r2 exactly
+    pp[4] = centre_a + [0.0, 0.0, -radius]
+    pp[5] = [np.nan, 1.0, 1.0]                          # no code: the f32 / f64 tests decide
+    pp[6] = [32.0, 32.0, -32.0]                         # a box corner
+    pp[7] = [-32.0, -32.0, 32.0]
+    M = 400
+    mpos = np.where((np.arange(M) % 2 == 0)[:, None], centre_a[None, :], centre_b[None, :])
+    mpos = mpos + np.where((np.arange(M) % 3 == 0)[:, None], rng.uniform(-0.5, 0.5, 3 * M).reshape(M, 3), 0.0)
+    sender = rng.below(n_a + n_b, M)
+    repl = rng.below(3, M).astype(np.uint8)
+    for scale in (1.0, 1e6):
+        q = pp.copy()
+        if scale != 1.0:
+            q[8] = [scale, -scale, scale]  # a far peer widens the box: every code step ~500 units
+        r, o = mk_router(), orc.COracle(16)
+        r.apply_ops(ops)
+        o.apply_ops(ops)
+        r.set_peer_positions(q)
+        r.set_radius(radius)
+        got = r.route(mpos, np.zeros(M, np.uint32), sender, repl)
+        want = o.route_radius(mpos, np.zeros(M, np.uint32), sender, repl, q, radius)
+        assert _same(got, want) > 0
+        r.close()

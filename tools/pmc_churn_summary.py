@@ -1,6 +1,6 @@
 """Per-tick HBM traffic of a C4 / C5 bench run from tools/pmc_churn.sh: FETCH_SIZE (x2, the gfx950
 correction of MI355X_MICROARCH.md) + WRITE_SIZE summed over the tick's kernels (update: k_delta_*,
-k_sort_*, k_bucket_*; positions: k_pos_f32; route: count / scan / emit / tick kernels), divided by
+k_sort_*, k_bucket_*; positions: k_pos_f32 / k_pos_box / k_pos_code; route: count / scan / emit / tick kernels), divided by
 the ticks run (warmup + steps).
     python tools/pmc_churn_summary.py gpurun_out/pmc_c5 --ticks 12 [--json profiles/r02_pmc_c5.json]"""
 import argparse
@@ -10,7 +10,7 @@ import glob
 import json
 import os
 
-TICK = ("k_delta_", "k_sort_", "k_bucket_", "k_pos_f32", "count_radius_kernel", "count_kernel", "tile_scan_kernel",
+TICK = ("k_delta_", "k_sort_", "k_bucket_", "k_pos_", "count_radius_kernel", "count_kernel", "tile_scan_kernel",
         "tile_finish_kernel", "emit_kernel", "emit_map_kernel", "tick_kernel")
 
 

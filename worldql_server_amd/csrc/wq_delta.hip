@@ -1364,9 +1364,10 @@ int table_remove_peers_inplace(wq_router* h, const uint64_t* keys, size_t n_rm) 
     }
     const size_t n_one = n_rm - n_all;  // keys sort by world first: the every-world ones are last
     RemoveSet rs{nullptr, 0, nullptr, (uint32_t)n_one};
+    std::vector<uint32_t> bits;  // read by an asynchronous copy: lives until the synchronize below
     if (n_all) {
         const uint32_t words = max_all / 32 + 1;
-        std::vector<uint32_t> bits(words, 0u);
+        bits.assign(words, 0u);
         for (size_t i = n_one; i < n_rm; ++i) {
             const uint32_t p = (uint32_t)keys[i];
             bits[p >> 5] |= 1u << (p & 31);

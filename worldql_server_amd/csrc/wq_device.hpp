@@ -211,7 +211,11 @@ struct TableView {
     double sf;
     // C5 radius filter (wq_set_radius): peer positions (n_ppos x 3) and r^2; r2 < 0: off
     const double* ppos;
-    const float4* ppos4;  // the same positions rounded to f32 {x, y, z, 0}: the first, exact-or-defer test
+    const float4* ppos4;  // the same positions rounded to f32 {x, y, z, 0}: the second, exact-or-defer test
+    // the first test: 4 bytes per peer (4 MB for C5's 1M entities, mostly L2-resident, where the f32
+    // rows take 16 MB): x, y on 11 bits and z on 10 over the positions' bounding box (kQNone: no code)
+    const uint32_t* pcode;
+    const double* qbox;   // {lo x, lo y, lo z, step x, step y, step z} of the codes
     uint32_t n_ppos;
     double r2;
     // per-peer boxes of the record cubes each peer is subscribed to (PeerBox); nullptr: none
@@ -293,8 +297,59 @@ __device__ __forceinline__ bool radius_f64(const TableView& t, double mx, double
     return d2 <= t.r2;
 }
 
+// ---- the 4-byte position codes (the radius filter's first test) ----
+// code = ux | uy << 11 | uz << 22 with u_d = rint((p_d - lo_d) / step_d), steps = extent / 2047
+// (x, y) and / 1022 (z, so no code is all ones): the decoded q_d = lo_d + u_d * step_d (f64) lies
+// within e_d = step_d / 2 (1 + 2^-40) + (|lo_d| + |q_d| + u_d step_d) 2^-49 of p_d — the rounding of
+// the division, of rint's argument and of the decode are all inside that margin. Peers without a
+// finite position get kQNone and go to the f32 / f64 tests.
+constexpr uint32_t kQNone = 0xFFFFFFFFu;
+constexpr uint32_t kQMaxXY = 2047u, kQMaxZ = 1022u;
+
+__device__ __forceinline__ uint32_t pos_code(double x, double y, double z, const double* box) {
+    if (!(isfinite(x) && isfinite(y) && isfinite(z))) return kQNone;
+    const double u[3] = {rint((x - box[0]) / box[3]), rint((y - box[1]) / box[4]), rint((z - box[2]) / box[5])};
+    const double mx[3] = {(double)kQMaxXY, (double)kQMaxXY, (double)kQMaxZ};
+    uint32_t q[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const double c = u[d] < 0.0 ? 0.0 : (u[d] > mx[d] ? mx[d] : u[d]);
+        q[d] = (uint32_t)c;
+    }
+    return q[0] | (q[1] << 11) | (q[2] << 22);
+}
+
+// The code test: 1 = certainly within r, 0 = certainly not, -1 = ask the f32 / f64 tests. With
+// the decoded q, a = m - q is within e of the reference's dx = fl(m - p) (plus that subtraction's
+// rounding), so as in radius_f32_test the reference's f64 d2 lies within E of fl(a.a).
+__device__ __forceinline__ int radius_code_test(uint32_t code, const double* box, double mx, double my, double mz,
+                                                double r2) {
+    if (code == kQNone) return -1;
+    const uint32_t u[3] = {code & kQMaxXY, (code >> 11) & kQMaxXY, code >> 22};
+    const double m[3] = {mx, my, mz};
+    double d2 = 0.0, E1 = 0.0;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const double ud = (double)u[d];
+        const double q = box[d] + ud * box[3 + d];
+        const double a = m[d] - q;
+        const double e = box[3 + d] * 0.5 * (1.0 + 0x1p-40) + (fabs(box[d]) + fabs(q) + ud * box[3 + d]) * 0x1p-49 +
+                         fabs(a) * 0x1p-50 + 0x1p-1000;
+        d2 += a * a;
+        E1 += e * (2.0 * fabs(a) + e);
+    }
+    const double E = E1 * 1.001 + d2 * 0x1p-40 + 0x1p-1000;
+    if (d2 + E <= r2) return 1;  // NaN (a message without a finite position): false
+    if (d2 - E > r2) return 0;
+    return -1;
+}
+
 __device__ __forceinline__ bool within_radius(const TableView& t, double mx, double my, double mz, uint32_t p) {
     if (p >= t.n_ppos) return false;
+    if (t.pcode) {
+        const int c = radius_code_test(t.pcode[p], t.qbox, mx, my, mz, t.r2);
+        if (c >= 0) return c > 0;
+    }
     const int d = radius_f32_test(t.ppos4[p], mx, my, mz, t.r2);
     return d >= 0 ? d > 0 : radius_f64(t, mx, my, mz, p);
 }

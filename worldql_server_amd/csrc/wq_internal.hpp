@@ -160,7 +160,9 @@ struct wq_router {
     wq::DevBuf h_in, h_out;
     // C5 radius filter (wq_set_radius / wq_set_peer_positions)
     wq::DevBuf ppos;
-    wq::DevBuf ppos4;  // f32 copy (float4 per peer) for the radius filter's first test
+    wq::DevBuf ppos4;  // f32 copy (float4 per peer) for the radius filter's second test
+    wq::DevBuf pcode;  // 4-byte position codes (the first test) and their box (wq_device.hpp)
+    wq::DevBuf qbox;   // u64 box keys [0, 6), then {lo, step} doubles [6, 12)
     uint64_t n_ppos = 0;
     double radius = 0.0;
     wq::ProfileEvents prof;
@@ -184,6 +186,8 @@ inline TableView table_view(const wq_router* h) {
     v.sf = (double)h->cube_size;
     v.ppos = h->ppos.as<double>();
     v.ppos4 = h->ppos4.as<float4>();
+    v.pcode = h->n_ppos ? h->pcode.as<uint32_t>() : nullptr;
+    v.qbox = h->qbox.p ? reinterpret_cast<const double*>(h->qbox.as<uint64_t>() + 6) : nullptr;
     v.n_ppos = (uint32_t)h->n_ppos;
     v.r2 = h->radius > 0.0 ? h->radius * h->radius : -1.0;
     v.n_pbox = h->tab.n_pbox;

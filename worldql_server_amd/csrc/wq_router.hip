@@ -142,7 +142,7 @@ int wq_router_destroy(wq_router* h) {
                       &h->key64_b, &h->flags, &h->scan, &h->sort_tmp, &h->small, &h->cube_id,
                       &h->cube_start, &h->rws.buf, &h->rws.info, &h->rws.e, &h->rws.tiles,
                       &h->h_in, &h->h_out, &h->tab.recs, &h->tab.rclaim, &h->tab.pbox, &h->shard_hist,
-                      &h->rec_keys, &h->rec_w, &h->rec_s, &h->rec_r, &h->ppos, &h->ppos4, &h->rws.agg, &h->rws.spill, &h->rws.scan_tmp,
+                      &h->rec_keys, &h->rec_w, &h->rec_s, &h->rec_r, &h->ppos, &h->ppos4, &h->pcode, &h->qbox, &h->rws.agg, &h->rws.spill, &h->rws.scan_tmp,
                       &h->dws.part, &h->dws.summ, &h->dws.dstat, &h->dws.rm_bits, &h->tab.stale};
     for (DevBuf* b : bufs) b->release();
     if (h->pend.ev) (void)hipEventDestroy(h->pend.ev);
@@ -194,6 +194,91 @@ static __global__ void k_pos_f32(const double* __restrict__ pos, uint64_t n, flo
     }
 }
 
+// The positions' bounding box (finite coordinates only) as order-preserving u64 keys: 6 words
+// {min x, y, z, max x, y, z}; a few hundred blocks, one atomic per block and word.
+__device__ __forceinline__ uint64_t ord_key(double x) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+__device__ __forceinline__ double ord_val(uint64_t k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & ~(1ull << 63)) : ~k));
+}
+
+static __global__ __launch_bounds__(256) void k_pos_box(const double* __restrict__ pos, uint64_t n,
+                                                        unsigned long long* __restrict__ box) {
+    __shared__ uint64_t part[4][6];
+    uint64_t lo[3] = {~0ull, ~0ull, ~0ull}, hi[3] = {0, 0, 0};
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const double v[3] = {pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]};
+        if (!(isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]))) continue;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const uint64_t k = ord_key(v[d]);
+            lo[d] = k < lo[d] ? k : lo[d];
+            hi[d] = k > hi[d] ? k : hi[d];
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint64_t a = __shfl_xor(lo[d], o, 64), b = __shfl_xor(hi[d], o, 64);
+            lo[d] = a < lo[d] ? a : lo[d];
+            hi[d] = b > hi[d] ? b : hi[d];
+        }
+    if ((threadIdx.x & 63) == 0)
+        for (int d = 0; d < 3; ++d) {
+            part[threadIdx.x >> 6][d] = lo[d];
+            part[threadIdx.x >> 6][3 + d] = hi[d];
+        }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        uint64_t v = part[0][threadIdx.x];
+        for (int w = 1; w < 4; ++w) {
+            const uint64_t x = part[w][threadIdx.x];
+            v = threadIdx.x < 3 ? (x < v ? x : v) : (x > v ? x : v);
+        }
+        if (threadIdx.x < 3) atomicMin(box + threadIdx.x, (unsigned long long)v);
+        else atomicMax(box + threadIdx.x, (unsigned long long)v);
+    }
+}
+
+// The box -> {lo, step} (kept at box + 6 as doubles for the count pass) and every peer's code.
+static __global__ __launch_bounds__(256) void k_pos_code(const double* __restrict__ pos, uint64_t n,
+                                                         unsigned long long* __restrict__ box, uint32_t* __restrict__ code) {
+    double qb[6];
+    bool any = true;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const uint64_t klo = box[d], khi = box[3 + d];
+        any = any && klo <= khi;  // no finite position at all: klo = ~0, khi = 0
+        const double lo = ord_val(klo), hi = ord_val(khi);
+        const double steps = d < 2 ? (double)kQMaxXY : (double)kQMaxZ;
+        qb[d] = lo;
+        qb[3 + d] = hi > lo ? (hi - lo) / steps : 1.0;
+    }
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) {
+        double* out = reinterpret_cast<double*>(box + 6);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) out[k] = qb[k];
+    }
+    if (i >= n) return;
+    const double x = pos[3 * i], y = pos[3 * i + 1], z = pos[3 * i + 2];
+    uint32_t c = any ? pos_code(x, y, z, qb) : kQNone;
+    if (c != kQNone) {  // belt and braces: a code must decode within half a step (+ rounding)
+        const uint32_t u[3] = {c & kQMaxXY, (c >> 11) & kQMaxXY, c >> 22};
+        const double v[3] = {x, y, z};
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const double q = qb[d] + (double)u[d] * qb[3 + d];
+            if (!(fabs(v[d] - q) <= qb[3 + d] * 0.5 * (1.0 + 0x1p-40) + (fabs(qb[d]) + fabs(q) + (double)u[d] * qb[3 + d]) * 0x1p-49))
+                c = kQNone;
+        }
+    }
+    code[i] = c;
+}
+
 static int set_peer_positions(wq_router* h, const double* pos, size_t n, hipMemcpyKind kind) {
     if (!h || (n && !pos) || n > 0xFFFFFFFFull) return WQ_E_INVALID;
     WQ_HIP(h, hipSetDevice(h->device));
@@ -202,10 +287,21 @@ static int set_peer_positions(wq_router* h, const double* pos, size_t n, hipMemc
     WQ_ALLOC(h, h->ppos4, (n ? n : 1) * 16);
     const bool d2d = kind == hipMemcpyDeviceToDevice;
     if (n && !d2d) WQ_HIP(h, hipMemcpyAsync(h->ppos.p, pos, n * 24, kind, h->stream));
+    WQ_ALLOC(h, h->pcode, (n ? n : 1) * 4);
+    WQ_ALLOC(h, h->qbox, 128);
     if (n) {
         hipLaunchKernelGGL(k_pos_f32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream,
                            d2d ? pos : h->ppos.as<double>(), (uint64_t)n, h->ppos4.as<float4>(),
                            d2d ? h->ppos.as<double>() : nullptr);
+        WQ_HIP(h, hipGetLastError());
+        // the 4-byte codes of the radius filter's first test: bounding box, then one code per peer
+        WQ_HIP(h, hipMemsetAsync(h->qbox.p, 0xFF, 24, h->stream));  // min keys: all ones
+        WQ_HIP(h, hipMemsetAsync(h->qbox.as<uint64_t>() + 3, 0, 24, h->stream));  // max keys: zero
+        const unsigned gb = (unsigned)std::min<size_t>(256, (n + 255) / 256);
+        hipLaunchKernelGGL(k_pos_box, dim3(gb), dim3(256), 0, h->stream, h->ppos.as<double>(), (uint64_t)n,
+                           h->qbox.as<unsigned long long>());
+        hipLaunchKernelGGL(k_pos_code, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream,
+                           h->ppos.as<double>(), (uint64_t)n, h->qbox.as<unsigned long long>(), h->pcode.as<uint32_t>());
         WQ_HIP(h, hipGetLastError());
     }
     if (kind == hipMemcpyHostToDevice) WQ_HIP(h, hipStreamSynchronize(h->stream));

@@ -1039,10 +1039,12 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
         !fail(alloc(sc.self_w, (M + 1) * 4)))
         fail(launch_shard_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, sc.slots.as<uint32_t>(),
                                 sc.perm.as<uint32_t>(), a_send, 2));
+    // host sources of status copies live until the call's host reads have synchronised the stream
+    std::vector<uint32_t> a_status(2 * G, 0);
+    std::vector<unsigned long long> c_status(4 * G, 0);
     if (late) {  // nothing to send: zero slots everywhere, and the status
-        std::vector<uint32_t> v(2 * G, 0);
-        for (uint32_t d = 0; d < G; ++d) v[2 * d + 1] = status_of(late);
-        WQ_HIP(h, hipMemcpyAsync(a_send, v.data(), 8 * G, hipMemcpyHostToDevice, s));
+        for (uint32_t d = 0; d < G; ++d) a_status[2 * d + 1] = status_of(late);
+        WQ_HIP(h, hipMemcpyAsync(a_send, a_status.data(), 8 * G, hipMemcpyHostToDevice, s));
     }
     std::vector<size_t> eight(G, 8), thirty2(G, 32);
     int rc;
@@ -1185,9 +1187,8 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
             if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "size launch (sharded tick)"));
         }
         if (late) {  // nothing routed here: zero sizes and the status
-            std::vector<unsigned long long> v(4 * G, 0);
-            for (uint32_t d = 0; d < G; ++d) v[4 * d + 2] = status_of(late);
-            WQ_HIP(h, hipMemcpyAsync(c_send, v.data(), 32 * G, hipMemcpyHostToDevice, s));
+            for (uint32_t d = 0; d < G; ++d) c_status[4 * d + 2] = status_of(late);
+            WQ_HIP(h, hipMemcpyAsync(c_send, c_status.data(), 32 * G, hipMemcpyHostToDevice, s));
         }
         {
             Xfer x{{c_send}, {thirty2.data()}, {c_recv}, {thirty2.data()}, 1};
@@ -1334,10 +1335,10 @@ int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_
                            R ? h->rws.last : nullptr, h->tab.stale.as<uint32_t>());
         if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "owner counts launch"));
     }
+    std::vector<unsigned long long> pc_status(2 * G, 0);  // lives until host read 2 below
     if (late) {
-        std::vector<unsigned long long> v(2 * G, 0);
-        for (uint32_t d = 0; d < G; ++d) v[2 * d + 1] = status_of(late);
-        WQ_HIP(h, hipMemcpyAsync(pc_send, v.data(), 16 * G, hipMemcpyHostToDevice, s));
+        for (uint32_t d = 0; d < G; ++d) pc_status[2 * d + 1] = status_of(late);
+        WQ_HIP(h, hipMemcpyAsync(pc_send, pc_status.data(), 16 * G, hipMemcpyHostToDevice, s));
     }
     {
         Xfer x{{pc_send}, {sixteen.data()}, {pc_recv}, {sixteen.data()}, 1};
