@@ -227,6 +227,20 @@ def run_c3(a, rank, world_size, local_rank, dev):
                  "parallelism": "1 GPU", "table_build_s": round(build_s, 3), "generate_s": round(gen_s, 1)},
                 roofline(B, t_ms / a.steps / 1e3, kernel, _pmc_traffic(PMC_C3, M, P), k_avg_s * 1e6),
                 "synthetic (splitmix64, SURVEY.md §8(d) C3 generator)")
+    # SURVEY.md §8(b)'s output contract proper: CSR offsets[M+1] + peers[P], msgs = NULL (no per-pair
+    # message index: the caller hands message m its slice peers[offsets[m] .. offsets[m+1]) as
+    # broadcast_to does). Same tick, same inputs; its peers are checked equal to the full form's.
+    ref_offs, ref_peers = offs.clone(), peers[:P].clone()
+    args_csr = args[:7] + (0, cap)
+    t2_ms = timed_ticks(lambda: r.route_device(*args_csr, 0), a.steps, stream, dev, 1, [r])
+    torch.cuda.synchronize(dev)
+    assert torch.equal(offs, ref_offs) and torch.equal(peers[:P], ref_peers), "CSR-only tick differs"
+    del ref_offs, ref_peers
+    B2 = B - 4 * P  # no msgs[P] written
+    out["csr_only"] = {"value": P * a.steps / (t2_ms / 1e3), "unit": "pairs/s", "ms_per_step": t2_ms / a.steps,
+                       "algorithmic_bytes": B2, "frac": B2 / (t2_ms / a.steps / 1e3) / 8e12,
+                       "note": "the same C3 tick with msgs = NULL: offsets + peers only (SURVEY.md §8(b) output); "
+                               "algorithmic bytes 69M + 4F + 4P + 4; peers checked equal to the full form's"}
     if not a.no_cpu_baseline:
         out["cpu_baseline"] = _cpu_route_sample(w, a.cpu_seconds, "C3")
         threads = min(16, os.cpu_count() or 1)

@@ -108,6 +108,57 @@ def test_delta_empty_and_revive_cubes():
     assert r.update_counts() == (2, 0)
 
 
+def test_delta_row_and_wave_path_edges():
+    """Cubes built at sizes around the bucket apply's limits (24 inline peers, 64-cube / 1,024-word
+    rounds, lists past kLaneList for the wave path) get batches that grow them past 24, shrink them
+    below 24, empty them, keep an inline cube inline under many ops, and put many ops on one cube;
+    every tick is checked against the oracle and must stay incremental."""
+    rng = np.random.default_rng(77)
+    r, o = mk_router(), orc.COracle(16)
+    sizes = [0, 1, 10, 20, 23, 24, 25, 30, 40, 50, 60, 63, 64, 65, 100, 300]
+    cells = np.array([[16.0 * i + 8.0, 8.0, 8.0] for i in range(len(sizes))])
+    w, p, ps = [], [], []
+    for i, n in enumerate(sizes):
+        pe = rng.choice(5000, n, replace=False).astype(np.uint32)
+        p.append(pe)
+        ps.append(np.tile(cells[i], (n, 1)))
+    allp = np.concatenate(p)
+    base = abi.ops_array(np.zeros(len(allp), np.uint32), allp, np.zeros(len(allp), np.uint8),
+                         pos=np.concatenate(ps))
+    r.apply_ops(base)
+    o.apply_ops(base)
+    # a filler table so a later batch stays incremental (a batch must be <= 1/4 of the table)
+    fill = _random_ops(rng, 60000, 2, 6000, 400.0, 1.0)
+    fill["world"] += 1
+    r.apply_ops(fill)
+    o.apply_ops(fill)
+    mpos = np.repeat(cells, 4, 0)
+    M = len(mpos)
+    for tick in range(6):
+        parts = []
+        for i, n in enumerate(sizes):
+            k = [0, 3, 12, 40, 41, 1, 4, 80, 24, 14, 4, 1, 0, 2, 30, 10][i] + tick
+            kinds = rng.integers(0, 2, k).astype(np.uint8)
+            if tick == 2 and i in (3, 7):   # empty two cubes completely
+                cur = o.route(cells[i:i + 1], np.zeros(1, np.uint32), np.zeros(1, np.uint32),
+                              np.ones(1, np.uint8))[1]
+                pe = cur.astype(np.uint32)
+                kinds = np.ones(len(pe), np.uint8)
+            else:
+                pe = np.concatenate([rng.choice(p[i], min(len(p[i]), k // 2)) if len(p[i]) else
+                                     np.zeros(0, np.uint32),
+                                     rng.integers(5000, 5200, k - min(len(p[i]), k // 2))]).astype(np.uint32)
+                rng.shuffle(pe)
+            parts.append(abi.ops_array(np.zeros(len(pe), np.uint32), pe, kinds[:len(pe)],
+                                       pos=np.tile(cells[i], (len(pe), 1))))
+        batch = abi.concat_ops(parts)
+        r.apply_ops(batch)
+        o.apply_ops(batch)
+        _check(r, o, mpos, np.zeros(M, np.uint32), rng.integers(0, 5200, M).astype(np.uint32),
+               np.tile(np.array([0, 1, 2, 1], np.uint8), M // 4))
+    assert r.update_counts()[1] == 0
+
+
 def test_delta_fallbacks_and_remove_peer():
     """An irregular key in a small batch takes the rebuild; REMOVE_PEER after incremental
     batches works from the regenerated state."""
