@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--G", type=int, default=8)
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--hot-peers", type=int, default=0,
+                    help="skew: one extra cube with this many subscribers ...")
+    ap.add_argument("--hot-frac", type=float, default=0.0, help="... that this fraction of the messages hit")
     a = ap.parse_args()
     import torch
     from worldql_server_amd import synth_ext
@@ -38,6 +41,17 @@ def main():
 
     w = synth_ext.config_c3(scale=a.scale)
     M, G = len(w.world), a.G
+    hot_note = ""
+    if a.hot_peers:  # one cube far from every hotspot, subscribed by peers 0 .. H-1, hit by hot_frac of M
+        from worldql_server_amd import abi
+        hp = np.full((a.hot_peers, 3), [200000.5, 8.5, 8.5])
+        hot_ops = abi.ops_array(np.zeros(a.hot_peers, np.uint32), np.arange(a.hot_peers, dtype=np.uint32),
+                                np.zeros(a.hot_peers, np.uint8), pos=hp)
+        w.ops = abi.concat_ops([w.ops, hot_ops])
+        idx = np.random.default_rng(7).choice(M, int(a.hot_frac * M), replace=False)
+        w.pos = w.pos.copy()
+        w.pos[idx] = [200000.5, 8.5, 8.5]
+        hot_note = f" + one cube with {a.hot_peers} subscribers hit by {len(idx)} messages"
     dev = torch.device("cuda:0")
     hub = Hub(G)
     routers = [Router(16, 0) for _ in range(G)]
@@ -77,7 +91,7 @@ def main():
     for t in th:
         t.join()
     assert not errors, errors
-    out = {"workload": f"C3 (scale {a.scale}): {M} messages, {len(w.ops)} subscriptions, G = {G} shards as hub "
+    out = {"workload": f"C3 (scale {a.scale}){hot_note}: {M} messages, {len(w.ops)} subscriptions, G = {G} shards as hub "
                        f"threads on one GPU (the bytes are those an {G}-GPU run moves over xGMI)",
            "G": G, "messages_per_tick": M, "pairs_per_tick": sum(x["pairs"] for x in res["slots"]),
            "wall_s": round(time.perf_counter() - t0, 1)}
@@ -85,6 +99,7 @@ def main():
         s = [x["sent_bytes"] for x in res[form]]
         r_ = [x["recv_bytes"] for x in res[form]]
         out[form] = {"sent_bytes_per_gpu_mean": float(np.mean(s)), "sent_bytes_per_gpu_max": int(max(s)),
+                     "sent_max_over_mean": float(max(s) / max(np.mean(s), 1.0)),
                      "recv_bytes_per_gpu_mean": float(np.mean(r_)), "recv_bytes_per_gpu_max": int(max(r_)),
                      "per_shard": res[form]}
     out["slots_vs_expanded"] = out["slots"]["sent_bytes_per_gpu_mean"] / out["expanded"]["sent_bytes_per_gpu_mean"]
