@@ -297,7 +297,9 @@ def test_rccl_exchange_one_rank():
 
 
 @pytest.mark.skipif(os.environ.get("WQ_TEST_RCCL_MULTI") != "1",
-                    reason="two RCCL ranks on ONE GPU: run on request (WQ_TEST_RCCL_MULTI=1) under an outer timeout")
+                    reason="two RCCL ranks on ONE GPU: run on request (WQ_TEST_RCCL_MULTI=1) under an outer timeout; on the "
+                           "MI355X pool RCCL refuses it (ncclCommInitRank: invalid usage, "
+                           "profiles/r03_rccl_two_ranks_one_gpu.log), so multi-rank RCCL needs a multi-GPU node")
 def test_rccl_exchange_two_processes_one_gpu():
     res = _run_procs(2, "rccl")
     if any(v[0] == "rccl-attach" for v in res.values()):
