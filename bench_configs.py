@@ -602,9 +602,45 @@ def run_c5(a, rank, world_size, local_rank, dev):
                 "synthetic (splitmix64, SURVEY.md §8(d) C5 generator)")
     r.close()
     if not a.no_cpu_baseline:
-        out["cpu_baseline"] = _cpu_c5_sample(init, [t[0] for t in ticks[:a.warmup + 1]], ticks[a.warmup][1],
-                                             c5.radius, a.cpu_seconds)
+        tick_ops = [t[0] for t in ticks[:a.warmup + 1]]
+        out["cpu_baseline"] = _cpu_c5_measured(init, tick_ops, ticks[a.warmup][1], c5.radius)
+        out["cpu_baseline_faithful"] = _cpu_c5_sample(init, tick_ops, ticks[a.warmup][1], c5.radius, a.cpu_seconds)
     return out
+
+
+def _cpu_c5_measured(init, tick_ops, pos_after, radius):
+    """One whole C5 tick MEASURED on 1 host thread by the C restatement in checker mode
+    (wqo_set_fast: the same sets, without remove_subscription's O(#cubes) scan of
+    area_map.rs:113-116): the tick's churn ops applied in order, then its 1M messages routed with the
+    radius filter (wqo_route_radius). The table before the tick is built untimed."""
+    import ctypes
+    from oracle import oracle as orc
+    vp = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    M = len(pos_after)
+    o = orc.COracle(16)
+    o.set_fast(True)
+    o.apply_ops(init)
+    for ops in tick_ops[:-1]:
+        o.apply_ops(ops)
+    ops = np.ascontiguousarray(tick_ops[-1])
+    world = np.zeros(M, np.uint32)
+    sender = np.arange(M, dtype=np.uint32)
+    repl = np.zeros(M, np.uint8)
+    offs = np.empty(M + 1, np.uint32)
+    pa = np.ascontiguousarray(pos_after)
+    t0 = time.perf_counter()
+    o.apply_ops(ops)
+    t_ops = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    P = o.lib.wqo_route_radius(o.h, vp(pa), vp(world), vp(sender), vp(repl), M, vp(pa), M, float(radius),
+                               vp(offs), None, 0, None)
+    t_route = time.perf_counter() - t0
+    o.close()
+    return {"value": P / (t_ops + t_route), "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"one whole C5 tick measured: {len(ops)} churn ops applied in {t_ops:.2f} s and {M} messages "
+                      f"routed with the radius filter in {t_route:.2f} s ({P} pairs), oracle/wq_oracle.c in checker "
+                      f"mode (the reference's sets without its O(#cubes) unsubscribe scan; see "
+                      f"cpu_baseline_faithful for that scan) on 1 host thread"}
 
 
 def _cpu_c5_sample(init, tick_ops, pos_after, radius, seconds):
