@@ -218,7 +218,7 @@ struct BucketLds {
     uint32_t lst[kRoundWords];      // a round's staged old lists (flat), or the wave path's one list
     union {
         struct {                    // a round
-            uint16_t wf[kRoundWords];  // staged word: bit 15 removed, bits 0-14 adds placed right before it
+            uint16_t wf[kRoundWords];  // staged word: bit 15 removed, bits 9-14 its cube in the round, 0-8 adds placed right before it
             uint8_t fl[kWin];          // per op: 1 add / 2 remove
             uint16_t at[kWin];         // per op: #old peers below it
             uint16_t pa[kWin + 1];     // exclusive prefix of add flags over the round's ops
@@ -664,7 +664,7 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                     if (x < T) {
                         const uint32_t u = owner_of(sm, x);
                         val[r] = reinterpret_cast<const uint32_t*>(sm.csrc[u])[x - sm.cpre[u]];
-                        sm.u.r.wf[x] = 0;
+                        sm.u.r.wf[x] = (uint16_t)(u << 9);  // the owner rides along (bits 9-14)
                     }
                 }
 #pragma unroll
@@ -765,10 +765,11 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                         const uint32_t x = g0 + r * 64 + lane;
                         const uint32_t w = x < T ? (uint32_t)sm.u.r.wf[x] : 0u;
                         const uint64_t mr = __ballot(w >> 15);
-                        const uint32_t ac = w & 0x7FFFu;
+                        const uint32_t ac = w & 0x1FFu;  // adds placed before it (<= kWin)
                         const uint32_t ainc = wave_incl_scan_dpp(ac);
                         rex[r] = cr + (uint32_t)__popcll(mr & lt);
-                        aex[r] = (ca + ainc - ac) | (w & 0x8000u) << 16 | ac << 16;  // bit 31 removed, 16-30 ac
+                        // bit 31 removed, 25-30 owner cube, 16-24 ac, 0-15 adds before the word
+                        aex[r] = (ca + ainc - ac) | (w & 0x8000u) << 16 | ((w >> 9) & 0x3Fu) << 25 | ac << 16;
                         cr += (uint32_t)__popcll(mr);
                         ca += (uint32_t)__builtin_amdgcn_readlane((int)ainc, 63);
                     }
@@ -776,7 +777,7 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                     for (int r = 0; r < NG; ++r) {
                         const uint32_t x = g0 + r * 64 + lane;
                         if (x < T && ((sm.smask[x >> 6] >> lane) & 1ull)) {
-                            const uint32_t u = owner_of(sm, x);
+                            const uint32_t u = (aex[r] >> 25) & 0x3Fu;
                             sm.cR[u] = (uint16_t)rex[r];
                             sm.cA[u] = (uint16_t)aex[r];
                         }
@@ -786,10 +787,10 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                     for (int r = 0; r < NG; ++r) {
                         const uint32_t x = g0 + r * 64 + lane;
                         if (x >= T || (aex[r] >> 31)) continue;
-                        const uint32_t u = owner_of(sm, x), d = sm.cdst[u];
+                        const uint32_t u = (aex[r] >> 25) & 0x3Fu, d = sm.cdst[u];
                         if (d == kNone) continue;
                         const uint32_t y = sm.lst[x];
-                        const uint32_t ax = aex[r] & 0xFFFFu, ac = (aex[r] >> 16) & 0x7FFFu;
+                        const uint32_t ax = aex[r] & 0xFFFFu, ac = (aex[r] >> 16) & 0x1FFu;
                         const uint32_t k = (x - sm.cpre[u]) - (rex[r] - sm.cR[u]) + (ax + ac - sm.cA[u]);
                         if (d != kInlineOnly) L[d + 1 + k] = y;
                         if (k < (uint32_t)kInline) reinterpret_cast<uint32_t*>(a.tb.recs + sm.cslot[u])[kInlineWord0 + k] = y;
