@@ -759,11 +759,17 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                 uint32_t cr = 0, ca = 0;
 #pragma unroll 1
                 for (uint32_t g0 = 0; g0 < T; g0 += NG * 64) {
-                    uint32_t rex[NG], aex[NG];
+                    uint32_t rex[NG], aex[NG], wv[NG];
+                    uint64_t sm_m[NG];
+#pragma unroll
+                    for (int r = 0; r < NG; ++r) {  // the chunks' mark words and list-start masks at once
+                        const uint32_t x = g0 + r * 64 + lane;
+                        wv[r] = x < T ? (uint32_t)sm.u.r.wf[x] : 0u;
+                        sm_m[r] = sm.smask[(x >> 6) < kRoundWords / 64 ? (x >> 6) : 0u];
+                    }
 #pragma unroll
                     for (int r = 0; r < NG; ++r) {
-                        const uint32_t x = g0 + r * 64 + lane;
-                        const uint32_t w = x < T ? (uint32_t)sm.u.r.wf[x] : 0u;
+                        const uint32_t w = wv[r];
                         const uint64_t mr = __ballot(w >> 15);
                         const uint32_t ac = w & 0x1FFu;  // adds placed before it (<= kWin)
                         const uint32_t ainc = wave_incl_scan_dpp(ac);
@@ -776,24 +782,35 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
 #pragma unroll
                     for (int r = 0; r < NG; ++r) {
                         const uint32_t x = g0 + r * 64 + lane;
-                        if (x < T && ((sm.smask[x >> 6] >> lane) & 1ull)) {
+                        if (x < T && ((sm_m[r] >> lane) & 1ull)) {
                             const uint32_t u = (aex[r] >> 25) & 0x3Fu;
                             sm.cR[u] = (uint16_t)rex[r];
                             sm.cA[u] = (uint16_t)aex[r];
                         }
                     }
                     wave_lds_sync();
+                    // every LDS read of the NG chunks first (one round trip), then the stores
+                    uint32_t cd[NG], cy[NG], cp[NG], cq[NG], cz[NG], cl[NG];
 #pragma unroll
                     for (int r = 0; r < NG; ++r) {
                         const uint32_t x = g0 + r * 64 + lane;
-                        if (x >= T || (aex[r] >> 31)) continue;
-                        const uint32_t u = (aex[r] >> 25) & 0x3Fu, d = sm.cdst[u];
-                        if (d == kNone) continue;
-                        const uint32_t y = sm.lst[x];
+                        const uint32_t u = (aex[r] >> 25) & 0x3Fu;  // (0 past T)
+                        cd[r] = sm.cdst[u];
+                        cy[r] = sm.lst[x < (uint32_t)kRoundWords ? x : 0u];
+                        cp[r] = sm.cpre[u];
+                        cq[r] = sm.cR[u];
+                        cz[r] = sm.cA[u];
+                        cl[r] = sm.cslot[u];
+                    }
+#pragma unroll
+                    for (int r = 0; r < NG; ++r) {
+                        const uint32_t x = g0 + r * 64 + lane;
+                        const uint32_t u = (aex[r] >> 25) & 0x3Fu, d = cd[r], y = cy[r];
+                        if (x >= T || (aex[r] >> 31) || d == kNone) continue;
                         const uint32_t ax = aex[r] & 0xFFFFu, ac = (aex[r] >> 16) & 0x1FFu;
-                        const uint32_t k = (x - sm.cpre[u]) - (rex[r] - sm.cR[u]) + (ax + ac - sm.cA[u]);
+                        const uint32_t k = (x - cp[r]) - (rex[r] - cq[r]) + (ax + ac - cz[r]);
                         if (d != kInlineOnly) L[d + 1 + k] = y;
-                        if (k < (uint32_t)kInline) reinterpret_cast<uint32_t*>(a.tb.recs + sm.cslot[u])[kInlineWord0 + k] = y;
+                        if (k < (uint32_t)kInline) reinterpret_cast<uint32_t*>(a.tb.recs + cl[r])[kInlineWord0 + k] = y;
                         atomicOr(reinterpret_cast<unsigned long long*>(&sm.csig[u]), (unsigned long long)peer_sig(y));
                     }
                 }
