@@ -313,14 +313,6 @@ __device__ __forceinline__ uint32_t lds_lower_bound_fixed(const uint32_t* a, uin
     return (len && a[lo] < v) ? lo + 1 : lo;
 }
 
-__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
-    return v;
-}
 
 // Inclusive wave64 prefix sum by DPP row shifts and row broadcasts (no LDS round trips).
 __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
@@ -619,7 +611,7 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                 oc <= (uint32_t)kInline ? reinterpret_cast<const uint32_t*>(a.tb.recs + slot) + kInlineWord0 : L + off + 1);
             bool isbig = act && oc > (uint32_t)kLaneList;
             uint32_t oc_st = isbig ? 0u : oc;
-            const uint32_t incl = wave_incl_scan_u32(oc_st, lane);
+            const uint32_t incl = wave_incl_scan_dpp(oc_st);
             // the round: the cubes whose staged words fit kRoundWords (at least one: oc <= kLaneList)
             n_round = (uint32_t)__popcll(__ballot(act && incl <= kRoundWords));
             act = act && (uint32_t)lane < n_round;
@@ -648,7 +640,7 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
             wave_lds_sync();
             {
                 const uint32_t pc = lane < (int)(kRoundWords / 64) ? (uint32_t)__popcll(sm.smask[lane]) : 0u;
-                const uint32_t ic = wave_incl_scan_u32(pc, lane);
+                const uint32_t ic = wave_incl_scan_dpp(pc);
                 if (lane < (int)(kRoundWords / 64)) sm.mcum[lane] = (uint16_t)(ic - pc);
             }
             wave_lds_sync();
@@ -656,16 +648,27 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
             // stage the round's old lists flat: all of the round's loads in flight at once
             // (T <= kRoundWords = 16 per lane)
             {
+                // owners and source addresses first (LDS only), then every global load: the
+                // sources are global memory (record inline words or `list`), so they are read as
+                // such — a flat load would also count in lgkmcnt, and each LDS wait would then wait
+                // for the loads issued before it
+                typedef const __attribute__((address_space(1))) uint32_t* gptr;
                 uint32_t val[kRoundWords / 64];
+                uint64_t src[kRoundWords / 64];
 #pragma unroll
                 for (int r = 0; r < (int)(kRoundWords / 64); ++r) {
                     const uint32_t x = r * 64 + lane;
-                    val[r] = 0u;
+                    src[r] = 0;
                     if (x < T) {
                         const uint32_t u = owner_of(sm, x);
-                        val[r] = reinterpret_cast<const uint32_t*>(sm.csrc[u])[x - sm.cpre[u]];
+                        src[r] = sm.csrc[u] + 4ull * (x - sm.cpre[u]);
                         sm.u.r.wf[x] = (uint16_t)(u << 9);  // the owner rides along (bits 9-14)
                     }
+                }
+#pragma unroll
+                for (int r = 0; r < (int)(kRoundWords / 64); ++r) {
+                    const uint32_t x = r * 64 + lane;
+                    val[r] = x < T ? *reinterpret_cast<gptr>(src[r]) : 0u;
                 }
 #pragma unroll
                 for (int r = 0; r < (int)(kRoundWords / 64); ++r) {
