@@ -14,7 +14,8 @@ import numpy as np
 from . import abi
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libwq_router.so")
+# WQ_LIBRARY: another in-tree build of the same sources (A/B timing of a kernel variant on one box)
+LIB_PATH = os.environ.get("WQ_LIBRARY") or os.path.join(PKG, "libwq_router.so")
 
 _lib = None
 
