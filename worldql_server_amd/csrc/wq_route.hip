@@ -13,6 +13,7 @@
 // launches. DESIGN.md §4-5 has the measurements behind each choice.
 // Output: CSR offsets[M+1] (message-major), peers[P], optional msgs[P].
 #include <algorithm>
+#include <cstdlib>
 
 #include "route_count.hpp"
 #include "route_emit.hpp"
@@ -289,8 +290,11 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         hipLaunchKernelGGL((emit_heavy_kernel<16>), eg, dim3(kBlock), 0, s, ep);
     else if (cfg.emit_heavy == 8)
         hipLaunchKernelGGL((emit_heavy_kernel<8>), eg, dim3(kBlock), 0, s, ep);
-    else if (cfg.emit_heavy == 116)
-        hipLaunchKernelGGL((emit_map_kernel<16>), eg, dim3(kBlock), 0, s, ep);
+    else if (cfg.emit_heavy == 116) {
+        // diagnostics only: extra LDS per block caps the emit's blocks per CU (occupancy sweeps)
+        static const size_t emit_lds = getenv("WQ_DEBUG_EMIT_LDS") ? strtoull(getenv("WQ_DEBUG_EMIT_LDS"), nullptr, 10) : 0;
+        hipLaunchKernelGGL((emit_map_kernel<16>), eg, dim3(kBlock), emit_lds, s, ep);
+    }
     else if (cfg.emit_heavy == 108)
         hipLaunchKernelGGL((emit_map_kernel<8>), eg, dim3(kBlock), 0, s, ep);
     else if (cfg.emit_stage == 4096 + 2)
