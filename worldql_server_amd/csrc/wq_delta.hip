@@ -514,11 +514,12 @@ __device__ __forceinline__ uint32_t bump_alloc(const BucketArgs& a, uint32_t wan
 
 __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
     __shared__ BucketLds sm;
-    if (a.status->flags & 3u) return;  // an op without a record: nothing applied, the rebuild takes the batch
+    const uint32_t B = blockIdx.x;
+    const uint32_t flags = a.status->flags;  // (loaded with the bucket bounds: one round trip)
+    const uint32_t s = a.bstart[B], e = a.bstart[B + 1];
+    if (flags & 3u) return;  // an op without a record: nothing applied, the rebuild takes the batch
     const int lane = threadIdx.x;
     const uint64_t lt = (1ull << lane) - 1ull;
-    const uint32_t B = blockIdx.x;
-    const uint32_t s = a.bstart[B], e = a.bstart[B + 1];
     uint64_t t_last = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
     const uint64_t lowmask = (1ull << a.lowbits) - 1ull;
     uint32_t* L = a.tb.list;
@@ -527,17 +528,21 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
     for (uint32_t w0 = s; w0 < e; w0 += kWin) {
         if (w0 != s) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // this wave's own earlier writes: same CU, same L2
         const uint32_t cnt = min((uint32_t)kWin, e - w0);
+        // the window's keys: clamped, unconditional loads (all four in flight; loads in per-lane
+        // branches each got their own vmcnt(0) wait)
         uint64_t v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t q = r * 64 + lane;
-            if (q < cnt) {
-                const uint64_t k = a.keys[w0 + q];
-                v[r] = (((k >> 33) & lowmask) << 48) | ((uint64_t)(uint32_t)k << 16) | ((uint64_t)q << 8) |
-                       ((k >> 32) & 1u);
-            } else {
-                v[r] = ~0ull;
-            }
+            v[r] = a.keys[w0 + (q < cnt ? q : 0u)];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t q = r * 64 + lane;
+            const uint64_t k = v[r];
+            v[r] = q < cnt ? ((((k >> 33) & lowmask) << 48) | ((uint64_t)(uint32_t)k << 16) | ((uint64_t)q << 8) |
+                              ((k >> 32) & 1u))
+                           : ~0ull;
         }
         if (cnt <= 64)
             wave_bitonic<1>(v, lane);
@@ -568,14 +573,13 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
             uint2 hw[4];
             uint32_t hc[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint32_t c = r * 64 + lane;
-                if (c < ncub) {
-                    const uint32_t slot = (B << a.lowbits) | (uint32_t)(sm.op[sm.cs[c]] >> 48);
-                    const uint32_t* rw = reinterpret_cast<const uint32_t*>(a.tb.recs + slot);
-                    hw[r] = *reinterpret_cast<const uint2*>(rw + 2);
-                    hc[r] = rw[6];
-                }
+            for (int r = 0; r < 4; ++r) {  // clamped, no per-lane branch: the rows' loads in flight together
+                if ((uint32_t)r * 64 >= ncub) break;  // (wave-uniform)
+                const uint32_t c = r * 64 + lane, cc = c < ncub ? c : 0u;
+                const uint32_t slot = (B << a.lowbits) | (uint32_t)(sm.op[sm.cs[cc]] >> 48);
+                const uint32_t* rw = reinterpret_cast<const uint32_t*>(a.tb.recs + slot);
+                hw[r] = *reinterpret_cast<const uint2*>(rw + 2);
+                hc[r] = rw[6];
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
