@@ -358,11 +358,19 @@ __global__ __launch_bounds__(kBlock) void k_sort_hist(const uint64_t* __restrict
     h[t] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+    // clamped, unconditional loads: all kSortPer in flight (a load under a per-lane branch gets its
+    // own vmcnt(0) wait, and the 16 loads completed one after another)
+    uint64_t kk[kSortPer];
+#pragma unroll
+    for (int r = 0; r < kSortPer; ++r) {
+        const uint64_t i = base + (uint64_t)r * kBlock + t;
+        kk[r] = keys[i < n ? i : (uint64_t)n - 1];
+    }
     uint32_t d[kSortPer];
 #pragma unroll
     for (int r = 0; r < kSortPer; ++r) {
         const uint64_t i = base + (uint64_t)r * kBlock + t;
-        d[r] = i < n ? (uint32_t)(keys[i] >> sh) & dmask : 0xFFFFFFFFu;
+        d[r] = i < n ? (uint32_t)(kk[r] >> sh) & dmask : 0xFFFFFFFFu;
     }
 #pragma unroll
     for (int r = 0; r < kSortPer; ++r)
