@@ -498,6 +498,7 @@ struct BucketArgs {
     uint64_t list_base;      // first free list word (t.list_used)
     uint64_t list_room;      // words available past list_base
     uint64_t* stamps;        // diagnostics (WQ_DELTA_STAMPS): per bucket, cycles per phase
+    uint32_t nb;             // buckets
 };
 
 // Diagnostic phase stamps of the bucket apply (lane 0 of each wave; WQ_DELTA_STAMPS only).
@@ -505,7 +506,7 @@ struct BucketArgs {
     do {                                                                       \
         if (a.stamps && lane == 0) {                                           \
             const uint64_t t_now = __builtin_amdgcn_s_memtime();               \
-            a.stamps[(uint64_t)blockIdx.x * 16 + (k)] += t_now - t_last;       \
+            a.stamps[(uint64_t)B * 16 + (k)] += t_now - t_last;                \
             t_last = t_now;                                                    \
         }                                                                      \
     } while (0)
@@ -522,17 +523,19 @@ __device__ __forceinline__ uint32_t bump_alloc(const BucketArgs& a, uint32_t wan
 
 __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
     __shared__ BucketLds sm;
-    const uint32_t B = blockIdx.x;
-    const uint32_t flags = a.status->flags;  // (loaded with the bucket bounds: one round trip)
-    const uint32_t s = a.bstart[B], e = a.bstart[B + 1];
+    const uint32_t flags = a.status->flags;
     if (flags & 3u) return;  // an op without a record: nothing applied, the rebuild takes the batch
     const int lane = threadIdx.x;
     const uint64_t lt = (1ull << lane) - 1ull;
-    uint64_t t_last = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
     const uint64_t lowmask = (1ull << a.lowbits) - 1ull;
     uint32_t* L = a.tb.list;
     int64_t de = 0, dl = 0;
     uint32_t nwave = 0;
+    // buckets blockIdx.x, + gridDim.x, ... (the launch gives each wave one or more buckets)
+    for (uint32_t B = blockIdx.x; B < a.nb; B += gridDim.x) {
+    const uint32_t s = a.bstart[B], e = a.bstart[B + 1];
+    uint64_t t_last = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+    if (B != blockIdx.x) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     for (uint32_t w0 = s; w0 < e; w0 += kWin) {
         if (w0 != s) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // this wave's own earlier writes: same CU, same L2
         const uint32_t cnt = min((uint32_t)kWin, e - w0);
@@ -1018,6 +1021,8 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
         }
     }
     WQ_STAMP(10);
+    wave_lds_sync();
+    }  // buckets
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         de += __shfl_xor(de, d, 64);
@@ -1298,7 +1303,14 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
         WQ_HIP(h, hipMemsetAsync(h->idx_b.p, 0, (uint64_t)NBr * 16 * 8, s));
         ba.stamps = h->idx_b.as<uint64_t>();
     }
-    hipLaunchKernelGGL(k_delta_bucket, dim3(NBr), dim3(64), 0, s, ba);
+    ba.nb = NBr;
+    // Buckets per wave (grid stride): two once there are >= 4,096 buckets. Tens of thousands of
+    // one-wave workgroups of 16 KB LDS each turn over faster than they work (C5: 32,768 buckets,
+    // update 0.81 -> 0.75 ms with two per wave; C4: 4,096, 0.198 -> 0.19); four leave C4 too few
+    // waves (0.254). WQ_DELTA_BPW overrides (diagnostics, tools/delta_bpw.sh).
+    static const int bpw_env = getenv("WQ_DELTA_BPW") ? std::max(1, atoi(getenv("WQ_DELTA_BPW"))) : 0;
+    const uint32_t bpw = bpw_env ? (uint32_t)bpw_env : (NBr >= 4096 ? 2u : 1u);
+    hipLaunchKernelGGL(k_delta_bucket, dim3((NBr + bpw - 1) / bpw), dim3(64), 0, s, ba);
     WQ_HIP(h, hipGetLastError());
     if (ba.stamps) {  // diagnostics: mean cycles per bucket and phase
         std::vector<uint64_t> st((size_t)NBr * 16);
