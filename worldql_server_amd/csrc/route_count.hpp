@@ -29,6 +29,7 @@ struct CountParams {
     wq_route_counters* cnt;
     wq_route_counters* cnt_next;
     uint32_t* health;  // sticky {error, overflow} words (flag_route)
+    uint32_t n_tiles = 0;  // count_kernel: tiles of kBlock * IPT messages (grid stride when > gridDim.x)
 };
 
 // e / locator once count, membership and list position are known (local_message.rs:60-86)
@@ -293,38 +294,41 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
         p.cnt_next->overflow = 0;
         p.cnt_next->error = 0;
     }
-    const uint32_t m0 = blockIdx.x * (kBlock * IPT);
-    uint64_t F_local = 0;
-    uint32_t E_local = 0;
-    uint32_t e_out[IPT];
-    uint2 inf_out[IPT];
-    count_rows<RAW_KEYS, IPT, DBG, FULL, SLOTS>(p.in, p.t, m0, e_out, inf_out, F_local, E_local);
+    const uint32_t nt = p.n_tiles ? p.n_tiles : gridDim.x;
+    for (uint32_t blk = blockIdx.x; blk < nt; blk += gridDim.x) {
+        const uint32_t m0 = blk * (kBlock * IPT);
+        uint64_t F_local = 0;
+        uint32_t E_local = 0;
+        uint32_t e_out[IPT];
+        uint2 inf_out[IPT];
+        count_rows<RAW_KEYS, IPT, DBG, FULL, SLOTS>(p.in, p.t, m0, e_out, inf_out, F_local, E_local);
 #pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-        const uint32_t m = m0 + i * kBlock + tid;
-        if (m < p.in.M) {
-            p.e[m] = e_out[i];
-            p.info[m] = inf_out[i];
+        for (int i = 0; i < IPT; ++i) {
+            const uint32_t m = m0 + i * kBlock + tid;
+            if (m < p.in.M) {
+                p.e[m] = e_out[i];
+                p.info[m] = inf_out[i];
+            }
         }
-    }
-
-    const uint64_t Fw = wave_sum_u64(F_local);
-    const uint64_t Ew = wave_sum_u64(E_local);
-    if (lane == 0) {
-        wave_F[wave] = Fw;
-        wave_E[wave] = Ew;
-    }
-    lds_barrier();
-    if (tid == 0) {
-        uint64_t Fb = 0, Eb = 0;
+        const uint64_t Fw = wave_sum_u64(F_local);
+        const uint64_t Ew = wave_sum_u64(E_local);
+        if (lane == 0) {
+            wave_F[wave] = Fw;
+            wave_E[wave] = Ew;
+        }
+        lds_barrier();
+        if (tid == 0) {
+            uint64_t Fb = 0, Eb = 0;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) {
-            Fb += wave_F[w];
-            Eb += wave_E[w];
+            for (int w = 0; w < kWaves; ++w) {
+                Fb += wave_F[w];
+                Eb += wave_E[w];
+            }
+            p.tile_F[blk] = Fb > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Fb;
+            p.tile_total[blk] = Eb > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Eb;
+            if (Eb > 0xFFFFFFFFull) flag_route(p.cnt, p.health, 2u, 0u);
         }
-        p.tile_F[blockIdx.x] = Fb > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Fb;
-        p.tile_total[blockIdx.x] = Eb > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Eb;
-        if (Eb > 0xFFFFFFFFull) flag_route(p.cnt, p.health, 2u, 0u);
+        lds_barrier();  // the next tile rewrites wave_F / wave_E
     }
 }
 

@@ -21,6 +21,7 @@ struct EmitParams {
     uint32_t* peers;              // nullptr: offsets only (no capacity)
     uint32_t* msgs;
     uint64_t capacity;
+    uint32_t n_blocks = 0;  // emit_map_kernel: 256-message blocks (grid stride when > gridDim.x)
 };
 
 // LDS of one emit row (256 messages): an image of a window of the row's output, aligned to
@@ -451,7 +452,9 @@ __global__ __launch_bounds__(kBlock) void emit_map_kernel(EmitParams p) {
     __shared__ uint32_t wave_tot[kWaves];
     __shared__ uint32_t part_tot[kWaves];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t m0 = blockIdx.x * kBlock;
+    const uint32_t nbk = p.n_blocks ? p.n_blocks : gridDim.x;
+    for (uint32_t blk = blockIdx.x; blk < nbk; blk += gridDim.x) {
+    const uint32_t m0 = blk * kBlock;
     const uint32_t m = m0 + tid;
     const uint32_t e = m < p.M ? p.e[m] : 0u;
     const uint2 inf = (p.peers && m < p.M) ? p.info[m] : make_uint2(0, kNone);
@@ -466,7 +469,7 @@ __global__ __launch_bounds__(kBlock) void emit_map_kernel(EmitParams p) {
 #pragma unroll
     for (int u = 0; u < kWaves; ++u) g += part_tot[u];
     if (m < p.M) p.offsets[m] = g + st;
-    if (!p.peers || T == 0) return;
+    if (p.peers && T != 0) {
     // the descriptor: recipient k of the message is word k + (k >= skip) from `base`
     const uint32_t* base = p.t.list;
     uint32_t skip = kNone;
@@ -554,6 +557,9 @@ __global__ __launch_bounds__(kBlock) void emit_map_kernel(EmitParams p) {
         }
         lds_barrier();  // the next window rewrites the map
     }
+    }  // outputs
+    lds_barrier();  // the next block's scan and descriptors reuse the LDS
+    }  // blocks
 }
 
 }  // namespace wq

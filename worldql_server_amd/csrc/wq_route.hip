@@ -253,7 +253,14 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     if (radius)
         hipLaunchKernelGGL(count_radius_kernel, dim3(n_count), dim3(kBlock), 0, s, cp);
     else
-        cfg.count(cp, s, n_count);
+        {
+        // two count tiles per block (grid stride): C3's 39,063 short blocks turn over less (with
+        // two emit blocks per workgroup, 1,294-1,303 vs 1,320-1,328 us per tick on one box; 3 or 4
+        // no better). WQ_DEBUG_COUNT_TPB overrides (diagnostics)
+        static const uint32_t tpb = getenv("WQ_DEBUG_COUNT_TPB") ? (uint32_t)std::max(1, atoi(getenv("WQ_DEBUG_COUNT_TPB"))) : 2u;
+        cp.n_tiles = n_count;
+        cfg.count(cp, s, (n_count + tpb - 1) / tpb);
+    }
     WQ_HIP(h, hipGetLastError());
 
     TileScanParams sp;
@@ -293,7 +300,10 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     else if (cfg.emit_heavy == 116) {
         // diagnostics only: extra LDS per block caps the emit's blocks per CU (occupancy sweeps)
         static const size_t emit_lds = getenv("WQ_DEBUG_EMIT_LDS") ? strtoull(getenv("WQ_DEBUG_EMIT_LDS"), nullptr, 10) : 0;
-        hipLaunchKernelGGL((emit_map_kernel<16>), eg, dim3(kBlock), emit_lds, s, ep);
+        // two 256-message blocks per workgroup (grid stride, see the count above); WQ_DEBUG_EMIT_BPB overrides
+        static const uint32_t bpb = getenv("WQ_DEBUG_EMIT_BPB") ? (uint32_t)std::max(1, atoi(getenv("WQ_DEBUG_EMIT_BPB"))) : 2u;
+        ep.n_blocks = eg.x;
+        hipLaunchKernelGGL((emit_map_kernel<16>), dim3((eg.x + bpb - 1) / bpb), dim3(kBlock), emit_lds, s, ep);
     }
     else if (cfg.emit_heavy == 108)
         hipLaunchKernelGGL((emit_map_kernel<8>), eg, dim3(kBlock), 0, s, ep);
