@@ -29,7 +29,7 @@ import numpy as np
 import bench
 from bench import HBM_PEAK_GBS, METRIC, algorithmic_bytes, reduce_over_ranks, roofline, timed_ticks
 
-PMC_C3 = "r02_pmc_route_c3.json"  # rocprofv3 --pmc summary of the C3 tick (tools/pmc_route.sh)
+PMC_C3 = "r03_pmc_route_c3.json"  # rocprofv3 --pmc summary of the C3 tick (tools/pmc_route.sh)
 
 
 def run(a, rank, world_size, local_rank, dev):
