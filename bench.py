@@ -11,9 +11,11 @@ each subscribed to a 3x3x3 neighbourhood (27M subscriptions), 10M LocalMessages 
   N = 1   the whole configuration on one GPU: every step is one full tick of the hot path on
           HBM-resident inputs (quantise -> probe -> filter -> CSR offsets + (msg, peer) pairs), with
           the C2 line (BASELINE.json configs[1]: 100k peers, 1M messages) nested under extra.c2.
-  N > 1   strong scaling by cube hash through the C ABI's sharded tick: every rank ingests M/N of
-          the messages; shard -> RCCL all-to-all of the records -> route on the owners -> RCCL
-          all-to-all of the pairs back to the ingesting GPU (wq_sharded_route_tick_device).
+  N > 1   strong scaling: every rank ingests M/N of the tick's messages. Headline: the replicated
+          table (every GPU holds the whole ~10 GB table and routes its slice with the single-GPU
+          tick, no exchange; DESIGN.md §6 says why); beside it, extra.cube_hash: the cube-hash
+          sharded tick over RCCL (20-byte slots to the owners, row references + cube-list pools
+          back; wq_sharded_route_tick_device). --shard cube makes that form the headline.
 The table is built once before timing. Every timed loop is checked afterwards through the
 routers' sticky health words (wq_route_health): no tick may have given up or overflowed.
 Other configs: --config c1 | c2 | c4 | c5 (bench_configs.py); --config c2 --shard cube = one world
@@ -52,8 +54,9 @@ def parse():
     ap.add_argument("--scale", type=float, default=1.0, help="shrink C2 (tests only; 1.0 = the headline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline's routing work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--shard", choices=["world", "cube"], default="world",
-                    help="multi-GPU partitioning (see module docstring)")
+    ap.add_argument("--shard", choices=["world", "cube", "replicate"], default="world",
+                    help="multi-GPU partitioning (see module docstring); C3: replicate (the default at N > 1) "
+                         "or cube as the headline form")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "r02_pmc_route.json"),
                     help="rocprofv3 --pmc summary of the C2 tick (roofline.traffic)")
     a = ap.parse_args()
@@ -231,8 +234,13 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # WQ_BENCH_ONE_GPU=1: a rehearsal of the N > 1 control flow with every rank on cuda:0 over gloo
+    # (RCCL refuses two ranks on one GPU); its timings mean nothing
+    rehearse = os.environ.get("WQ_BENCH_ONE_GPU") == "1"
+    if rehearse:
+        local_rank = 0
     if world_size > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group("gloo" if rehearse else "nccl", init_method="env://")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 

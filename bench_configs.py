@@ -174,8 +174,10 @@ def run_c3(a, rank, world_size, local_rank, dev):
     t0 = time.perf_counter()
     w = synth_ext.config_c3(scale=a.scale)
     gen_s = time.perf_counter() - t0
-    if world_size > 1 or a.shard == "cube":  # (--shard cube at N = 1: the same sharded tick over one RCCL rank)
-        return _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s)
+    if world_size > 1 or a.shard in ("cube", "replicate"):
+        # N > 1: both multi-GPU forms, the replicated table as the headline unless
+        # --shard cube; --shard cube / replicate at N = 1: that form alone on one rank
+        return _run_c3_multi(a, w, rank, world_size, local_rank, dev, gen_s)
     M = len(w.world)
     r = Router(w.cube_size, local_rank)
     stream = torch.cuda.Stream(device=dev)
@@ -275,29 +277,102 @@ def _xgmi_model():
     return out
 
 
+def _gloo_exchange(dist):
+    """The caller's all-to-all (wq_shard_attach_exchange) over the bench's gloo group: device -> host,
+    gloo, host -> device. Only for WQ_BENCH_ONE_GPU rehearsals (RCCL refuses two ranks on one GPU)."""
+    import ctypes
+    import torch
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the HIP runtime PyTorch already loaded
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+
+    def fn(send, sb, recv, rb, stream):
+        assert hip.hipStreamSynchronize(stream or None) == 0
+        src = np.empty(max(sum(sb), 1), np.uint8)
+        if sum(sb):
+            assert hip.hipMemcpy(src.ctypes.data, send, sum(sb), 4) == 0
+        dst = torch.empty(sum(rb), dtype=torch.uint8)
+        dist.all_to_all_single(dst, torch.from_numpy(src[:sum(sb)]), list(rb), list(sb))
+        if sum(rb):
+            assert hip.hipMemcpy(recv, dst.numpy().ctypes.data, sum(rb), 4) == 0
+    return fn
+
+
 def attach_rccl(r, rank: int, world_size: int) -> None:
     """This rank's router becomes shard `rank` of world_size over its own RCCL communicator (the id
     travels over the bench's process group)."""
     import torch.distributed as dist
     from worldql_server_amd.router import rccl_unique_id
+    if os.environ.get("WQ_BENCH_ONE_GPU") == "1" and world_size > 1:
+        r.attach_exchange(world_size, rank, _gloo_exchange(dist))  # rehearsal: every rank on cuda:0
+        return
     uid = [rccl_unique_id() if rank == 0 else None]
     if world_size > 1:
         dist.broadcast_object_list(uid, src=0)
     r.attach_rccl(world_size, rank, uid[0])
 
 
-def _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s):
-    """C3 strong scaling through the C ABI's sharded tick (wq_sharded_route_tick_device over RCCL):
-    every rank ingests M/N of the 10M messages; each tick groups them by owner, exchanges the
-    records, routes on the owners and returns every (message, peer) pair to the ingesting GPU in
-    message order. value = all ranks' pairs / the max-over-ranks time of the timed ticks."""
+def _c3_slice(w, rank, world_size, dev):
     import torch
-    from worldql_server_amd.router import Router
-
     M_all = len(w.world)
     lo, hi = rank * M_all // world_size, (rank + 1) * M_all // world_size
+    t = (torch.from_numpy(w.pos[lo:hi]).to(dev), torch.from_numpy(w.world[lo:hi].view(np.int32)).to(dev),
+         torch.from_numpy(w.sender[lo:hi].view(np.int32)).to(dev), torch.from_numpy(w.repl[lo:hi]).to(dev))
+    torch.cuda.synchronize(dev)
+    return lo, hi, t
+
+
+def _c3_replicated(a, w, rank, world_size, local_rank, dev, stream, sl):
+    """The replicated-table form (wq_router_create_multi_mode's WQ_MULTI_REPLICATE, one process per
+    GPU): every rank holds the WHOLE table (C3: ~10 GB of 288 GB; every op applied on every GPU) and
+    routes its own M/N messages with the single-GPU tick — no exchange at all."""
+    import torch
+    from worldql_server_amd.router import Router
+    lo, hi, (pos, world, sender, repl) = sl
     M = hi - lo
-    stream = torch.cuda.Stream(device=dev)
+    r = Router(w.cube_size, local_rank)
+    r.set_stream(stream.cuda_stream)
+    t0 = time.perf_counter()
+    r.apply_ops(w.ops)
+    build_s = time.perf_counter() - t0
+    offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    r.route_device(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
+                   0, 0, 0, cnt.data_ptr())
+    torch.cuda.synchronize(dev)
+    P = int(_counters(cnt)["n_pairs"][0])
+    r.set_fanout_hint(P / max(M, 1))  # a server passes its previous tick's P / M
+    cap = P + 1024
+    peers = torch.empty(cap, dtype=torch.int32, device=dev)
+    msgs = torch.empty(cap, dtype=torch.int32, device=dev)
+    args = (pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
+            peers.data_ptr(), msgs.data_ptr(), cap)
+    for _ in range(max(a.warmup, 1)):
+        r.route_device(*args, 0)
+    r.route_device(*args, cnt.data_ptr())
+    torch.cuda.synchronize(dev)
+    c = _counters(cnt)[0]
+    P, F = int(c["n_pairs"]), int(c["n_candidates"])
+    assert c["overflow"] == 0 and c["error"] == 0, c
+    t_ms = timed_ticks(lambda: r.route_device(*args, 0), a.steps, stream, dev, world_size, [r])
+    r.close()
+    t_max_ms, pairs_all = reduce_over_ranks(t_ms, P, dev, world_size)
+    B_all, _ = reduce_over_ranks(0.0, algorithmic_bytes(M, F, P), dev, world_size)
+    del peers, msgs
+    return {"t_max_ms": t_max_ms, "pairs_all": int(pairs_all), "B_all": int(B_all), "build_s": build_s,
+            "P_rank": P, "M_rank": M}
+
+
+def _c3_cube(a, w, rank, world_size, local_rank, dev, stream, sl, owner_form: bool):
+    """The cube-hash form (wq_sharded_route_tick_device over RCCL): every rank holds the buckets it
+    owns and ingests M/N messages; a tick sends the remote ones to their owners as 20-byte slots and
+    gets back 12-byte row references + one pool of cube lists per owner, exchanges sized by budgets
+    from the previous tick (one host read per tick, at its end)."""
+    import torch
+    from worldql_server_amd.router import Router
+    lo, hi, (pos, world, sender, repl) = sl
+    M = hi - lo
     r = Router(w.cube_size, local_rank)
     r.set_stream(stream.cuda_stream)
     attach_rccl(r, rank, world_size)
@@ -305,13 +380,9 @@ def _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s):
     r.sharded_apply_ops(w.ops)
     build_s = time.perf_counter() - t0
     st = r.stats()
-    pos = torch.from_numpy(w.pos[lo:hi]).to(dev)
-    world = torch.from_numpy(w.world[lo:hi].view(np.int32)).to(dev)
-    sender = torch.from_numpy(w.sender[lo:hi].view(np.int32)).to(dev)
-    repl = torch.from_numpy(w.repl[lo:hi]).to(dev)
     offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
-    r.set_fanout_hint(40.0)  # C3's fan-out: the owners route with count / scan / emit
+    r.set_fanout_hint(40.0)
     cap = 64 * M + 1024
     peers = torch.empty(cap, dtype=torch.int32, device=dev)
     msgs = torch.empty(cap, dtype=torch.int32, device=dev)
@@ -326,27 +397,15 @@ def _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s):
     for _ in range(max(a.warmup, 1)):
         tick()
     t_ms = timed_ticks(tick, a.steps, stream, dev, world_size, [r])
+    exact, budgeted = r.shard_tick_stats()
     t_max_ms, pairs_all = reduce_over_ranks(t_ms, state["P"], dev, world_size)
     sent, _ = r.shard_last_bytes()  # the last timed tick's bytes to the other GPUs (xGMI)
     sent_max, _ = reduce_over_ranks(float(sent), 0, dev, world_size)
-    out = _line(a, world_size, pairs_all * a.steps / (t_max_ms / 1e3), t_max_ms / a.steps, "strong",
-                f"C3 over {world_size} GPUs by cube hash: 1M peers x 3x3x3, 10M LocalMessages/tick in total, "
-                "256 Zipf(1) Gaussian hotspots + 10% uniform, cube_size 16, ExceptSelf"
-                + ("" if a.scale == 1.0 else f" (scaled {a.scale})"),
-                {"messages_per_tick": M_all, "messages_per_gpu": M, "peers": w.n_peers,
-                 "subscriptions_this_shard": int(st["n_entries"]), "pairs_per_tick": int(pairs_all),
-                 "parallelism": f"cube-hash x{world_size} (wq_sharded_route_tick_device over RCCL: 20-byte slots "
-                                "out, row references + per-destination cube-list pools back)",
-                 "xgmi_bytes_per_gpu": int(sent_max), "table_build_s": round(build_s, 3),
-                 "generate_s": round(gen_s, 1)},
-                roofline(algorithmic_bytes(M_all, int(pairs_all), int(pairs_all)) // world_size, t_max_ms / a.steps / 1e3,
-                         "whole sharded tick per GPU (shard + exchanges + owner route + unshard); bytes = the "
-                         "tick's SURVEY §8(d) bytes / N"),
-                "synthetic (splitmix64, SURVEY.md §8(d) C3 generator)")
-    out["xgmi_model"] = _xgmi_model()
-    if not a.no_extra:
-        # SURVEY.md §8(e) step 5's other option: the same collective tick with the pairs left on the
-        # owner that routed them (wq_sharded_route_owner_device) — no return exchange
+    out = {"t_max_ms": t_max_ms, "pairs_all": int(pairs_all), "build_s": build_s,
+           "subscriptions_this_shard": int(st["n_entries"]), "xgmi_bytes_per_gpu": int(sent_max),
+           "exact_ticks": exact, "budgeted_ticks": budgeted}
+    if owner_form:
+        # SURVEY.md §8(e) step 5's other option: the pairs left on the owner (no return exchange)
         own = {"P": 0}
 
         def tick_owner():
@@ -355,39 +414,93 @@ def _run_c3_sharded(a, w, rank, world_size, local_rank, dev, gen_s):
         for _ in range(max(a.warmup, 1)):
             tick_owner()
         t_ms = timed_ticks(tick_owner, a.steps, stream, dev, world_size, [r])
-        t_max_ms, pairs_own = reduce_over_ranks(t_ms, own["P"], dev, world_size)
+        t2, pairs_own = reduce_over_ranks(t_ms, own["P"], dev, world_size)
         assert pairs_own == pairs_all, (pairs_own, pairs_all)  # every pair routed exactly once
-        out["extra"] = {"pairs_on_owner": {
-            "value": pairs_own * a.steps / (t_max_ms / 1e3), "unit": "pairs/s", "ms_per_step": t_max_ms / a.steps,
-            "n_gpus": world_size, "steps": a.steps, "warmup": a.warmup, "scaling": "strong",
-            "note": "same tick, pairs left on the owning GPU (no return all-to-all): "
-                    "shard -> RCCL all-to-all of the records -> route on the owners"}}
+        out["pairs_on_owner"] = {"value": pairs_own * a.steps / (t2 / 1e3), "unit": "pairs/s",
+                                 "ms_per_step": t2 / a.steps, "note": "same tick, pairs left on the owning GPU"}
     r.close()
-    if not a.no_extra:
-        # the alternative 288 GB of HBM allows: every GPU holds the WHOLE table (C3: ~10 GB; every op
-        # is applied on every GPU) and routes its own slice with the single-GPU tick — no exchange
-        rr = Router(w.cube_size, local_rank)
-        rr.set_stream(stream.cuda_stream)
-        rr.apply_ops(w.ops)
-        rr.set_fanout_hint(40.0)
-        cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
-
-        def tick_replica():
-            rr.route_device(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
-                            peers.data_ptr(), msgs.data_ptr(), cap, cnt.data_ptr())
-        for _ in range(max(a.warmup, 1)):
-            tick_replica()
-        t_ms = timed_ticks(tick_replica, a.steps, stream, dev, world_size, [rr])
-        P_rep = int(_counters(cnt).reshape(-1)[0]["n_pairs"])
-        t_max_ms, pairs_rep = reduce_over_ranks(t_ms, P_rep, dev, world_size)
-        assert pairs_rep == pairs_all, (pairs_rep, pairs_all)
-        out["extra"]["replicated_table"] = {
-            "value": pairs_rep * a.steps / (t_max_ms / 1e3), "unit": "pairs/s", "ms_per_step": t_max_ms / a.steps,
-            "n_gpus": world_size, "steps": a.steps, "warmup": a.warmup, "scaling": "strong",
-            "note": "every GPU holds the whole table (all ops applied everywhere) and routes its own M/N "
-                    "messages with the single-GPU tick: no exchange"}
-        rr.close()
+    del peers, msgs
     return out
+
+
+def _run_c3_multi(a, w, rank, world_size, local_rank, dev, gen_s):
+    """C3 over N GPUs, strong scaling (the 10M messages of a tick split over the ranks), both
+    multi-GPU forms measured in the same run on the same slices:
+      replicate   every GPU holds the whole table and routes its slice — the headline (DESIGN.md §6:
+                  C3's table is ~10 GB of 288 GB, so the exchange the cube-hash form needs buys
+                  nothing at this size; value = all ranks' pairs / the max-over-ranks time)
+      cube        the cube-hash sharded tick over RCCL (the form for tables beyond one GPU's HBM),
+                  under extra.cube_hash (--shard cube: the headline instead)
+    Each timed region: barrier + synchronize, K ticks, synchronize + barrier, max over ranks."""
+    import threading
+    import torch
+    head = "cube" if a.shard == "cube" else "replicate"
+    stream = torch.cuda.Stream(device=dev)
+    sl = _c3_slice(w, rank, world_size, dev)
+    M_all = len(w.world)
+    M = sl[1] - sl[0]
+    res = {}
+    forms = [head] if (world_size == 1 or a.no_extra) else [head, "cube" if head == "replicate" else "replicate"]
+
+    def line():
+        h = res[head]
+        t = h["t_max_ms"]
+        B = res["replicate"]["B_all"] if "replicate" in res else algorithmic_bytes(M_all, h["pairs_all"], h["pairs_all"])
+        par = (f"replicated table x{world_size} (every GPU holds all {len(w.ops)} subscriptions and routes its "
+               f"{M} of the {M_all} messages; no exchange)" if head == "replicate" else
+               f"cube-hash x{world_size} (wq_sharded_route_tick_device over RCCL: 20-byte slots out, row "
+               "references + per-destination cube-list pools back, budgeted exchanges)")
+        cfg = {"messages_per_tick": M_all, "messages_per_gpu": M, "peers": w.n_peers,
+               "pairs_per_tick": h["pairs_all"], "parallelism": par, "table_build_s": round(h["build_s"], 3),
+               "generate_s": round(gen_s, 1)}
+        if head == "cube":
+            cfg.update({k: h[k] for k in ("subscriptions_this_shard", "xgmi_bytes_per_gpu", "exact_ticks",
+                                          "budgeted_ticks")})
+        out = _line(a, world_size, h["pairs_all"] * a.steps / (t / 1e3), t / a.steps, "strong",
+                    f"C3 over {world_size} GPU(s): 1M peers x 3x3x3, 10M LocalMessages/tick in total, "
+                    "256 Zipf(1) Gaussian hotspots + 10% uniform, cube_size 16, ExceptSelf"
+                    + ("" if a.scale == 1.0 else f" (scaled {a.scale})"), cfg,
+                    roofline(B // world_size, t / a.steps / 1e3,
+                             "whole tick per GPU; bytes = the tick's SURVEY §8(d) bytes / N" +
+                             (" (count / tile_scan / emit on each GPU's slice)" if head == "replicate" else
+                              " (own-cube count + slots + exchanges + owner count + pools + emit)")),
+                    "synthetic (splitmix64, SURVEY.md §8(d) C3 generator)")
+        out["xgmi_model"] = _xgmi_model()
+        extra = {}
+        for f in forms[1:]:
+            if f in res:
+                x = res[f]
+                e = {"value": x["pairs_all"] * a.steps / (x["t_max_ms"] / 1e3), "unit": "pairs/s",
+                     "ms_per_step": x["t_max_ms"] / a.steps, "n_gpus": world_size, "scaling": "strong"}
+                e.update({k: v for k, v in x.items() if k not in ("t_max_ms", "pairs_all", "B_all")})
+                extra["cube_hash" if f == "cube" else "replicated_table"] = e
+            else:
+                extra["cube_hash" if f == "cube" else "replicated_table"] = {"error": "did not finish in time"}
+        if extra:
+            out["extra"] = extra
+        return out
+
+    for i, f in enumerate(forms):
+        dog = None
+        if i > 0:
+            # the second form must not cost the headline: if it hangs (an RCCL collective that
+            # never completes), rank 0 prints the headline line and every rank leaves
+            def bail():
+                if rank == 0:
+                    print(json.dumps(line()), flush=True)
+                os._exit(0)
+            dog = threading.Timer(300.0, bail)
+            dog.daemon = True
+            dog.start()
+        if f == "replicate":
+            res[f] = _c3_replicated(a, w, rank, world_size, local_rank, dev, stream, sl)
+        else:
+            res[f] = _c3_cube(a, w, rank, world_size, local_rank, dev, stream, sl, owner_form=not a.no_extra)
+        if dog:
+            dog.cancel()
+    if "replicate" in res and "cube" in res:
+        assert res["replicate"]["pairs_all"] == res["cube"]["pairs_all"]  # the same pairs either way
+    return line()
 
 
 def _cpu_route_sample(w, seconds, name):

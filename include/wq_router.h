@@ -108,11 +108,49 @@ int wq_router_create(uint16_t cube_size, int device, wq_router** out);
  *   wq_route_global[_device], wq_get_stats
  *   wq_set_radius, wq_set_peer_positions[_device], wq_set_fanout_hint, wq_route_health: every shard
  * Device-pointer calls take arrays on devices[0], ordered after the handle's stream (wq_set_stream),
- * and are synchronous on return. The sharded entry points (wq_shard_*, wq_sharded_*) and the
- * instrumentation hooks are for single-device handles. */
+ * and are synchronous on return — except wq_apply_ops_device, which keeps the single-GPU contract:
+ * an invalid batch is not applied and shows as error bit 16 of wq_route_health (the call returns
+ * WQ_OK); on the replicate layout it is also asynchronous. The cube-hash layout partitions a device
+ * batch by owner on devices[0] (one read-back of the per-shard counts). The sharded entry points
+ * (wq_shard_*, wq_sharded_*) and the instrumentation hooks are for single-device handles. */
 int wq_router_create_multi(uint16_t cube_size, int n_gpus, const int* devices, wq_router** out);
-/* Shards behind a handle (1 for wq_router_create). */
+/* The same with the layout chosen (wq_router_create_multi = WQ_MULTI_CUBE_HASH):
+ *   WQ_MULTI_CUBE_HASH  the table partitioned by cube hash, as above (tables beyond one GPU's HBM);
+ *   WQ_MULTI_REPLICATE  every device holds the WHOLE table and routes its own slice of a tick with
+ *                       the single-GPU tick — no exchange at all (C3's table is ~10 GB of 288 GB).
+ *                       Every op is applied on every device (the op stream is the only thing all
+ *                       devices see); wq_apply_ops_device stays asynchronous; queries go to device 0.
+ * Results are the one-table results either way. */
+#define WQ_MULTI_CUBE_HASH 0
+#define WQ_MULTI_REPLICATE 1
+int wq_router_create_multi_mode(uint16_t cube_size, int n_gpus, const int* devices, int mode, wq_router** out);
+/* Sub-handles behind a handle (1 for wq_router_create), and the layout (-1 for a single-GPU handle). */
 int wq_multi_info(wq_router* h, uint32_t* n_gpus);
+int wq_multi_mode(wq_router* h, int* mode);
+/* The scaling form of a multi-GPU tick: every device routes the messages it ingested and keeps its
+ * CSR (no pair crosses to devices[0]). in[g] = the messages on devices[g] (device pointers there,
+ * complete before the call; keys or positions as wq_route_tick); out[g] = views into the handle's
+ * workspace on devices[g], valid until the next call on the handle: offsets[n_msgs + 1] (from 0),
+ * peers[n_pairs], msgs[n_pairs] (the index within the slice; NULL unless with_msgs). Per message
+ * the recipients are exactly wq_route_tick's for the same message on one table. Synchronous. */
+typedef struct wq_msg_slice {
+    const double* d_pos;
+    const int64_t* d_keys;
+    const uint32_t* d_world;
+    const uint32_t* d_sender;
+    const uint8_t* d_repl;
+    uint64_t n_msgs;
+} wq_msg_slice;
+typedef struct wq_slice_view {
+    int32_t device;
+    uint32_t pad_;
+    uint64_t n_msgs;
+    uint64_t n_pairs;
+    const uint32_t* offsets;
+    const uint32_t* peers;
+    const uint32_t* msgs;
+} wq_slice_view;
+int wq_route_tick_slices_device(wq_router* h, const wq_msg_slice* in, int with_msgs, wq_slice_view* out);
 int wq_router_destroy(wq_router* h);
 const char* wq_last_error(const wq_router* h);
 /* Use the caller's HIP stream (hipStream_t as void*); NULL restores the handle's own stream. */
@@ -274,10 +312,14 @@ int wq_route_records_device(wq_router* h, const wq_msg_rec* d_recs, size_t n_msg
  *                                   return for those messages on one GPU holding the whole table
  *                                   (offsets[M+1] and peers[P] in message order, msgs[P] optional).
  * The tick is collective: all G shards call it (M may be 0), each on its own thread or process.
- * It reads two small count vectors back to the host (the exchange sizes) and is synchronous on
- * return; *n_pairs = P. If P > capacity the tick still completes (its peers are not left waiting),
- * returns WQ_E_CAPACITY with offsets written, and wq_sharded_copy_out re-copies the kept result
- * into a larger buffer without another exchange. Exchange failures return WQ_E_RCCL.
+ * Its exchanges are sized by budgets every shard derives from the previous tick's sizes (both ends
+ * of a pair agree without a read-back), so it reads the device once, at its end, and is synchronous
+ * on return; *n_pairs = P. The first tick, and a tick whose sizes outgrew a budget (every shard
+ * learns it from the exchanged status words and all redo the tick), read the sizes back first. If
+ * P > capacity the tick still completes (its peers are not left waiting), returns WQ_E_CAPACITY
+ * with offsets written, and wq_sharded_copy_out re-copies the kept result into a larger buffer
+ * without another exchange — as long as the table is unchanged since (WQ_E_INVALID otherwise).
+ * Exchange failures return WQ_E_RCCL.
  * Exchanges: RCCL (one process per GPU, or several handles of one process), an in-process hub
  * (G handles of one process, peer copies over xGMI), or the caller's own all-to-all. */
 #define WQ_RCCL_ID_BYTES 128
@@ -312,6 +354,9 @@ int wq_sharded_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, ui
  * wq_shard_last_bytes: bytes this shard sent to / received from OTHER shards in its latest sharded
  * tick (the xGMI volume; the self segment is not counted). */
 int wq_shard_last_bytes(wq_router* h, uint64_t* sent, uint64_t* received);
+/* Slot ticks run exactly (the sizes read back twice: the first tick, or a redo after a tick outgrew
+ * its budgets) and on budgets (one host read per tick, at its end), on this shard so far. */
+int wq_shard_tick_stats(wq_router* h, uint64_t* exact, uint64_t* budgeted);
 /* Test / tuning hook: 1 = the sharded tick returns expanded pairs even with the radius filter off
  * (the earlier form), 0 = row references and pools (default). Results are identical. */
 int wq_debug_set_shard_form(wq_router* h, int expanded);

@@ -8,6 +8,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "world_map.hpp"
 
 using namespace worldql;
@@ -21,9 +23,10 @@ static int g_fail = 0;
         }                                                              \
     } while (0)
 
-// devs empty: one GPU (wq_router_create); else one handle over those devices (wq_router_create_multi)
+// devs empty: one GPU (wq_router_create); else one handle over those devices (wq_router_create_multi_mode)
+static int g_mode = WQ_MULTI_CUBE_HASH;
 static WorldMap* make_map(const std::vector<int>& devs) {
-    return devs.empty() ? new WorldMap(16) : new WorldMap(16, devs);
+    return devs.empty() ? new WorldMap(16) : new WorldMap(16, devs, g_mode);
 }
 
 static void area_subscriptions(const std::vector<int>& devs) {
@@ -140,6 +143,79 @@ static void multi_route(const std::vector<int>& devs) {
     CHECK(r.peers.size() > M);  // the neighbourhoods overlap: plenty of recipients
 }
 
+// The scaling form: each device's own messages routed where they are (wq_route_tick_slices_device);
+// every view must hold, per message, what the map's membership queries say.
+static void slices_route(const std::vector<int>& devs) {
+    if (devs.empty()) return;
+    std::unique_ptr<WorldMap> wmp(make_map(devs));
+    WorldMap& wm = *wmp;
+    AreaMap& map = wm.get_mut("world");
+    std::vector<wq_op> ops;
+    uint64_t x = 777;
+    auto rnd = [&]() { x = x * 6364136223846793005ull + 1442695040888963407ull; return (double)(x >> 11) * 0x1p-53; };
+    for (uint32_t p = 0; p < 300; ++p)
+        for (int k = 0; k < 3; ++k) {
+            wq_op op{};
+            op.world = map.world_id();
+            op.peer = p;
+            op.kind = WQ_OP_SUBSCRIBE;
+            op.u.pos[0] = rnd() * 64 - 32, op.u.pos[1] = rnd() * 64 - 32, op.u.pos[2] = rnd() * 64 - 32;
+            ops.push_back(op);
+        }
+    wm.apply_ops(ops);
+    const size_t G = devs.size(), per = 1000;
+    std::vector<std::vector<double>> pos(G, std::vector<double>(3 * per));
+    std::vector<std::vector<uint32_t>> sender(G, std::vector<uint32_t>(per));
+    std::vector<std::vector<uint8_t>> repl(G, std::vector<uint8_t>(per));
+    std::vector<wq_msg_slice> in(G);
+    std::vector<void*> bufs;
+    for (size_t g = 0; g < G; ++g) {
+        for (size_t i = 0; i < per; ++i) {
+            for (int d = 0; d < 3; ++d) pos[g][3 * i + d] = rnd() * 64 - 32;
+            sender[g][i] = (uint32_t)(rnd() * 300);
+            repl[g][i] = (uint8_t)(rnd() * 3);
+        }
+        std::vector<uint32_t> world(per, map.world_id());
+        CHECK(hipSetDevice(devs[g]) == hipSuccess);
+        void *dp, *dw, *ds, *dr;
+        CHECK(hipMalloc(&dp, per * 24) == hipSuccess && hipMalloc(&dw, per * 4) == hipSuccess &&
+              hipMalloc(&ds, per * 4) == hipSuccess && hipMalloc(&dr, per) == hipSuccess);
+        CHECK(hipMemcpy(dp, pos[g].data(), per * 24, hipMemcpyHostToDevice) == hipSuccess);
+        CHECK(hipMemcpy(dw, world.data(), per * 4, hipMemcpyHostToDevice) == hipSuccess);
+        CHECK(hipMemcpy(ds, sender[g].data(), per * 4, hipMemcpyHostToDevice) == hipSuccess);
+        CHECK(hipMemcpy(dr, repl[g].data(), per, hipMemcpyHostToDevice) == hipSuccess);
+        bufs.insert(bufs.end(), {dp, dw, ds, dr});
+        in[g] = wq_msg_slice{static_cast<const double*>(dp), nullptr, static_cast<const uint32_t*>(dw),
+                             static_cast<const uint32_t*>(ds), static_cast<const uint8_t*>(dr), per};
+    }
+    const std::vector<wq_slice_view> v = wm.route_slices(in);
+    size_t bad = 0, pairs = 0;
+    for (size_t g = 0; g < G; ++g) {
+        CHECK(v[g].device == devs[g] && v[g].n_msgs == per);
+        std::vector<uint32_t> offs(per + 1), peers(v[g].n_pairs);
+        CHECK(hipSetDevice(v[g].device) == hipSuccess);
+        CHECK(hipMemcpy(offs.data(), v[g].offsets, (per + 1) * 4, hipMemcpyDeviceToHost) == hipSuccess);
+        if (!peers.empty())
+            CHECK(hipMemcpy(peers.data(), v[g].peers, peers.size() * 4, hipMemcpyDeviceToHost) == hipSuccess);
+        CHECK(offs[per] == v[g].n_pairs);
+        for (size_t i = 0; i < per && bad < 5; ++i) {
+            std::vector<uint32_t> want;
+            for (uint32_t p : map.get_subscribed_peers(Vector3{pos[g][3 * i], pos[g][3 * i + 1], pos[g][3 * i + 2]})) {
+                const bool keep = repl[g][i] == WQ_REPL_INCLUDING_SELF ? true
+                                  : repl[g][i] == WQ_REPL_ONLY_SELF    ? p == sender[g][i]
+                                                                       : p != sender[g][i];
+                if (keep) want.push_back(p);
+            }
+            const std::vector<uint32_t> got(peers.begin() + offs[i], peers.begin() + offs[i + 1]);
+            if (got != want) ++bad;
+        }
+        pairs += peers.size();
+    }
+    CHECK(bad == 0);
+    CHECK(pairs > G * per);
+    for (void* b : bufs) (void)hipFree(b);
+}
+
 static void sanitize() {
     auto ok = [](const char* in, const char* want) {
         std::string out;
@@ -174,12 +250,17 @@ int main(int argc, char** argv) {
         std::printf(g_fail ? "FAILED\n" : "host ok\n");
         return g_fail ? 1 : 0;
     }
-    // one GPU, then one handle over G = 1, 2, 3 shards (all on device 0 here)
+    // one GPU, then one handle over G = 1, 2, 3 devices (all device 0 here), in both layouts
     const std::vector<std::vector<int>> configs = {{}, {0}, {0, 0}, {0, 0, 0}};
-    for (const auto& devs : configs) {
-        area_subscriptions(devs);
-        world_subscriptions(devs);
-        multi_route(devs);
+    for (int mode : {WQ_MULTI_CUBE_HASH, WQ_MULTI_REPLICATE}) {
+        g_mode = mode;
+        for (const auto& devs : configs) {
+            if (mode == WQ_MULTI_REPLICATE && devs.empty()) continue;  // ran once already
+            area_subscriptions(devs);
+            world_subscriptions(devs);
+            multi_route(devs);
+            slices_route(devs);
+        }
     }
     std::printf(g_fail ? "FAILED (%d)\n" : "ok\n", g_fail);
     return g_fail ? 1 : 0;

@@ -18,10 +18,13 @@ def binary(tmp_path_factory):
         build()
     out = str(tmp_path_factory.mktemp("cpp") / "test_world_map")
     libdir = os.path.dirname(LIB)
-    subprocess.check_call(["g++", "-std=c++17", "-O1", "-Wall", "-Wextra",
+    # the slices test stages its messages on each device itself: the HIP host API (no device code)
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-Wall", "-Wextra", "-D__HIP_PLATFORM_AMD__",
                            "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "worldql_server_amd", "cpp"),
+                           "-I", "/opt/rocm/include",
                            os.path.join(ROOT, "tests", "cpp", "test_world_map.cpp"), "-o", out,
-                           "-L", libdir, "-lwq_router", f"-Wl,-rpath,{libdir}"])
+                           "-L", libdir, "-lwq_router", f"-Wl,-rpath,{libdir}",
+                           "-L", "/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"])
     return out
 
 

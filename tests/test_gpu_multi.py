@@ -1,7 +1,8 @@
-"""One handle over G GPUs (wq_router_create_multi, csrc/wq_multi.hip) against the oracle: the
+"""One handle over G GPUs (wq_router_create_multi_mode, csrc/wq_multi.hip) against the oracle: the
 reference keeps ONE WorldMap in one task (worldql_server/src/processing/thread.rs:119), and the
-multi handle must answer every call with that one table's result. G in {1, 2, 3} shards, all on
-cuda:0 here (the box has one GPU; devices may repeat)."""
+multi handle must answer every call with that one table's result, in both layouts (cube-hash shards,
+and replicas of the whole table). G in {1, 2, 3}, all on cuda:0 here (the box has one GPU; devices
+may repeat)."""
 import numpy as np
 import pytest
 
@@ -21,14 +22,18 @@ def _workload():
     return w, abi.concat_ops([un, rm])
 
 
+MODES = ["cube", "replicate"]
+
+
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("G", [1, 2, 3])
-def test_multi_handle_is_one_table(G):
+def test_multi_handle_is_one_table(G, mode):
     import torch
     from worldql_server_amd.router import Router
     w, churn = _workload()
     M = len(w.world)
-    r = Router.multi(16, [0] * G)
-    assert r.n_gpus() == G
+    r = Router.multi(16, [0] * G, mode=mode)
+    assert r.n_gpus() == G and r.multi_mode() == {"cube": abi.MULTI_CUBE_HASH, "replicate": abi.MULTI_REPLICATE}[mode]
     o = orc.COracle(16)
     r.apply_ops(w.ops)
     o.apply_ops(w.ops)
@@ -102,14 +107,15 @@ def test_multi_handle_is_one_table(G):
     r.close()
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("G", [2, 3])
-def test_multi_handle_radius_filter(G):
+def test_multi_handle_radius_filter(G, mode):
     """C5's exact radius filter through the multi handle: positions and radius go to every shard."""
     from worldql_server_amd.router import Router
     w = synth.uniform_box(33, 3000, 9000, 64.0, neighbourhood=True, repl_mode="mixed")
     rng = np.random.default_rng(33)
     peer_pos = rng.uniform(-64, 64, (3000, 3))
-    r = Router.multi(16, [0] * G)
+    r = Router.multi(16, [0] * G, mode=mode)
     r.apply_ops(w.ops)
     r.set_peer_positions(peer_pos)
     r.set_radius(14.0)
@@ -118,4 +124,151 @@ def test_multi_handle_radius_filter(G):
     offs, peers, _ = r.route(w.pos, w.world, w.sender, w.repl)
     wo_, wp_ = o.route_radius(w.pos, w.world, w.sender, w.repl, peer_pos, 14.0)[:2]
     assert (offs == wo_).all() and (peers == wp_).all() and len(peers) > 0
+    r.close()
+
+
+def _dev_slices(w, G, dev):
+    """G contiguous slices of the tick's messages as device tensors (one per device of the handle)."""
+    import torch
+    M = len(w.world)
+    out = []
+    for g in range(G):
+        lo, hi = M * g // G, M * (g + 1) // G
+        t = (torch.from_numpy(np.ascontiguousarray(w.pos[lo:hi])).to(dev),
+             torch.from_numpy(np.ascontiguousarray(w.world[lo:hi]).view(np.int32)).to(dev),
+             torch.from_numpy(np.ascontiguousarray(w.sender[lo:hi]).view(np.int32)).to(dev),
+             torch.from_numpy(np.ascontiguousarray(w.repl[lo:hi])).to(dev))
+        out.append((lo, hi, t))
+    torch.cuda.synchronize()
+    return out
+
+
+class _DevWords:
+    """32-bit words at a device address, for torch.as_tensor (__cuda_array_interface__)."""
+
+    def __init__(self, ptr, n):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i4", "data": (ptr, True), "version": 3}
+
+
+def _view_arrays(v):
+    """A slice view's CSR (device pointers into the handle's workspace) copied to the host."""
+    import torch
+    n, P = int(v.n_msgs), int(v.n_pairs)
+
+    def get(ptr, cnt):
+        if cnt == 0:
+            return np.empty(0, np.uint32)
+        return torch.as_tensor(_DevWords(ptr, cnt), device="cuda:0").cpu().numpy().view(np.uint32)
+    return get(v.offsets, n + 1), get(v.peers, P), (get(v.msgs, P) if v.msgs else None)
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("G", [1, 2, 3])
+def test_multi_slices_stay_on_their_devices(G, mode):
+    """wq_route_tick_slices_device: every device routes its own ingested slice and keeps its CSR
+    (the scaling form: no pair crosses to devices[0]); each view equals the oracle's CSR of that
+    slice, twice (the second reuses the staging)."""
+    import torch
+    from worldql_server_amd.router import Router
+    w, churn = _workload()
+    r = Router.multi(16, [0] * G, mode=mode)
+    o = orc.COracle(16)
+    for ops in (w.ops, churn):
+        r.apply_ops(ops)
+        o.apply_ops(ops)
+    dev = torch.device("cuda:0")
+    sl = _dev_slices(w, G, dev)
+    for _ in range(2):
+        views = r.route_slices_device([(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), hi - lo)
+                                       for lo, hi, t in sl], with_msgs=True)
+        for (lo, hi, _), v in zip(sl, views):
+            want_offs, want_peers, _ = o.route(w.pos[lo:hi], w.world[lo:hi], w.sender[lo:hi], w.repl[lo:hi])
+            offs, peers, msgs = _view_arrays(v)
+            assert v.device == 0 and v.n_msgs == hi - lo
+            assert (offs == want_offs).all() and (peers == want_peers).all()
+            assert (msgs == np.repeat(np.arange(hi - lo, dtype=np.uint32), np.diff(want_offs.astype(np.int64)))).all()
+    assert r.route_health() == (0, 0)
+    r.close()
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_multi_device_batches(mode):
+    """wq_apply_ops_device on a multi handle keeps the single-GPU contract: a valid batch
+    is applied (cube hash: partitioned by owner on devices[0]; replicate: on every replica,
+    asynchronously), a batch holding an invalid op is not applied at all, the call returns WQ_OK and
+    wq_route_health reports error bit 16."""
+    import torch
+    from worldql_server_amd.router import Router
+    w, churn = _workload()
+    G = 3
+    r = Router.multi(16, [0] * G, mode=mode)
+    o = orc.COracle(16)
+    r.apply_ops(w.ops)
+    o.apply_ops(w.ops)
+    sub_unsub = churn[churn["kind"] != abi.OP_REMOVE_PEER]
+    dev = torch.device("cuda:0")
+    d_ops = torch.from_numpy(np.ascontiguousarray(sub_unsub).view(np.uint8).copy()).to(dev)
+    torch.cuda.synchronize()
+    r.apply_ops_device(d_ops.data_ptr(), len(sub_unsub))
+    o.apply_ops(sub_unsub)
+    want_offs, want_peers, _ = o.route(w.pos, w.world, w.sender, w.repl)
+    offs, peers, _ = r.route(w.pos, w.world, w.sender, w.repl)
+    assert (offs == want_offs).all() and (peers == want_peers).all()
+    assert r.route_health() == (0, 0)
+    bad = np.ascontiguousarray(w.ops[:50]).copy()
+    bad["kind"] = abi.OP_UNSUBSCRIBE
+    bad["kind"][17] = abi.OP_REMOVE_PEER
+    d_bad = torch.from_numpy(bad.view(np.uint8).copy()).to(dev)
+    torch.cuda.synchronize()
+    r.apply_ops_device(d_bad.data_ptr(), len(bad))  # returns WQ_OK: the rejection is in the health bits
+    offs, peers, _ = r.route(w.pos, w.world, w.sender, w.repl)
+    assert (offs == want_offs).all() and (peers == want_peers).all()  # nothing of it applied
+    err, _ = r.route_health()
+    assert err & 16, err
+    r.close()
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_multi_health_counts_only_the_callers_capacity(mode):
+    """the multi handle's internal staging starts at 16 pairs per message and grows; that
+    must not show as an overflow in wq_route_health when the caller's own capacity was enough —
+    while a caller capacity that is too small must."""
+    import torch
+    from worldql_server_amd.router import Router
+    w = synth.uniform_box(37, 400, 3000, 24.0, neighbourhood=True, repl_mode="mixed")  # ~100 per message
+    G = 2
+    r = Router.multi(16, [0] * G, mode=mode)
+    o = orc.COracle(16)
+    r.apply_ops(w.ops)
+    o.apply_ops(w.ops)
+    want_offs, want_peers, _ = o.route(w.pos, w.world, w.sender, w.repl)
+    assert len(want_peers) > 20 * len(w.world)
+    offs, peers, _ = r.route(w.pos, w.world, w.sender, w.repl, capacity=len(want_peers) + 10)
+    assert (peers == want_peers).all()
+    assert r.route_health() == (0, 0)
+    from worldql_server_amd.router import WQError
+    with pytest.raises(WQError):
+        r.route(w.pos, w.world, w.sender, w.repl, capacity=len(want_peers) // 2)
+    assert r.route_health()[1] == 1
+    r.close()
+
+
+def test_multi_global_route_keeps_shard_errors():
+    """wq_route_health on a multi handle ORs its own words into the shards' bits (a route
+    on the handle's own any-keys must not overwrite a shard's error)."""
+    import torch
+    from worldql_server_amd.router import Router
+    w, _ = _workload()
+    r = Router.multi(16, [0] * 2, mode="cube")
+    r.apply_ops(w.ops)
+    r.route_global(np.array([0, 1], np.uint32), np.array([1, 2], np.uint32), np.array([0, 0], np.uint8))
+    dev = torch.device("cuda:0")
+    bad = np.ascontiguousarray(w.ops[:8]).copy()
+    bad["world"][3] = abi.WORLD_INVALID
+    d_bad = torch.from_numpy(bad.view(np.uint8).copy()).to(dev)
+    torch.cuda.synchronize()
+    r.apply_ops_device(d_bad.data_ptr(), len(bad))
+    r.route_global(np.array([0], np.uint32), np.array([1], np.uint32), np.array([0], np.uint8))
+    err, _ = r.route_health()
+    assert err & 16, err
     r.close()

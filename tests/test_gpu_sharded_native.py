@@ -492,3 +492,103 @@ def test_hub_full_c3_two_shards_route_check():
         # what crossed: far less than the expanded pairs a remote owner would otherwise return
         assert 0 < sent < 4 * len(peers), (sent, len(peers))
     assert P > 4e8
+
+
+def _run_shards(G, body, timeout=300):
+    errors = []
+
+    def wrap(rank):
+        try:
+            body(rank)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=wrap, args=(k,)) for k in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout)
+    assert not errors, errors
+
+
+def test_hub_budgeted_ticks_grow_and_redo():
+    """The slot tick's exchanges are sized by budgets from the previous tick (no read-back before
+    them): the first tick runs exact, the next on budgets; a tick with twice the messages outgrows
+    them, every shard learns it from the exchanged status words and all redo that tick exactly; the
+    results are the whole-table oracle's every time."""
+    import torch
+    from worldql_server_amd.router import Hub, Router
+    w, _ = _workload(seed=23)
+    M = len(w.world)
+    G = 3
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    results = [None] * G
+
+    def body(rank):
+        r = routers[rank]
+        r.attach_hub(hub, rank)
+        r.sharded_apply_ops(w.ops)
+        lo, hi = _slice(M, G, rank)
+        half = lo + (hi - lo) // 2
+        got = [_tick(r, w, lo, half, dev), _tick(r, w, lo, half, dev), _tick(r, w, lo, hi, dev),
+               _tick(r, w, lo, hi, dev), _tick(r, w, lo, lo + 7, dev)]
+        results[rank] = (got, r.shard_tick_stats())
+
+    _run_shards(G, body)
+    for rank in range(G):
+        lo, hi = _slice(M, G, rank)
+        half = lo + (hi - lo) // 2
+        got, (exact, budgeted) = results[rank]
+        for g, (a, b) in zip(got, [(lo, half), (lo, half), (lo, hi), (lo, hi), (lo, lo + 7)]):
+            _check(g, _expected([w.ops], w, a, b), b - a)
+        # tick 1 exact; 2 budgeted; 3 budgeted, outgrown, redone exact; 4 and 5 budgeted
+        assert (exact, budgeted) == (2, 4), (exact, budgeted)
+    for r in routers:
+        r.close()
+    hub.close()
+
+
+def test_copy_out_after_a_table_change_is_refused():
+    """a slot tick's own-cube rows point into the table, so wq_sharded_copy_out after any
+    change of the table (here an op batch) must refuse instead of mixing old counts with new lists."""
+    import torch
+    from worldql_server_amd.router import Hub, Router, WQError
+    w, churn = _workload(seed=29)
+    M = len(w.world)
+    G = 2
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    codes = [None] * G
+
+    def body(rank):
+        r = routers[rank]
+        r.attach_hub(hub, rank)
+        r.sharded_apply_ops(w.ops)
+        lo, hi = _slice(M, G, rank)
+        n = hi - lo
+        pos = torch.from_numpy(np.ascontiguousarray(w.pos[lo:hi])).to(dev)
+        wo = torch.from_numpy(np.ascontiguousarray(w.world[lo:hi]).view(np.int32)).to(dev)
+        se = torch.from_numpy(np.ascontiguousarray(w.sender[lo:hi]).view(np.int32)).to(dev)
+        rp = torch.from_numpy(np.ascontiguousarray(w.repl[lo:hi])).to(dev)
+        offs = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        small = torch.empty(8, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(dev)
+        rc, P = r.sharded_route_device(pos.data_ptr(), wo.data_ptr(), se.data_ptr(), rp.data_ptr(), n,
+                                       offs.data_ptr(), small.data_ptr(), None, 8)
+        assert rc == abi.WQ_E_CAPACITY and P > 8
+        r.sharded_apply_ops(churn)
+        big = torch.empty(P, dtype=torch.int32, device=dev)
+        try:
+            r.sharded_copy_out(offs.data_ptr(), big.data_ptr(), None, P)
+            codes[rank] = 0
+        except WQError as e:
+            codes[rank] = e.code
+
+    _run_shards(G, body)
+    assert codes == [abi.WQ_E_INVALID] * G
+    for r in routers:
+        r.close()
+    hub.close()

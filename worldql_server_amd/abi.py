@@ -87,6 +87,22 @@ class OwnerView(ctypes.Structure):
                 ("n_recs", ctypes.c_uint64), ("n_pairs", ctypes.c_uint64), ("seg", ctypes.c_uint32 * (MAX_SHARDS + 1))]
 
 
+# wq_router_create_multi_mode layouts
+MULTI_CUBE_HASH = 0
+MULTI_REPLICATE = 1
+
+
+class MsgSlice(ctypes.Structure):  # struct wq_msg_slice: one device's ingested messages
+    _fields_ = [("d_pos", ctypes.c_void_p), ("d_keys", ctypes.c_void_p), ("d_world", ctypes.c_void_p),
+                ("d_sender", ctypes.c_void_p), ("d_repl", ctypes.c_void_p), ("n_msgs", ctypes.c_uint64)]
+
+
+class SliceView(ctypes.Structure):  # struct wq_slice_view: one device's CSR, left on that device
+    _fields_ = [("device", ctypes.c_int32), ("pad_", ctypes.c_uint32), ("n_msgs", ctypes.c_uint64),
+                ("n_pairs", ctypes.c_uint64), ("offsets", ctypes.c_void_p), ("peers", ctypes.c_void_p),
+                ("msgs", ctypes.c_void_p)]
+
+
 # struct wq_msg_rec: 40 bytes on the wire between GPUs
 REC_POS = 1  # wq_msg_rec.flags: key holds the f64 position bits (radius filter on)
 MSG_REC_DTYPE = np.dtype({

@@ -101,10 +101,11 @@ class WorldMap {
         int rc = wq_router_create(cube_size, device, &h_);
         if (rc) throw Error(rc, std::string("wq_router_create: ") + wq_last_error(nullptr));
     }
-    // The same map over several GPUs behind one handle (wq_router_create_multi; devices may repeat).
-    WorldMap(uint16_t cube_size, const std::vector<int>& devices) {
-        int rc = wq_router_create_multi(cube_size, (int)devices.size(), devices.data(), &h_);
-        if (rc) throw Error(rc, std::string("wq_router_create_multi: ") + wq_last_error(nullptr));
+    // The same map over several GPUs behind one handle (wq_router_create_multi_mode; devices may
+    // repeat): WQ_MULTI_CUBE_HASH shards the table, WQ_MULTI_REPLICATE holds it whole on each device.
+    WorldMap(uint16_t cube_size, const std::vector<int>& devices, int mode = WQ_MULTI_CUBE_HASH) {
+        int rc = wq_router_create_multi_mode(cube_size, (int)devices.size(), devices.data(), mode, &h_);
+        if (rc) throw Error(rc, std::string("wq_router_create_multi_mode: ") + wq_last_error(nullptr));
     }
     ~WorldMap() {
         for (auto& kv : maps_) delete kv.second;
@@ -157,6 +158,13 @@ class WorldMap {
         check(rc);
         r.peers.resize(n);
         return r;
+    }
+    // The scaling form over the handle's devices: slice g's messages (device pointers on device g)
+    // routed there, each CSR left on its device (wq_route_tick_slices_device).
+    std::vector<wq_slice_view> route_slices(const std::vector<wq_msg_slice>& slices, bool with_msgs = false) {
+        std::vector<wq_slice_view> v(slices.size());
+        check(wq_route_tick_slices_device(h_, slices.data(), with_msgs ? 1 : 0, v.data()));
+        return v;
     }
     wq_router* handle() { return h_; }
     void check(int rc) const {

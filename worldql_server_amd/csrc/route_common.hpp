@@ -80,6 +80,14 @@ __device__ __forceinline__ void check_stale(const TableView& t, wq_route_counter
 constexpr int kSlotWords = 5;
 constexpr uint32_t kSlotReg = 0, kSlotHead = 1, kSlotTail = 2;
 
+// Budgeted slot segments of the sharded tick (wq_shard.hip launch_budget_slots): owner d's slots at
+// [base[d], base[d] + budget[d]) of the send buffer.
+struct SlotLayout {
+    uint32_t base[WQ_MAX_SHARDS + 1];
+    uint32_t budget[WQ_MAX_SHARDS];
+};
+constexpr uint32_t kStBudget = 0x80000000u;  // exchange status bit: some budget of the tick was too small
+
 struct RouteIn {
     const double* pos;
     const int64_t* keys;
@@ -89,6 +97,11 @@ struct RouteIn {
     uint32_t M;
     int64_t si;
     const uint32_t* slots = nullptr;  // count_kernel<..., SLOTS = true>: M compact slots instead of the above
+    uint32_t own_G = 1, own_me = 0;   // count_kernel<..., OWN = true>: count only shard own_me's cubes of own_G
 };
+
+// info.x of a row the sharded tick's owner shipped back: word offset into the received cube-list
+// pool (both locator flags set; only ever decoded when EmitParams::pool is set)
+constexpr uint32_t kLocPool = 0xC0000000u;
 
 }  // namespace wq

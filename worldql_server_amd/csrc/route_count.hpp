@@ -58,7 +58,10 @@ constexpr uint32_t kStDone = 0, kStProbe = 1, kStVerify = 2;
 // m >= in.M), with F (candidates) and E (recipients) accumulated into the caller's sums.
 // FULL: the whole record line is read in the first round (the sender filter then needs no extra
 // round) and its peer chunks 2-7 are handed back in peers_out (FULL only; valid for inline records).
-template <bool RAW_KEYS, int IPT, int DBG = 0, bool FULL = false, bool SLOTS = false>
+// OWN (the sharded tick's ingesting GPU, route_common.hpp RouteIn::own_*): only the messages whose
+// cube this shard owns are counted; every other message gets e = 0 here (its row comes back from
+// its owner, wq_sharded.hip).
+template <bool RAW_KEYS, int IPT, int DBG = 0, bool FULL = false, bool SLOTS = false, bool OWN = false>
 __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& tv, uint32_t m0,
                                            uint32_t (&e_out)[IPT], uint2 (&inf_out)[IPT], uint64_t& F_local,
                                            uint32_t& E_local, uint4 (*peers_out)[6] = nullptr) {
@@ -106,7 +109,7 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
         const uint32_t m = m0 + i * kBlock + tid;
-        const bool valid = m < in.M && in_kind[i] != kSlotTail;
+        bool valid = m < in.M && in_kind[i] != kSlotTail;
         const uint32_t w = in_w[i];
         int64_t x = 0, y = 0, z = 0;
         pk[i] = 0;
@@ -133,6 +136,7 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
                 z = coord_clamp_dev(__longlong_as_double((long long)in_c[i][2]), tv.sf, in.si);
             }
             reg = pack_key(w, x, y, z, tv.sf, &pk[i], &ext[i]);
+            if (OWN) valid = valid && shard_of(w, x, y, z, in.own_G) == in.own_me;
         }
         // lanes with nothing to probe read a dummy line spread by message index (never one shared
         // line: a chip-wide hot line serialises on its L2 channel)
@@ -283,7 +287,7 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
     }
 }
 
-template <bool RAW_KEYS, int IPT, int MINW, int DBG = 0, bool FULL = false, bool SLOTS = false>
+template <bool RAW_KEYS, int IPT, int MINW, int DBG = 0, bool FULL = false, bool SLOTS = false, bool OWN = false>
 __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
     __shared__ uint64_t wave_F[kWaves];
     __shared__ uint64_t wave_E[kWaves];
@@ -301,7 +305,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
         uint32_t E_local = 0;
         uint32_t e_out[IPT];
         uint2 inf_out[IPT];
-        count_rows<RAW_KEYS, IPT, DBG, FULL, SLOTS>(p.in, p.t, m0, e_out, inf_out, F_local, E_local);
+        count_rows<RAW_KEYS, IPT, DBG, FULL, SLOTS, OWN>(p.in, p.t, m0, e_out, inf_out, F_local, E_local);
 #pragma unroll
         for (int i = 0; i < IPT; ++i) {
             const uint32_t m = m0 + i * kBlock + tid;

@@ -22,6 +22,9 @@ struct EmitParams {
     uint32_t* msgs;
     uint64_t capacity;
     uint32_t n_blocks = 0;  // emit_map_kernel: 256-message blocks (grid stride when > gridDim.x)
+    // emit_map_kernel in the sharded tick: rows whose info.x carries kLocPool read the received
+    // cube-list pool at that word offset (wq_sharded.hip); nullptr everywhere else
+    const uint32_t* pool = nullptr;
 };
 
 // LDS of one emit row (256 messages): an image of a window of the row's output, aligned to
@@ -474,7 +477,10 @@ __global__ __launch_bounds__(kBlock) void emit_map_kernel(EmitParams p) {
     const uint32_t* base = p.t.list;
     uint32_t skip = kNone;
     if (e) {
-        if (inf.x & kLocSelf) {
+        if (p.pool && (inf.x & kLocPool) == kLocPool) {
+            base = p.pool + (inf.x & kLocMask);
+            skip = inf.y;
+        } else if (inf.x & kLocSelf) {
             base = p.sender + m;
         } else if (inf.x & kLocGlobal) {
             base = p.t.list + (inf.x & ~kLocGlobal) + 1;

@@ -30,6 +30,10 @@ struct GatherParams {
     const uint32_t* e = nullptr;            // row lengths
     const uint32_t* tile_prefix = nullptr;  // exclusive prefix of the 256-row totals
     uint32_t* offsets = nullptr;            // out: offsets[0 .. n)
+    // CSR = false, optional: block b's rows go to out[blk_base[b] + (start[i] - start[256 b])], and
+    // outputs at or beyond blk_lim[b] are not written (the sharded tick's budgeted pool segments)
+    const uint64_t* blk_base = nullptr;
+    const uint64_t* blk_lim = nullptr;
 };
 
 template <int R>
@@ -90,6 +94,11 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(GatherParams p) {
         st = i < p.n ? p.start[i] - g : T;
     }
     if (T == 0 || !p.out) return;  // block-uniform
+    uint64_t obase = g, olim = p.capacity;
+    if (!CSR && p.blk_base) {
+        obase = p.blk_base[blockIdx.x];
+        olim = p.blk_lim[blockIdx.x];
+    }
     sm.desc[tid] = make_uint4(st, d0.y, d0.z, d0.w);  // (rows of length 0 are never read)
     uint4* my_map = reinterpret_cast<uint4*>(sm.map) + tid * (R / 8);
     for (uint32_t w0 = 0; w0 < T; w0 += W) {
@@ -148,8 +157,8 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(GatherParams p) {
 #pragma unroll
         for (int u = 0; u < R; ++u) {
             const uint32_t r = w0 + u * kBlock + tid;
-            const uint64_t o = (uint64_t)g + r;
-            if (r < T && o < p.capacity) {
+            const uint64_t o = obase + r;
+            if (r < T && o < olim) {
                 p.out[o] = val[u];
                 if (p.out_row) p.out_row[o] = i0 + own[u];
             }

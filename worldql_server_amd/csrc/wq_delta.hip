@@ -1392,6 +1392,7 @@ int table_resolve(wq_router* h, bool blocking) {
         return WQ_OK;
     }
     h->n_delta_fallbacks++;
+    h->table_gen++;
     h->cur_ops = pd.ops;
     return table_rebuild_batch(h, pd.n);
 }

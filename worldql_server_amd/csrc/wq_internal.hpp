@@ -143,6 +143,9 @@ struct wq_router {
     uint64_t n_delta_applies = 0, n_delta_fallbacks = 0, n_delta_wave_batches = 0;
     uint64_t n_delta_batches = 0;  // batch tags of the record claims (wq_delta.hip)
     bool dstat_pending = false;
+    // bumped by every change of the table (an op batch, a removal, a re-applied device batch):
+    // results that point into the table (the slot tick's kept rows) are valid for one generation
+    uint64_t table_gen = 0;
 
     // build scratch
     wq::DevBuf ev_h, ev_w, ev_kx, ev_ky, ev_kz, ev_p, ev_kind, d_ops;
@@ -238,6 +241,7 @@ int multi_remove_peers(wq_router* h, const uint32_t* peers, size_t n);
 int multi_route_tick(wq_router* h, const double* pos, const int64_t* keys, const uint32_t* world,
                      const uint32_t* sender, const uint8_t* repl, size_t M, uint32_t* offsets, uint32_t* peers,
                      uint32_t* msgs, size_t capacity, size_t* n_pairs, bool on_device);
+int multi_route_slices(wq_router* h, const wq_msg_slice* in, int with_msgs, wq_slice_view* out);
 int multi_is_subscribed(wq_router* h, size_t n, const uint32_t* world, const uint32_t* peer, int raw,
                         const void* kp, uint8_t* out);
 int multi_stats(wq_router* h, wq_stats* out);

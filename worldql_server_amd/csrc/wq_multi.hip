@@ -2,22 +2,30 @@
 // devices, ...)), the reference's one-owner model kept at the boundary.
 //
 // The reference owns one WorldMap in one task (worldql_server/src/processing/thread.rs:119, driven
-// by the select! loop at :122-146). wq_router_create_multi gives that task one handle again: inside,
-// G shard handles (one per device, cube-hash owners, wq_sharded.hip) attached to an in-process hub,
-// and G worker threads — one per shard, since a sharded tick is collective — that the calling thread
-// hands each call to and waits for. What a call does on the multi handle:
-//   wq_apply_ops / _device, wq_remove_peers   every shard gets the whole op stream and keeps what it
-//                                             owns (+ every REMOVE_PEER): wq_sharded_apply_ops
-//   wq_route_tick / _device                   the messages split in G contiguous slices, one per
-//                                             shard, routed by the sharded tick (owners anywhere),
-//                                             the G CSRs concatenated into the caller's in message
-//                                             order: exactly the one-table result
-//   wq_is_subscribed                          every shard answers, OR (only the owner can hold it)
-//   wq_is_subscribed_any, wq_world_peers,     the shards' any-keys (world << 32 | peer) merged
-//   wq_route_global[_device], wq_get_stats    (sort + unique) into the handle's own any-keys on
-//                                             devices[0], then the single-GPU kernels on them
-//   radius filter / peer positions / hint     forwarded to every shard
-// Device-pointer calls take their arrays on devices[0] and are synchronous on return.
+// by the select! loop at :122-146). wq_router_create_multi[_mode] gives that task one handle again:
+// inside, G sub-handles (one per device) and G worker threads — one per sub-handle, since a sharded
+// tick is collective — that the calling thread hands each call to and waits for. Two layouts:
+//   WQ_MULTI_CUBE_HASH  every (world, cube) bucket lives on one shard (cube-hash owner, wq_sharded.hip);
+//                       the sub-handles share an in-process hub and a tick is the sharded tick
+//   WQ_MULTI_REPLICATE  every device holds the whole table (288 GB of HBM holds C3's ~10 GB many
+//                       times over) and routes its own slice of the messages with the single-GPU
+//                       tick: no exchange at all; every op is applied on every device
+// What a call does on the multi handle:
+//   wq_apply_ops, wq_remove_peers     cube hash: every shard gets the whole stream and keeps what it
+//                                     owns (+ every REMOVE_PEER); replicate: every replica applies all
+//   wq_apply_ops_device               cube hash: ops validated and partitioned by owner on devices[0]
+//                                     (one read-back of G counts), each shard's part applied on its
+//                                     device; replicate: the batch to every replica, asynchronous
+//   wq_route_tick / _device           the messages in G contiguous slices, one per sub-handle, the G
+//                                     CSRs concatenated into the caller's in message order: exactly
+//                                     the one-table result (all pairs cross to devices[0])
+//   wq_route_tick_slices_device       each device's own messages routed where they are, each CSR left
+//                                     on its device (views): the scaling form
+//   wq_is_subscribed[_any], wq_world_peers, wq_route_global[_device], wq_get_stats
+//                                     cube hash: shard answers combined (any-keys merged on
+//                                     devices[0]); replicate: replica 0 answers
+//   radius filter / peer positions / hint   forwarded to every sub-handle
+// Device-pointer calls take their arrays on devices[0] (the slice form: on each slice's device).
 #include <algorithm>
 #include <condition_variable>
 #include <cstring>
@@ -34,14 +42,19 @@ namespace wq {
 
 struct MultiCtx {
     uint32_t G = 0;
+    int mode = WQ_MULTI_CUBE_HASH;
     std::vector<int> dev;
     std::vector<wq_router*> sub;
     wq_hub* hub = nullptr;
-    // per shard, on its device: staged inputs and outputs of a tick
-    std::vector<DevBuf> in, out;
+    // per sub-handle, on its device: staged inputs and outputs of a tick, device op batches
+    // (two, alternating: a sub-handle may re-apply its previous batch at its next call)
+    std::vector<DevBuf> in, out, ops0, ops1;
     std::vector<uint64_t> cap, P;
+    std::vector<uint32_t> flip;
     bool any_dirty = true;  // the merged any-keys need rebuilding (an op was applied since)
-    DevBuf tmp, cnt;        // merge scratch (devices[0])
+    DevBuf tmp, cnt, part;  // devices[0] scratch: the any-key merge, the device op partition
+    hipEvent_t ready = nullptr;
+    uint32_t err_sticky = 0, ovf_sticky = 0;  // the handle's own health bits (wq_route_health)
     // worker pool: worker g runs task(g) on device dev[g]
     std::vector<std::thread> th;
     std::mutex mu;
@@ -78,7 +91,7 @@ void worker(MultiCtx* m, uint32_t g) {
     }
 }
 
-// f(g) on every shard's worker at once; the first failing shard's status and message.
+// f(g) on every sub-handle's worker at once; the first failing one's status and message.
 int run_all(wq_router* h, const std::function<int(uint32_t)>& f) {
     MultiCtx& m = *h->multi;
     {
@@ -92,7 +105,7 @@ int run_all(wq_router* h, const std::function<int(uint32_t)>& f) {
     }
     for (uint32_t g = 0; g < m.G; ++g)
         if (m.rc[g]) {
-            h->err = "shard " + std::to_string(g) + ": " + m.sub[g]->err;
+            h->err = "device " + std::to_string(g) + ": " + m.sub[g]->err;
             return m.rc[g];
         }
     (void)hipSetDevice(h->device);
@@ -111,54 +124,138 @@ int add_u32(wq_router* s, uint32_t* a, uint64_t n, uint32_t c) {
     return WQ_OK;
 }
 
+// A device op batch on devices[0] -> its owner shard per op (G = an invalid op: REMOVE_PEER or
+// the reserved world id, which the device-batch contract rejects) and the count per owner.
+__global__ void k_multi_op_owner(const wq_op* __restrict__ ops, uint32_t n, double sf, int64_t si, uint32_t G,
+                                 uint32_t* __restrict__ owner, uint32_t* __restrict__ counts) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const wq_op op = ops[i];
+    uint32_t o = G;
+    if (op.kind <= WQ_OP_UNSUBSCRIBE && op.world != WQ_WORLD_INVALID) {
+        int64_t x, y, z;
+        if (op.key_is_raw) {
+            x = op.u.key[0];
+            y = op.u.key[1];
+            z = op.u.key[2];
+        } else {
+            x = coord_clamp_dev(op.u.pos[0], sf, si);
+            y = coord_clamp_dev(op.u.pos[1], sf, si);
+            z = coord_clamp_dev(op.u.pos[2], sf, si);
+        }
+        o = shard_of(op.world, x, y, z, G);
+    }
+    owner[i] = o;
+    atomicAdd(counts + o, 1u);
+}
+
+__global__ void k_multi_iota(uint32_t* __restrict__ a, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = i;
+}
+
+__global__ void k_multi_gather_ops(const wq_op* __restrict__ ops, const uint32_t* __restrict__ order, uint32_t n,
+                                   wq_op* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = ops[order[i]];
+}
+
 // Slice g of M messages.
 void slice(uint64_t M, uint32_t G, uint32_t g, uint64_t* lo, uint64_t* hi) {
     *lo = M * g / G;
     *hi = M * (g + 1) / G;
 }
 
-// One shard's part of a tick: its slice's inputs staged at `din` (device g) — pos or keys, world,
-// sender, repl at the offsets below — routed by the sharded tick into the shard's output staging
-// (offsets, peers, msgs), grown and re-copied when the pairs outgrow it. m.P[g] = its pairs.
-int shard_tick(wq_router* h, uint32_t g, const char* din, uint64_t Mg, bool keys, bool msgs) {
-    MultiCtx& m = *h->multi;
-    wq_router* s = m.sub[g];
-    const size_t o_w = al(Mg * 24), o_s = al(o_w + Mg * 4), o_r = al(o_s + Mg * 4);
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        const uint64_t cap = m.cap[g];
-        const size_t op = al((Mg + 1) * 4), om = al(op + cap * 4);
-        WQ_ALLOC(s, m.out[g], om + (msgs ? cap * 4 : 0) + kAlign);
-        char* dout = m.out[g].as<char>();
-        size_t P = 0;
-        int rc = wq_sharded_route_tick_device(
-            s, keys ? nullptr : reinterpret_cast<const double*>(din), keys ? reinterpret_cast<const int64_t*>(din) : nullptr,
-            reinterpret_cast<const uint32_t*>(din + o_w), reinterpret_cast<const uint32_t*>(din + o_s),
-            reinterpret_cast<const uint8_t*>(din + o_r), Mg, reinterpret_cast<uint32_t*>(dout),
-            reinterpret_cast<uint32_t*>(dout + op), msgs ? reinterpret_cast<uint32_t*>(dout + om) : nullptr, cap, &P);
-        m.P[g] = P;
-        if (rc == WQ_E_CAPACITY && P > cap && P <= 0xFFFFFFFFull) {
-            // the shard's staging was short: grow it and copy the kept result out again (no re-exchange)
-            m.cap[g] = P + P / 4 + 1024;
-            const uint64_t c2 = m.cap[g];
-            const size_t op2 = al((Mg + 1) * 4), om2 = al(op2 + c2 * 4);
-            WQ_ALLOC(s, m.out[g], om2 + (msgs ? c2 * 4 : 0) + kAlign);
-            char* d2 = m.out[g].as<char>();
-            return wq_sharded_copy_out(s, reinterpret_cast<uint32_t*>(d2), reinterpret_cast<uint32_t*>(d2 + op2),
-                                       msgs ? reinterpret_cast<uint32_t*>(d2 + om2) : nullptr, c2);
-        }
-        return rc;
-    }
+// One sub-handle's messages (device pointers on its device).
+struct SliceIn {
+    const double* pos;
+    const int64_t* keys;
+    const uint32_t* world;
+    const uint32_t* sender;
+    const uint8_t* repl;
+    uint64_t M;
+};
+
+// Output staging of sub-handle g: offsets, peers, msgs at these offsets of m.out[g].
+void out_layout(uint64_t M, uint64_t cap, size_t* op, size_t* om) {
+    *op = al((M + 1) * 4);
+    *om = al(*op + cap * 4);
+}
+
+// The sub-handle's health words hold an overflow bit for every staging attempt that came up short
+// (the handle grows its staging and routes / copies again): not the caller's overflow. Cleared.
+int clear_staging_overflow(wq_router* s) {
+    if (!s->rws.buf.p) return WQ_OK;
+    WQ_HIP(s, hipMemsetAsync(route_health(s) + 1, 0, 4, s->stream));
     return WQ_OK;
 }
 
-// Per shard: the CSR slice, rebased (offsets + base, msgs + lo), into the caller's arrays —
+// One sub-handle's part of a tick: its messages routed into its output staging (offsets, peers,
+// msgs), grown when the pairs outgrow it. m.P[g] = its pairs. Cube hash: the sharded tick (every
+// sub-handle takes part: it is collective); replicate: the single-GPU tick on the replica.
+int tick_into(wq_router* h, uint32_t g, const SliceIn& x, bool msgs) {
+    MultiCtx& m = *h->multi;
+    wq_router* s = m.sub[g];
+    if (!m.cap[g]) m.cap[g] = 16 * x.M + 1024;
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        const uint64_t cap = m.cap[g];
+        size_t op, om;
+        out_layout(x.M, cap, &op, &om);
+        WQ_ALLOC(s, m.out[g], om + (msgs ? cap * 4 : 0) + kAlign);
+        char* dout = m.out[g].as<char>();
+        uint32_t* d_off = reinterpret_cast<uint32_t*>(dout);
+        uint32_t* d_peers = reinterpret_cast<uint32_t*>(dout + op);
+        uint32_t* d_msgs = msgs ? reinterpret_cast<uint32_t*>(dout + om) : nullptr;
+        if (m.mode == WQ_MULTI_CUBE_HASH) {
+            size_t P = 0;
+            int rc = wq_sharded_route_tick_device(s, x.pos, x.keys, x.world, x.sender, x.repl, x.M, d_off, d_peers,
+                                                  d_msgs, cap, &P);
+            m.P[g] = P;
+            if (rc == WQ_E_CAPACITY && P > cap && P <= 0xFFFFFFFFull) {
+                // the staging was short: grow it and copy the kept result out again (no re-exchange)
+                m.cap[g] = P + P / 4 + 1024;
+                const uint64_t c2 = m.cap[g];
+                size_t op2, om2;
+                out_layout(x.M, c2, &op2, &om2);
+                WQ_ALLOC(s, m.out[g], om2 + (msgs ? c2 * 4 : 0) + kAlign);
+                char* d2 = m.out[g].as<char>();
+                rc = wq_sharded_copy_out(s, reinterpret_cast<uint32_t*>(d2), reinterpret_cast<uint32_t*>(d2 + op2),
+                                         msgs ? reinterpret_cast<uint32_t*>(d2 + om2) : nullptr, c2);
+                if (rc == WQ_OK) rc = clear_staging_overflow(s);
+            }
+            return rc;
+        }
+        // replicate: the single-GPU tick, P read back
+        int rc = wq_route_tick_device(s, x.pos, x.keys, x.world, x.sender, x.repl, x.M, d_off, d_peers, d_msgs, cap,
+                                      nullptr);
+        if (rc) return rc;
+        wq_route_counters c{};
+        WQ_HIP(s, hipMemcpyAsync(&c, s->rws.last, sizeof(c), hipMemcpyDeviceToHost, s->stream));
+        WQ_HIP(s, hipStreamSynchronize(s->stream));
+        if (x.M == 0) c.n_pairs = 0;
+        if (c.error & 4u) return set_error(s, WQ_E_TIMEOUT, "route look-back spin gave up");
+        if (c.error & 8u) return set_error(s, WQ_E_INVALID, "a replica's table still misses a device batch");
+        if (c.error) return set_error(s, WQ_E_CAPACITY, "more than 2^32-1 pairs in one tick");
+        m.P[g] = c.n_pairs;
+        // the next tick's shape from this one's fan-out, as the host-array tick does (a replica's
+        // device ticks are read back here anyway)
+        if (s->fanout_auto && x.M >= 256) s->heavy_fanout = (double)c.n_pairs >= WQ_HEAVY_FANOUT * (double)x.M;
+        if (c.n_pairs <= cap) return WQ_OK;
+        if (c.n_pairs > 0xFFFFFFFFull) return set_error(s, WQ_E_CAPACITY, "more than 2^32-1 pairs in one tick");
+        m.cap[g] = c.n_pairs + c.n_pairs / 4 + 1024;  // short: grow the staging and route again
+        if (int r2 = clear_staging_overflow(s)) return r2;
+    }
+    return set_error(s, WQ_E_CAPACITY, "replica staging kept growing");
+}
+
+// Per sub-handle: the CSR slice, rebased (offsets + base, msgs + lo), into the caller's arrays —
 // host arrays (kind D2H) or devices[0] arrays (peer copies).
 int shard_copy_back(wq_router* h, uint32_t g, uint64_t lo, uint64_t Mg, uint64_t base, uint32_t* offsets,
                     uint32_t* peers, uint32_t* msgs, size_t capacity, bool to_host) {
     MultiCtx& m = *h->multi;
     wq_router* s = m.sub[g];
-    const uint64_t cap = m.cap[g];
-    const size_t op = al((Mg + 1) * 4), om = al(op + cap * 4);
+    size_t op, om;
+    out_layout(Mg, m.cap[g], &op, &om);
     char* dout = m.out[g].as<char>();
     uint32_t* d_off = reinterpret_cast<uint32_t*>(dout);
     uint32_t* d_msgs = reinterpret_cast<uint32_t*>(dout + om);
@@ -183,16 +280,53 @@ int shard_copy_back(wq_router* h, uint32_t g, uint64_t lo, uint64_t Mg, uint64_t
     return WQ_OK;
 }
 
+// A device op batch (on devices[0]) to sub-handle g: copied to its alternating staging buffer on
+// its own stream after the caller's stream has produced it, then applied (asynchronously).
+int apply_staged(wq_router* h, uint32_t g, const wq_op* src, size_t n) {
+    MultiCtx& m = *h->multi;
+    wq_router* s = m.sub[g];
+    if (!n) return WQ_OK;
+    DevBuf& st = (m.flip[g] ^= 1u) ? m.ops1[g] : m.ops0[g];
+    WQ_ALLOC(s, st, n * sizeof(wq_op));
+    WQ_HIP(s, hipStreamWaitEvent(s->stream, m.ready, 0));
+    if (m.dev[g] == h->device)
+        WQ_HIP(s, hipMemcpyAsync(st.p, src, n * sizeof(wq_op), hipMemcpyDeviceToDevice, s->stream));
+    else
+        WQ_HIP(s, hipMemcpyPeerAsync(st.p, m.dev[g], src, h->device, n * sizeof(wq_op), s->stream));
+    return wq_apply_ops_device(s, st.as<wq_op>(), n);
+}
+
 }  // namespace
 
-// The shards' any-keys, merged into the multi handle's own (devices[0]) when an op changed them.
+// The any-keys behind the handle's queries, in its own (devices[0]) table when an op changed them:
+// the shards' merged (cube hash), or replica 0's (replicate).
 int multi_merge_any(wq_router* h) {
     MultiCtx& m = *h->multi;
     if (!m.any_dirty) return WQ_OK;
+    hipStream_t st = h->stream;
+    if (m.mode == WQ_MULTI_REPLICATE) {
+        wq_router* s = m.sub[0];
+        (void)hipSetDevice(s->device);
+        if (int rc = table_ensure_any(s)) return rc;
+        WQ_HIP(s, hipStreamSynchronize(s->stream));
+        (void)hipSetDevice(h->device);
+        const uint64_t n = s->tab.n_any;
+        WQ_ALLOC(h, h->tab.any, (n ? n : 1) * 8);
+        if (n) {
+            if (m.dev[0] == h->device)
+                WQ_HIP(h, hipMemcpyAsync(h->tab.any.p, s->tab.any.p, n * 8, hipMemcpyDeviceToDevice, st));
+            else
+                WQ_HIP(h, hipMemcpyPeerAsync(h->tab.any.p, h->device, s->tab.any.p, m.dev[0], n * 8, st));
+            WQ_HIP(h, hipStreamSynchronize(st));
+        }
+        h->tab.n_any = n;
+        h->any_stale = false;
+        m.any_dirty = false;
+        return WQ_OK;
+    }
     if (int rc = run_all(h, [&](uint32_t g) { return table_ensure_any(m.sub[g]); })) return rc;
     uint64_t total = 0;
     for (wq_router* s : m.sub) total += s->tab.n_any;
-    hipStream_t st = h->stream;
     WQ_ALLOC(h, h->tab.any, (total ? total : 1) * 8);
     WQ_ALLOC(h, h->key64_a, (total ? total : 1) * 8);
     uint64_t at = 0;
@@ -219,7 +353,7 @@ int multi_merge_any(wq_router* h) {
         WQ_HIP(h, rocprim::unique(nullptr, b2, sorted, h->key64_b.as<uint64_t>(), (uint64_t*)nullptr, (size_t)total,
                                   rocprim::equal_to<uint64_t>(), st));
         WQ_ALLOC(h, m.tmp, std::max(b1, b2));
-        WQ_ALLOC(m.sub[0], m.cnt, 64);
+        WQ_ALLOC(h, m.cnt, 64);
         WQ_HIP(h, rocprim::radix_sort_keys(m.tmp.p, b1, keys, sorted, (size_t)total, 0, 64, st));
         WQ_HIP(h, rocprim::unique(m.tmp.p, b2, sorted, h->key64_b.as<uint64_t>(), m.cnt.as<uint64_t>(), (size_t)total,
                                   rocprim::equal_to<uint64_t>(), st));
@@ -235,20 +369,67 @@ int multi_merge_any(wq_router* h) {
 }
 
 int multi_apply_ops(wq_router* h, const wq_op* ops, size_t n) {
-    h->multi->any_dirty = true;
-    return run_all(h, [&](uint32_t g) { return wq_sharded_apply_ops(h->multi->sub[g], ops, n); });
+    MultiCtx& m = *h->multi;
+    m.any_dirty = true;
+    if (m.mode == WQ_MULTI_REPLICATE) return run_all(h, [&](uint32_t g) { return wq_apply_ops(m.sub[g], ops, n); });
+    return run_all(h, [&](uint32_t g) { return wq_sharded_apply_ops(m.sub[g], ops, n); });
 }
 
+// The device-batch contract of the single-GPU handle on G devices: an invalid op (REMOVE_PEER, the
+// reserved world id) rejects the whole batch, reported as error bit 16 of wq_route_health and in
+// wq_last_error while the call itself returns WQ_OK. Replicate: every replica takes the batch
+// asynchronously (each rejects an invalid one itself). Cube hash: the ops are validated and
+// partitioned by owner on devices[0] — one read-back of G + 1 counts, not of the batch — and each
+// shard's part is applied on its own device.
 int multi_apply_ops_device(wq_router* h, const wq_op* d_ops, size_t n) {
-    std::vector<wq_op> ops(n);
-    if (n) {
-        WQ_HIP(h, hipStreamSynchronize(h->stream));
-        WQ_HIP(h, hipMemcpy(ops.data(), d_ops, n * sizeof(wq_op), hipMemcpyDeviceToHost));
+    MultiCtx& m = *h->multi;
+    const uint32_t G = m.G;
+    if (n == 0) return WQ_OK;
+    if (n >= 0xFFFFFFFFull) return set_error(h, WQ_E_INVALID, "device op batch larger than 2^32 - 1 ops");
+    m.any_dirty = true;
+    hipStream_t st = h->stream;
+    if (m.mode == WQ_MULTI_REPLICATE) {
+        WQ_HIP(h, hipEventRecord(m.ready, st));
+        return run_all(h, [&](uint32_t g) { return apply_staged(h, g, d_ops, n); });
     }
-    for (const wq_op& o : ops)  // the device-batch contract: subscribe / unsubscribe only
-        if (o.kind > WQ_OP_UNSUBSCRIBE || o.world == WQ_WORLD_INVALID)
-            return set_error(h, WQ_E_INVALID, "device op batch: REMOVE_PEER or the reserved world id");
-    return multi_apply_ops(h, ops.data(), n);
+    WQ_ALLOC(h, h->key32_a, n * 4);
+    WQ_ALLOC(h, h->key32_b, n * 4);
+    WQ_ALLOC(h, h->idx_a, n * 4);
+    WQ_ALLOC(h, h->idx_b, n * 4);
+    WQ_ALLOC(h, m.part, n * sizeof(wq_op));
+    WQ_ALLOC(h, m.cnt, 4 * (WQ_MAX_SHARDS + 1));
+    uint32_t* owner = h->key32_a.as<uint32_t>();
+    uint32_t* cnt = m.cnt.as<uint32_t>();
+    WQ_HIP(h, hipMemsetAsync(cnt, 0, 4 * (G + 1), st));
+    const unsigned gr = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(k_multi_op_owner, dim3(gr), dim3(256), 0, st, d_ops, (uint32_t)n, (double)h->cube_size,
+                       (int64_t)h->cube_size, G, owner, cnt);
+    hipLaunchKernelGGL(k_multi_iota, dim3(gr), dim3(256), 0, st, h->idx_a.as<uint32_t>(), (uint32_t)n);
+    WQ_HIP(h, hipGetLastError());
+    std::vector<uint32_t> c(G + 1);
+    WQ_HIP(h, hipMemcpyAsync(c.data(), cnt, 4 * (G + 1), hipMemcpyDeviceToHost, st));
+    WQ_HIP(h, hipStreamSynchronize(st));
+    if (c[G]) {  // rejected whole, as a single-GPU handle rejects it
+        m.err_sticky |= kErrBadBatch;
+        h->err = "bad op (kind or reserved world id) in a device batch: that batch was not applied";
+        return WQ_OK;
+    }
+    // stable partition by owner: a radix sort of (owner, op index) over the owner's bits
+    int bits = 1;
+    while ((1u << bits) <= G) ++bits;
+    size_t tb = 0;
+    WQ_HIP(h, rocprim::radix_sort_pairs(nullptr, tb, owner, h->key32_b.as<uint32_t>(), h->idx_a.as<uint32_t>(),
+                                        h->idx_b.as<uint32_t>(), n, 0, bits, st));
+    WQ_ALLOC(h, m.tmp, tb);
+    WQ_HIP(h, rocprim::radix_sort_pairs(m.tmp.p, tb, owner, h->key32_b.as<uint32_t>(), h->idx_a.as<uint32_t>(),
+                                        h->idx_b.as<uint32_t>(), n, 0, bits, st));
+    hipLaunchKernelGGL(k_multi_gather_ops, dim3(gr), dim3(256), 0, st, d_ops, h->idx_b.as<uint32_t>(), (uint32_t)n,
+                       m.part.as<wq_op>());
+    WQ_HIP(h, hipGetLastError());
+    WQ_HIP(h, hipEventRecord(m.ready, st));
+    std::vector<size_t> off(G + 1, 0);
+    for (uint32_t g = 0; g < G; ++g) off[g + 1] = off[g] + c[g];
+    return run_all(h, [&](uint32_t g) { return apply_staged(h, g, m.part.as<wq_op>() + off[g], c[g]); });
 }
 
 int multi_remove_peers(wq_router* h, const uint32_t* peers, size_t n) {
@@ -262,22 +443,17 @@ int multi_route_tick(wq_router* h, const double* pos, const int64_t* keys, const
     MultiCtx& m = *h->multi;
     const uint32_t G = m.G;
     const bool use_keys = keys != nullptr;
-    hipEvent_t ready = nullptr;
-    if (on_device) {  // the caller's arrays (devices[0]) are complete once its stream gets here
-        WQ_HIP(h, hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-        WQ_HIP(h, hipEventRecord(ready, h->stream));
-    }
+    if (on_device) WQ_HIP(h, hipEventRecord(m.ready, h->stream));  // the caller's arrays are complete here
     int rc = run_all(h, [&](uint32_t g) -> int {
         wq_router* s = m.sub[g];
         uint64_t lo, hi;
         slice(M, G, g, &lo, &hi);
         const uint64_t Mg = hi - lo;
-        if (!m.cap[g]) m.cap[g] = 16 * Mg + 1024;
         const size_t o_w = al(Mg * 24), o_s = al(o_w + Mg * 4), o_r = al(o_s + Mg * 4), n_in = al(o_r + Mg + 1);
         WQ_ALLOC(s, m.in[g], n_in);
         char* din = m.in[g].as<char>();
         const void* src_k = use_keys ? (const void*)(keys + 3 * lo) : (const void*)(pos ? pos + 3 * lo : nullptr);
-        if (on_device) WQ_HIP(s, hipStreamWaitEvent(s->stream, ready, 0));
+        if (on_device) WQ_HIP(s, hipStreamWaitEvent(s->stream, m.ready, 0));
         auto put = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
             if (!bytes) return hipSuccess;
             if (!on_device) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s->stream);
@@ -288,9 +464,12 @@ int multi_route_tick(wq_router* h, const double* pos, const int64_t* keys, const
         WQ_HIP(s, put(din + o_w, world + lo, Mg * 4));
         WQ_HIP(s, put(din + o_s, sender + lo, Mg * 4));
         WQ_HIP(s, put(din + o_r, repl + lo, Mg));
-        return shard_tick(h, g, din, Mg, use_keys, msgs != nullptr);
+        SliceIn x{use_keys ? nullptr : reinterpret_cast<const double*>(din),
+                  use_keys ? reinterpret_cast<const int64_t*>(din) : nullptr,
+                  reinterpret_cast<const uint32_t*>(din + o_w), reinterpret_cast<const uint32_t*>(din + o_s),
+                  reinterpret_cast<const uint8_t*>(din + o_r), Mg};
+        return tick_into(h, g, x, msgs != nullptr);
     });
-    if (ready) (void)hipEventDestroy(ready);
     if (rc) return rc;
     std::vector<uint64_t> base(G + 1, 0);
     for (uint32_t g = 0; g < G; ++g) base[g + 1] = base[g] + m.P[g];
@@ -310,13 +489,47 @@ int multi_route_tick(wq_router* h, const double* pos, const int64_t* keys, const
     } else {
         offsets[M] = last;
     }
-    if (P > capacity) return set_error(h, WQ_E_CAPACITY, "output capacity too small (required size in *n_pairs)");
+    if (P > capacity) {
+        m.ovf_sticky = 1;  // as a single-GPU tick's sticky overflow word
+        return set_error(h, WQ_E_CAPACITY, "output capacity too small (required size in *n_pairs)");
+    }
+    return WQ_OK;
+}
+
+int multi_route_slices(wq_router* h, const wq_msg_slice* in, int with_msgs, wq_slice_view* out) {
+    MultiCtx& m = *h->multi;
+    for (uint32_t g = 0; g < m.G; ++g) {
+        const wq_msg_slice& x = in[g];
+        if (x.n_msgs >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per slice");
+        if (x.n_msgs && (!x.d_world || !x.d_sender || !x.d_repl || (!x.d_pos && !x.d_keys)))
+            return set_error(h, WQ_E_INVALID, "a slice with messages but without its arrays");
+    }
+    int rc = run_all(h, [&](uint32_t g) -> int {
+        const wq_msg_slice& x = in[g];
+        SliceIn si{x.d_keys ? nullptr : x.d_pos, x.d_keys, x.d_world, x.d_sender, x.d_repl, x.n_msgs};
+        return tick_into(h, g, si, with_msgs != 0);
+    });
+    if (rc) return rc;
+    for (uint32_t g = 0; g < m.G; ++g) {
+        size_t op, om;
+        out_layout(in[g].n_msgs, m.cap[g], &op, &om);
+        const char* d = m.out[g].as<char>();
+        wq_slice_view& v = out[g];
+        v.device = m.dev[g];
+        v.pad_ = 0;
+        v.n_msgs = in[g].n_msgs;
+        v.n_pairs = m.P[g];
+        v.offsets = reinterpret_cast<const uint32_t*>(d);
+        v.peers = reinterpret_cast<const uint32_t*>(d + op);
+        v.msgs = with_msgs ? reinterpret_cast<const uint32_t*>(d + om) : nullptr;
+    }
     return WQ_OK;
 }
 
 int multi_is_subscribed(wq_router* h, size_t n, const uint32_t* world, const uint32_t* peer, int raw,
                         const void* kp, uint8_t* out) {
     MultiCtx& m = *h->multi;
+    if (m.mode == WQ_MULTI_REPLICATE) return wq_is_subscribed(m.sub[0], n, world, peer, raw, kp, out);
     std::vector<std::vector<uint8_t>> part(m.G, std::vector<uint8_t>(n));
     if (int rc = run_all(h, [&](uint32_t g) { return wq_is_subscribed(m.sub[g], n, world, peer, raw, kp, part[g].data()); }))
         return rc;
@@ -332,7 +545,7 @@ int multi_set_positions(wq_router* h, const double* pos, size_t n, bool on_devic
     MultiCtx& m = *h->multi;
     if (!on_device)
         return run_all(h, [&](uint32_t g) { return wq_set_peer_positions(m.sub[g], pos, n); });
-    // device positions live on devices[0]: every shard takes its own copy (peer reads)
+    // device positions live on devices[0]: every sub-handle takes its own copy (peer reads)
     WQ_HIP(h, hipStreamSynchronize(h->stream));
     return run_all(h, [&](uint32_t g) -> int {
         wq_router* s = m.sub[g];
@@ -357,11 +570,15 @@ int multi_stats(wq_router* h, wq_stats* out) {
     if (int rc = run_all(h, [&](uint32_t g) { return wq_get_stats(m.sub[g], &st[g]); })) return rc;
     if (int rc = multi_merge_any(h)) return rc;
     memset(out, 0, sizeof(*out));
-    for (const wq_stats& s : st) {
-        out->n_entries += s.n_entries;
-        out->n_cubes += s.n_cubes;
-        out->table_slots += s.table_slots;
-        out->hash_fallbacks += s.hash_fallbacks;
+    if (m.mode == WQ_MULTI_REPLICATE) {
+        *out = st[0];
+    } else {
+        for (const wq_stats& s : st) {
+            out->n_entries += s.n_entries;
+            out->n_cubes += s.n_cubes;
+            out->table_slots += s.table_slots;
+            out->hash_fallbacks += s.hash_fallbacks;
+        }
     }
     out->n_any = h->tab.n_any;
     out->cube_size = h->cube_size;
@@ -377,6 +594,9 @@ int multi_health(wq_router* h, uint32_t* error_bits, uint32_t* overflow) {
         *error_bits |= e[g];
         *overflow |= o[g];
     }
+    *error_bits |= m.err_sticky;
+    *overflow |= m.ovf_sticky;
+    m.err_sticky = m.ovf_sticky = 0;
     return WQ_OK;
 }
 
@@ -392,13 +612,18 @@ void multi_release(wq_router* h) {
         if (t.joinable()) t.join();
     for (uint32_t g = 0; g < m->sub.size(); ++g) {
         (void)hipSetDevice(m->dev[g]);
+        if (m->sub[g]) (void)hipStreamSynchronize(m->sub[g]->stream);
         m->in[g].release();
         m->out[g].release();
+        m->ops0[g].release();
+        m->ops1[g].release();
         if (m->sub[g]) wq_router_destroy(m->sub[g]);
     }
     (void)hipSetDevice(h->device);
     m->tmp.release();
     m->cnt.release();
+    m->part.release();
+    if (m->ready) (void)hipEventDestroy(m->ready);
     if (m->hub) wq_hub_destroy(m->hub);
     delete m;
     h->multi = nullptr;
@@ -408,8 +633,11 @@ void multi_release(wq_router* h) {
 
 using namespace wq;
 
-extern "C" int wq_router_create_multi(uint16_t cube_size, int n_gpus, const int* devices, wq_router** out) {
-    if (!out || cube_size == 0 || n_gpus < 1 || n_gpus > WQ_MAX_SHARDS || !devices) return WQ_E_INVALID;
+extern "C" int wq_router_create_multi_mode(uint16_t cube_size, int n_gpus, const int* devices, int mode,
+                                           wq_router** out) {
+    if (!out || cube_size == 0 || n_gpus < 1 || n_gpus > WQ_MAX_SHARDS || !devices ||
+        (mode != WQ_MULTI_CUBE_HASH && mode != WQ_MULTI_REPLICATE))
+        return WQ_E_INVALID;
     *out = nullptr;
     wq_router* h = nullptr;
     int rc = wq_router_create(cube_size, devices[0], &h);  // the handle itself: devices[0], the merged any-keys
@@ -422,18 +650,23 @@ extern "C" int wq_router_create_multi(uint16_t cube_size, int n_gpus, const int*
     h->multi = m;
     const uint32_t G = (uint32_t)n_gpus;
     m->G = G;
+    m->mode = mode;
     m->dev.assign(devices, devices + G);
     m->sub.assign(G, nullptr);
     m->in.resize(G);
     m->out.resize(G);
+    m->ops0.resize(G);
+    m->ops1.resize(G);
     m->cap.assign(G, 0);
     m->P.assign(G, 0);
+    m->flip.assign(G, 0);
     m->rc.assign(G, 0);
-    rc = wq_hub_create(G, &m->hub);
+    if (hipEventCreateWithFlags(&m->ready, hipEventDisableTiming) != hipSuccess) rc = WQ_E_HIP;
+    if (rc == WQ_OK && mode == WQ_MULTI_CUBE_HASH) rc = wq_hub_create(G, &m->hub);
     for (uint32_t g = 0; g < G && rc == WQ_OK; ++g) {
         rc = wq_router_create(cube_size, devices[g], &m->sub[g]);
-        if (rc == WQ_OK) rc = wq_shard_attach_hub(m->sub[g], m->hub, g);
-        if (rc) h->err = std::string("shard ") + std::to_string(g) + ": " + wq_last_error(m->sub[g]);
+        if (rc == WQ_OK && mode == WQ_MULTI_CUBE_HASH) rc = wq_shard_attach_hub(m->sub[g], m->hub, g);
+        if (rc) h->err = std::string("device ") + std::to_string(g) + ": " + wq_last_error(m->sub[g]);
     }
     if (rc == WQ_OK) {
         try {
@@ -451,8 +684,25 @@ extern "C" int wq_router_create_multi(uint16_t cube_size, int n_gpus, const int*
     return WQ_OK;
 }
 
+extern "C" int wq_router_create_multi(uint16_t cube_size, int n_gpus, const int* devices, wq_router** out) {
+    return wq_router_create_multi_mode(cube_size, n_gpus, devices, WQ_MULTI_CUBE_HASH, out);
+}
+
 extern "C" int wq_multi_info(wq_router* h, uint32_t* n_gpus) {
     if (!h || !n_gpus) return WQ_E_INVALID;
     *n_gpus = h->multi ? h->multi->G : 1;
     return WQ_OK;
+}
+
+extern "C" int wq_multi_mode(wq_router* h, int* mode) {
+    if (!h || !mode) return WQ_E_INVALID;
+    *mode = h->multi ? h->multi->mode : -1;
+    return WQ_OK;
+}
+
+extern "C" int wq_route_tick_slices_device(wq_router* h, const wq_msg_slice* in, int with_msgs, wq_slice_view* out) {
+    if (!h || !in || !out) return WQ_E_INVALID;
+    if (!h->multi) return set_error(h, WQ_E_INVALID, "wq_route_tick_slices_device needs a multi-GPU handle");
+    WQ_HIP(h, hipSetDevice(h->device));
+    return multi_route_slices(h, in, with_msgs, out);
 }

@@ -356,8 +356,9 @@ int wq_route_health(wq_router* h, uint32_t* error_bits, uint32_t* overflow) {
     WQ_HIP(h, hipMemcpyAsync(w, h->rws.buf.p, 8, hipMemcpyDeviceToHost, h->stream));
     WQ_HIP(h, hipMemsetAsync(h->rws.buf.p, 0, 8, h->stream));
     WQ_HIP(h, hipStreamSynchronize(h->stream));
-    *error_bits = w[0];
-    *overflow = w[1];
+    // OR, not assign: a multi handle's shard bits are already in (and cleared on the shards)
+    *error_bits |= w[0];
+    *overflow |= w[1];
     return WQ_OK;
 }
 

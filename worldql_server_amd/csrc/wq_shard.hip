@@ -33,6 +33,7 @@ struct ShardIn {
     double sf;
     int64_t si;
     bool pos_rec;  // records carry the positions (radius filter on)
+    uint32_t me = kNone;  // budgeted slots (slot_*_kernel): this shard's own messages take no slot
 };
 
 template <bool RAW>
@@ -296,6 +297,195 @@ __global__ void __launch_bounds__(kBlock)
     }
 }
 
+// ---- budgeted slots (the sharded tick of wq_sharded.hip) ----------------------------------------
+// Only messages owned by ANOTHER shard become slots: the ingesting shard counts the messages of its
+// own cubes in place (count_kernel<..., OWN>). Owner d's slots go to the segment
+// [L.base[d], L.base[d] + L.budget[d]) of the send buffer — sizes fixed on the host before the tick
+// (the previous tick's counts with headroom, or this tick's exact counts), so the exchanges can be
+// enqueued without reading anything back. The true count per owner and a budget-overflow bit go to
+// the small exchange vector (a[2d], a[2d + 1]); slots past a budget are not written.
+// (SlotLayout, kStBudget: route_common.hpp)
+
+// (b1) per-block owner histogram as shard_count_kernel, own messages weighing 0.
+template <bool RAW>
+__global__ void __launch_bounds__(kBlock) slot_count_kernel(ShardIn in, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t cnt[WQ_MAX_SHARDS];
+    for (uint32_t d = threadIdx.x; d < in.G; d += kBlock) cnt[d] = 0;
+    __syncthreads();
+    const uint32_t m0 = blockIdx.x * kShardTile + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint32_t m = m0 + i * kBlock;
+        bool valid = m < in.M;
+        uint32_t own = 0xFFFFFFFFu, wt = 0;
+        if (valid) {
+            int64_t x, y, z;
+            msg_key<RAW>(in, m, x, y, z);
+            const uint32_t w = in.world[m];
+            own = shard_of(w, x, y, z, in.G);
+            wt = msg_weight<RAW, true>(in, w, x, y, z);
+            valid = own != in.me;
+        }
+        const uint64_t wide = __ballot(valid && wt == 2);
+        uint64_t todo = __ballot(valid);
+        while (todo) {
+            const int leader = __ffsll((unsigned long long)todo) - 1;
+            const uint32_t d = __shfl(own, leader, 64);
+            const uint64_t mask = __ballot(valid && own == d);
+            if (lane == leader) atomicAdd(&cnt[d], (uint32_t)(__popcll(mask) + __popcll(mask & wide)));
+            todo &= ~mask;
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < in.G; d += kBlock) counts[(uint64_t)d * in.nblk + blockIdx.x] = cnt[d];
+}
+
+// (b2) one block: per owner, the exclusive scan of its column of block counts (in place); the
+// owner's total and the budget bit to a[2d], a[2d + 1].
+__global__ void __launch_bounds__(kScanThreads1)
+    slot_scan_kernel(uint32_t* __restrict__ v, uint32_t nblk, uint32_t G, SlotLayout L, uint32_t* __restrict__ a) {
+    __shared__ uint32_t wsum[kScanThreads1 / 64];
+    __shared__ uint32_t carry_s;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t d = 0; d < G; ++d) {
+        uint32_t* col = v + (uint64_t)d * nblk;
+        if (threadIdx.x == 0) carry_s = 0;
+        __syncthreads();
+        for (uint32_t base = 0; base < nblk; base += kScanThreads1) {
+            const uint32_t i = base + threadIdx.x;
+            const uint32_t x = i < nblk ? col[i] : 0;
+            const uint32_t inc = wave_incl_scan_add(x, lane);
+            if (lane == 63) wsum[wave] = inc;
+            __syncthreads();
+            if (wave == 0) {
+                const uint32_t s = lane < kScanThreads1 / 64 ? wsum[lane] : 0;
+                const uint32_t si = wave_incl_scan_add(s, lane);
+                if (lane < kScanThreads1 / 64) wsum[lane] = si - s;
+            }
+            __syncthreads();
+            const uint32_t carry = carry_s;
+            if (i < nblk) col[i] = carry + wsum[wave] + inc - x;
+            __syncthreads();
+            if (threadIdx.x == kScanThreads1 - 1) carry_s = carry + wsum[wave] + inc;
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            a[2 * d] = carry_s;
+            a[2 * d + 1] = carry_s > L.budget[d] ? kStBudget : 0u;
+        }
+        __syncthreads();
+    }
+}
+
+// (b3) the stable ballot-ranked scatter of shard_scatter20_kernel into the budgeted segments; a
+// message that does not fit its owner's budget whole is not written (nor is any after it).
+template <bool RAW>
+__global__ void __launch_bounds__(kBlock)
+    slot_scatter_kernel(ShardIn in, const uint32_t* __restrict__ colbase, SlotLayout L, uint32_t* __restrict__ out,
+                        uint32_t* __restrict__ perm) {
+    __shared__ uint32_t wc[kShardIPT * kWaves][WQ_MAX_SHARDS];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t k = threadIdx.x; k < kShardIPT * kWaves * WQ_MAX_SHARDS; k += kBlock) (&wc[0][0])[k] = 0;
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1;
+    const uint32_t m0 = blockIdx.x * kShardTile + threadIdx.x;
+    int64_t kx[kShardIPT], ky[kShardIPT], kz[kShardIPT];
+    uint64_t pk[kShardIPT];
+    uint32_t ext[kShardIPT], own[kShardIPT], rank[kShardIPT];
+    bool reg[kShardIPT], go[kShardIPT];
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint32_t m = m0 + i * kBlock;
+        go[i] = m < in.M;
+        own[i] = 0xFFFFFFFFu;
+        rank[i] = 0;
+        reg[i] = true;
+        if (go[i]) {
+            msg_key<RAW>(in, m, kx[i], ky[i], kz[i]);
+            const uint32_t w = in.world[m];
+            own[i] = shard_of(w, kx[i], ky[i], kz[i], in.G);
+            reg[i] = pack_key(w, kx[i], ky[i], kz[i], in.sf, &pk[i], &ext[i]);
+            go[i] = own[i] != in.me;
+        }
+        const uint64_t wide = __ballot(go[i] && !reg[i]);
+        uint64_t todo = __ballot(go[i]);
+        while (todo) {
+            const int leader = __ffsll((unsigned long long)todo) - 1;
+            const uint32_t d = __shfl(own[i], leader, 64);
+            const uint64_t mask = __ballot(go[i] && own[i] == d);
+            if (go[i] && own[i] == d) rank[i] = __popcll(mask & lt) + __popcll(mask & wide & lt);
+            if (lane == leader) wc[i * kWaves + wave][d] = __popcll(mask) + __popcll(mask & wide);
+            todo &= ~mask;
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < in.G; d += kBlock) {
+        uint32_t run = colbase[(uint64_t)d * in.nblk + blockIdx.x];
+#pragma unroll
+        for (int k = 0; k < kShardIPT * kWaves; ++k) {
+            const uint32_t t = wc[k][d];
+            wc[k][d] = run;
+            run += t;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint32_t m = m0 + i * kBlock;
+        if (!go[i]) continue;
+        const uint32_t d = own[i];
+        const uint32_t j = wc[i * kWaves + wave][d] + rank[i];  // within the owner's segment
+        if (j + (reg[i] ? 1u : 2u) > L.budget[d]) continue;    // over budget: the tick is redone exactly
+        const uint32_t slot = L.base[d] + j;
+        uint32_t* o = out + (uint64_t)kSlotWords * slot;
+        const uint32_t rp = in.repl[m];
+        if (reg[i]) {
+            o[0] = (uint32_t)pk[i];
+            o[1] = (uint32_t)(pk[i] >> 32);
+            o[2] = ext[i];
+            o[3] = in.sender[m];
+            o[4] = rp | (kSlotReg << 8);
+            perm[slot] = m;
+        } else {
+            o[0] = (uint32_t)(uint64_t)kx[i];
+            o[1] = (uint32_t)((uint64_t)kx[i] >> 32);
+            o[2] = in.world[m];
+            o[3] = in.sender[m];
+            o[4] = rp | (kSlotHead << 8);
+            o[5] = (uint32_t)(uint64_t)ky[i];
+            o[6] = (uint32_t)((uint64_t)ky[i] >> 32);
+            o[7] = (uint32_t)(uint64_t)kz[i];
+            o[8] = (uint32_t)((uint64_t)kz[i] >> 32);
+            o[9] = kSlotTail << 8;
+            perm[slot] = m;
+            perm[slot + 1] = kNone;
+        }
+    }
+}
+
+// (b4) the unused rest of every segment becomes tail slots (route to nobody; perm kNone), so the
+// owner can count its whole receive budget without knowing the true counts. Over budget, the last
+// slot of the segment is overwritten as well (a head whose tail did not fit); that tick is redone.
+__global__ void __launch_bounds__(kBlock)
+    slot_pad_kernel(SlotLayout L, uint32_t G, const uint32_t* __restrict__ a, uint32_t* __restrict__ out,
+                    uint32_t* __restrict__ perm) {
+    const uint32_t d = blockIdx.y;
+    if (d >= G) return;
+    const uint32_t B = L.budget[d], n = a[2 * d];
+    const uint32_t from = n < B ? n : (B ? B - 1 : 0);
+    for (uint32_t j = from + blockIdx.x * kBlock + threadIdx.x; j < B; j += gridDim.x * kBlock) {
+        const uint32_t slot = L.base[d] + j;
+        uint32_t* o = out + (uint64_t)kSlotWords * slot;
+        o[0] = 0;
+        o[1] = 0;
+        o[2] = 0;
+        o[3] = 0;
+        o[4] = kSlotTail << 8;
+        perm[slot] = kNone;
+    }
+}
+
 __global__ void op_owner_kernel(const wq_op* __restrict__ ops, uint32_t n, double sf, int64_t si, uint32_t G,
                                 uint32_t* __restrict__ owner) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -415,6 +605,61 @@ int launch_shard_slots(wq_router* h, const double* d_pos, const int64_t* d_keys,
         hipLaunchKernelGGL((shard_scatter20_kernel<false>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist, d_slots,
                            d_perm);
     WQ_HIP(h, hipGetLastError());
+    return WQ_OK;
+}
+
+// Budgeted slots of this shard's messages owned by other shards (the slot_* kernels above): the
+// slots in L's segments of d_slots, perm[slot] = message (kNone for tails and padding), the true
+// count and budget bit per owner at d_a[2d], d_a[2d + 1] (zeroed for this shard itself).
+// phases: 1 = the counts only (histogram + scan), 2 = the scatter and padding after them, 3 = both.
+int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                        const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, uint32_t me,
+                        const SlotLayout& L, uint32_t* d_slots, uint32_t* d_perm, uint32_t* d_a, int phases) {
+    hipStream_t s = h->stream;
+    ShardIn in;
+    in.pos = d_pos;
+    in.keys = d_keys;
+    in.world = d_world;
+    in.sender = d_sender;
+    in.repl = d_repl;
+    in.M = (uint32_t)M;
+    in.G = G;
+    in.nblk = (uint32_t)((M + kShardTile - 1) / kShardTile);
+    in.sf = (double)h->cube_size;
+    in.si = (int64_t)h->cube_size;
+    in.pos_rec = false;
+    in.me = me;
+    if (M && (phases & 1)) {
+        WQ_ALLOC(h, h->shard_hist, (uint64_t)in.nblk * G * 4);
+        uint32_t* hist = h->shard_hist.as<uint32_t>();
+        if (d_keys)
+            hipLaunchKernelGGL((slot_count_kernel<true>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist);
+        else
+            hipLaunchKernelGGL((slot_count_kernel<false>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist);
+        WQ_HIP(h, hipGetLastError());
+        hipLaunchKernelGGL(slot_scan_kernel, dim3(1), dim3(kScanThreads1), 0, s, hist, in.nblk, G, L, d_a);
+        WQ_HIP(h, hipGetLastError());
+    } else if (phases & 1) {
+        WQ_HIP(h, hipMemsetAsync(d_a, 0, 8 * G, s));
+    }
+    if (!(phases & 2)) return WQ_OK;
+    if (M) {
+        uint32_t* hist = h->shard_hist.as<uint32_t>();
+        if (d_keys)
+            hipLaunchKernelGGL((slot_scatter_kernel<true>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist, L, d_slots,
+                               d_perm);
+        else
+            hipLaunchKernelGGL((slot_scatter_kernel<false>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist, L, d_slots,
+                               d_perm);
+        WQ_HIP(h, hipGetLastError());
+    }
+    uint32_t bmax = 0;
+    for (uint32_t d = 0; d < G; ++d) bmax = std::max(bmax, L.budget[d]);
+    if (bmax) {
+        const unsigned gx = std::min<unsigned>(64u, (bmax + kBlock - 1) / kBlock);
+        hipLaunchKernelGGL(slot_pad_kernel, dim3(gx, G), dim3(kBlock), 0, s, L, G, d_a, d_slots, d_perm);
+        WQ_HIP(h, hipGetLastError());
+    }
     return WQ_OK;
 }
 

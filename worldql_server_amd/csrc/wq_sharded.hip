@@ -37,6 +37,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include "route_count.hpp"
+#include "route_emit.hpp"
 #include "route_gather.hpp"
 #include "route_scan.hpp"
 
@@ -44,9 +45,9 @@ namespace wq {
 int launch_shard_messages(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
                           const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, wq_msg_rec* d_out,
                           uint32_t* d_counts);
-int launch_shard_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
-                       const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, uint32_t* d_slots,
-                       uint32_t* d_perm, uint32_t* d_counts, uint32_t stride);
+int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                        const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, uint32_t me,
+                        const SlotLayout& L, uint32_t* d_slots, uint32_t* d_perm, uint32_t* d_a, int phases);
 int launch_route_records(wq_router* h, const wq_msg_rec* d_recs, size_t M, uint32_t* d_offsets, uint32_t* d_peers,
                          uint32_t* d_msgs, size_t capacity);
 int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
@@ -70,6 +71,8 @@ struct wq_hub {
         const size_t* const* sbytes = nullptr;
         int n = 0;
         int device = 0;
+        hipEvent_t ready = nullptr;  // the poster's send buffers are complete once this has fired
+        hipEvent_t done = nullptr;   // the poster has finished reading its peers' send buffers
     };
     std::vector<Post> post;
     std::vector<uint32_t> attached;
@@ -150,14 +153,20 @@ RcclApi& rccl() {
 
 constexpr int kXNone = 0, kXHub = 1, kXRccl = 2, kXCallback = 3;
 constexpr double kHubTimeoutS = 120.0;
-// The small exchange vectors (ShardCtx::small, allocated at attach): the slot counts exchange
-// {slots, status} u32 x 2 per shard (send at kSmallA, receive after it), the pool-size exchange
-// {pool words, 0, status, 0} u64 x 4 per shard (send at kSmallC, receive after it), and the
-// message-side counters of a slot tick (kSmallCnt: P and the error bits, from its tile scan).
+// The small exchange vectors (ShardCtx::small, allocated at attach). Slot tick: A = {slots, status}
+// u32 x 2 per shard (send at kSmallA, receive right after), C = {pool words, status} u32 x 2 per
+// shard (send at kSmallC, receive right after), and at kSmallCnt four counter blocks: the
+// message-side tile scan (P, error / overflow bits), the own-cube count pass, the owner's count pass
+// over received slots, and a scratch block (the count kernels' "next call" slot). Status words:
+// bits 0-7 the negated WQ_E_* code of a local failure, 8-23 device error bits (8 stale table, 4
+// spin, 2 > 2^32 pairs), 31 (kStBudget) an exchange budget was too small. The expanded-return tick
+// uses {count, status} u32 x 2 at kSmallA and {pairs, status} u64 x 2 at kSmallC.
 constexpr size_t kSmallA = 0, kSmallC = 1024, kSmallCnt = 5120, kSmallBytes = 8192;
+constexpr size_t kCntScan = 0, kCntSelf = 1, kCntOwner = 2, kCntScratch = 3;
 static_assert(kSmallA + 4 * WQ_MAX_SHARDS * 4 <= kSmallC && kSmallC + 8 * WQ_MAX_SHARDS * 8 <= kSmallCnt &&
-                  kSmallCnt + sizeof(wq_route_counters) <= kSmallBytes,
+                  kSmallCnt + 4 * sizeof(wq_route_counters) <= kSmallBytes,
               "small exchange vector layout");
+constexpr uint32_t kStCodeMask = 0xFFu;
 
 }  // namespace
 
@@ -169,10 +178,10 @@ struct SegBounds {
 // One exchange of n buffers: buffer k sends sbytes[k][d] bytes to rank d (segments contiguous in
 // rank order from send[k]) and receives rbytes[k][s] from rank s into recv[k].
 struct Xfer {
-    const void* send[2];
-    const size_t* sbytes[2];
-    void* recv[2];
-    const size_t* rbytes[2];
+    const void* send[3];
+    const size_t* sbytes[3];
+    void* recv[3];
+    const size_t* rbytes[3];
     int n;
 };
 
@@ -189,16 +198,29 @@ struct ShardCtx {
     std::vector<uint32_t> sc, rc;
     std::vector<uint64_t> ps, pr;
     // workspace of the slot tick (compact slots out, row references + cube-list pools back)
-    DevBuf slots, perm, rslots, ocnt, hslot, plen, poff, claim, lead, self_ref, ref_send, ref_recv, pool_send,
-        pool_recv, desc_fill, desc_msg, e_msg, self_w, mtiles;
+    DevBuf slots, perm, rslots, ocnt, hslot, plen, poff, claim, lead, ref_send, ref_recv, pool_send, pool_recv,
+        desc_fill, e_msg, info_msg, mtiles, otiles, blk;
     uint64_t claim_cap = 0;  // claim table entries (power of two); 0 = not allocated
     uint64_t ticks = 0;      // slot ticks run: the claim table's tag
+    // exchange budgets of the slot tick, identical on both ends of every pair: slots me -> d and
+    // s -> me (whole 256-slot blocks; 0 for this shard itself), pool words me -> s and o -> me. Set
+    // from the previous tick's true sizes with headroom; without them (first tick, or after a tick
+    // whose sizes outgrew them) the tick runs exact, reading the sizes back twice.
+    std::vector<uint32_t> b1_out, b1_in;
+    std::vector<uint64_t> b2_out, b2_in;
+    bool budgets = false;
+    uint64_t n_exact = 0, n_budget = 0;  // slot ticks of each kind (wq_shard_tick_stats)
+    void* hsmall = nullptr;              // pinned copy of the small vectors at the end of a tick
+    hipStream_t side = nullptr;          // the own-cube count pass, beside the exchanges
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_ready = nullptr, ev_done = nullptr;
     // bytes this shard sent to / received from OTHER shards in its latest tick (xGMI volume)
     uint64_t last_sent = 0, last_recv = 0;
     // the latest tick, kept for wq_sharded_copy_out after WQ_E_CAPACITY
     uint64_t last_M = 0, last_P = 0;
     bool last_ready = false;
-    bool last_slots = false;  // the latest tick was a slot tick (copy_out = scan + gather of desc_msg)
+    bool last_slots = false;  // the latest tick was a slot tick (copy_out = scan + emit of its rows)
+    uint64_t last_gen = 0;    // its table generation: its own-cube rows point into the table
+    const uint32_t* last_sender = nullptr;  // its d_sender (OnlySelf rows read the sender)
 };
 
 namespace {
@@ -252,13 +274,18 @@ int exchange(wq_router* h, const Xfer& x) {
         return WQ_OK;
     }
     if (sc.kind == kXHub) {
+        // No host wait on the GPU: each rank's send buffers are complete at its `ready` event, which
+        // the readers' streams wait on before their peer copies; each reader records `done` after
+        // them, and every rank's stream waits on all `done` events before it goes on (and may
+        // overwrite a send buffer). The host threads only meet at the two barriers.
         wq_hub& hub = *sc.hub;
-        WQ_HIP(h, hipStreamSynchronize(s));  // this rank's send buffers are complete
+        WQ_HIP(h, hipEventRecord(sc.ev_ready, s));
         wq_hub::Post& mine = hub.post[me];
         mine.send = x.send;
         mine.sbytes = x.sbytes;
         mine.n = x.n;
         mine.device = h->device;
+        mine.ready = sc.ev_ready;
         if (!hub.barrier(kHubTimeoutS)) return set_error(h, WQ_E_RCCL, "hub exchange: a peer never arrived");
         int rc = WQ_OK;
         for (uint32_t src = 0; src < G && rc == WQ_OK; ++src) {
@@ -266,6 +293,13 @@ int exchange(wq_router* h, const Xfer& x) {
             if (p.n != x.n) {
                 rc = set_error(h, WQ_E_INVALID, "hub exchange: ranks disagree on the buffer count");
                 break;
+            }
+            if (src != me) {
+                const hipError_t we = hipStreamWaitEvent(s, p.ready, 0);
+                if (we != hipSuccess) {
+                    rc = set_error(h, WQ_E_HIP, "hub exchange wait", we);
+                    break;
+                }
             }
             for (int k = 0; k < x.n; ++k) {
                 const size_t bytes = p.sbytes[k][me];
@@ -288,11 +322,14 @@ int exchange(wq_router* h, const Xfer& x) {
                 }
             }
         }
-        const hipError_t e = hipStreamSynchronize(s);  // done reading the peers' buffers ...
-        if (!hub.barrier(kHubTimeoutS))                // ... before any of them reuses one
+        hipError_t e = hipEventRecord(sc.ev_done, s);  // done reading the peers' buffers ...
+        mine.done = sc.ev_done;
+        if (!hub.barrier(kHubTimeoutS))                  // ... before any of them reuses one
             return set_error(h, WQ_E_RCCL, "hub exchange: a peer never finished");
+        for (uint32_t d = 0; d < G && e == hipSuccess; ++d)
+            if (d != me) e = hipStreamWaitEvent(s, hub.post[d].done, 0);
         if (rc) return rc;
-        if (e != hipSuccess) return set_error(h, WQ_E_HIP, "hub exchange sync", e);
+        if (e != hipSuccess) return set_error(h, WQ_E_HIP, "hub exchange events", e);
         return WQ_OK;
     }
     return set_error(h, WQ_E_INVALID, "no exchange attached");
@@ -543,64 +580,6 @@ __device__ __forceinline__ const uint32_t* row_src(uint32_t kind, uint32_t off, 
     return kind == kRefList ? list + off : reinterpret_cast<const uint32_t*>(recs) + ((uint64_t)off * 32 + kInlineWord0);
 }
 
-__device__ __forceinline__ void put_desc(uint4* desc_msg, uint32_t* e_msg, uint32_t m, uint32_t e, uint32_t skip,
-                                         const uint32_t* src) {
-    const uint64_t a = reinterpret_cast<uint64_t>(src);
-    desc_msg[m] = make_uint4(e, skip, (uint32_t)a, (uint32_t)(a >> 32));
-    e_msg[m] = e;
-}
-
-// (owner) the count pass over the received slots (route_count.hpp count_rows, one slot per lane).
-// This shard's own slots — all of them at G = 1 — resolve right here into their messages'
-// descriptors (pointers into the table): the ingesting side is this GPU, so nothing is staged and
-// the record lines the count just read are still in the caches when the gather follows. A remote
-// source's slot leaves its count and locator for the claim / reference kernels.
-struct SlotCountParams {
-    CountParams c;
-    uint32_t self_lo, self_hi;  // this shard's own segment of the received slots
-    const uint32_t* perm;       // sent slot -> message
-    uint32_t self_sent;         // first sent slot of the own segment
-    const uint32_t* sender;
-    uint4* desc_msg;
-    uint32_t* e_msg;
-    uint32_t* self_w;
-};
-
-__global__ __launch_bounds__(kBlock, 8) void k_count_slots(SlotCountParams p) {
-    const int tid = threadIdx.x;
-    if (blockIdx.x == 0 && tid == 0) {
-        p.c.cnt_next->n_pairs = 0;
-        p.c.cnt_next->n_candidates = 0;
-        p.c.cnt_next->overflow = 0;
-        p.c.cnt_next->error = 0;
-    }
-    const uint32_t m0 = blockIdx.x * kBlock;
-    uint64_t F_local = 0;
-    uint32_t E_local = 0;
-    uint32_t e_out[1];
-    uint2 inf_out[1];
-    count_rows<true, 1, 0, false, true>(p.c.in, p.c.t, m0, e_out, inf_out, F_local, E_local);
-    const uint32_t i = m0 + tid;
-    if (i >= p.c.in.M) return;
-    if (i >= p.self_lo && i < p.self_hi) {
-        const uint32_t m = p.perm[p.self_sent + (i - p.self_lo)];
-        if (m == kNone) return;  // a tail slot
-        uint32_t kind, off, skip;
-        slot_row(inf_out[0], &kind, &off, &skip);
-        const uint32_t e = e_out[0];
-        if (kind == kRefSelf) {
-            if (e) p.self_w[m] = p.sender[m];
-            put_desc(p.desc_msg, p.e_msg, m, e, kNone, p.self_w + m);
-        } else {
-            put_desc(p.desc_msg, p.e_msg, m, e, skip == kRefSkipNone ? kNone : skip,
-                     row_src(kind, off, p.c.t.list, p.c.t.recs));
-        }
-        return;
-    }
-    p.c.e[i] = e_out[0];
-    p.c.info[i] = inf_out[0];
-}
-
 // (owner, remote slots) a remote source's slot becomes its reference into the source's pool and,
 // for the claiming slot, the pool row copying its cube's peers.
 __global__ __launch_bounds__(kBlock) void k_ref_make(RefOwnerParams p) {
@@ -625,50 +604,94 @@ __global__ __launch_bounds__(kBlock) void k_ref_make(RefOwnerParams p) {
     p.ref_send[t] = ref;
 }
 
-// (owner, G > 1) the per-destination words of the pool-size exchange: {pool words, 0, status, 0}.
-// status = error bits of the count pass (8: stale table) << 32.
-__global__ void k_ref_sizes(const uint32_t* __restrict__ poff, SegBounds rrem, uint32_t G,
-                            const uint32_t* __restrict__ stale, unsigned long long* __restrict__ out) {
-    const uint32_t d = threadIdx.x;
-    if (d >= G) return;
-    const uint32_t err = (stale && *stale) ? kErrStale : 0u;
-    out[4 * d] = poff ? (unsigned long long)(poff[rrem.b[d + 1]] - poff[rrem.b[d]]) : 0ull;
-    out[4 * d + 1] = 0;
-    out[4 * d + 2] = (unsigned long long)err << 32;
-    out[4 * d + 3] = 0;
-}
-
-struct ResolveParams {
-    const uint32_t* perm;     // sent slot -> message (kNone: a tail slot)
-    const uint32_t* sender;   // the caller's d_sender
-    const uint3* ref_recv;    // references from the remote owners, in sent-slot order (own segment left out)
-    uint32_t self_a, self_b;  // this shard's own segment of the sent slots
-    SegBounds sseg;           // sent slots per owner
-    uint32_t G, n;            // n = remote slots
-    const uint32_t* pool;     // the pools received, owner after owner
-    uint64_t pbase[WQ_MAX_SHARDS + 1];
-    uint4* desc_msg;          // per message: {recipients, skip, pointer}
-    uint32_t* e_msg;          // per message: recipients
-    uint32_t* self_w;         // per message: the sender, for OnlySelf rows
+// (owner) the C vector of the pool-size exchange, per source d: {pool words for d, status}. The
+// status carries the owner's device error bits (8: stale table, plus its count pass's bits) and the
+// budget bit when this shard knows of ANY budget that was too small — its own slot segments (A
+// sent), any source's (A received: every shard receives every A vector), or its own pools here — so
+// after the exchange every shard knows the same: redo the tick exactly, or not.
+struct CVecParams {
+    const uint32_t* a_send;  // 2G words
+    const uint32_t* a_recv;  // 2G words
+    const uint32_t* poff;    // nullable: no remote slots
+    SegBounds rb;            // the receive layout's segments (remote slot index per source)
+    uint64_t b2[WQ_MAX_SHARDS];  // pool word budgets me -> d (~0: no budget, the exact pass)
+    uint32_t G;
+    const uint32_t* stale;
+    const wq_route_counters* cnt;  // the owner count pass's counters (nullable)
+    uint32_t* c_send;        // out: 2G words
 };
 
-// (ingesting GPU) per slot sent to a remote owner: the message's row descriptor, in message order.
+__global__ void k_c_vector(CVecParams p) {
+    const uint32_t d = threadIdx.x;
+    const bool in = d < p.G;
+    uint32_t pool = 0;
+    bool over = false;
+    if (in) {
+        pool = p.poff ? p.poff[p.rb.b[d + 1]] - p.poff[p.rb.b[d]] : 0u;
+        over = (uint64_t)pool > p.b2[d] || (p.a_send[2 * d + 1] & kStBudget) || (p.a_recv[2 * d + 1] & kStBudget);
+    }
+    const bool any_over = __any(over);
+    uint32_t bits = (p.stale && *p.stale) ? kErrStale : 0u;
+    if (p.cnt) bits |= p.cnt->error;
+    if (in) {
+        p.c_send[2 * d] = pool;
+        p.c_send[2 * d + 1] = ((bits & 0xFFFFu) << 8) | (any_over ? kStBudget : 0u);
+    }
+}
+
+// (owner) per 256-slot block of the receive layout (segments are whole blocks): where its pool rows
+// go in the send buffer (the source's budgeted segment) and where that segment ends.
+struct PoolBlocksParams {
+    const uint32_t* poff;
+    SegBounds rb;
+    uint64_t pb[WQ_MAX_SHARDS + 1];  // pool segment bases (words) in the send buffer
+    uint32_t G, nblk;
+    uint64_t* base;
+    uint64_t* lim;
+};
+
+__global__ void k_pool_blocks(PoolBlocksParams p) {
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    if (b >= p.nblk) return;
+    const uint32_t i0 = b * kBlock;
+    const uint32_t s = seg_find(p.rb, p.G, i0);
+    p.base[b] = p.pb[s] + (p.poff[i0] - p.poff[p.rb.b[s]]);
+    p.lim[b] = p.pb[s + 1];
+}
+
+// (ingesting GPU) the row of every slot it sent, from its owner's reference: e and the locator in
+// message order (emit_map_kernel's info: a pool row as kLocPool | word offset into the received
+// pools). A reference that does not lie inside its owner's pool segment — an owner that failed, or
+// a tick whose budgets were too small (both reported after the tick) — routes to nobody, so no
+// kernel ever reads outside the pools.
+struct ResolveParams {
+    const uint32_t* perm;     // sent slot -> message (kNone: tails, padding)
+    const uint3* ref_recv;    // references, in the send layout
+    SegBounds sb;             // the send layout's segments (slot index per owner)
+    uint32_t G, n;            // n = slots in the send layout
+    uint64_t prb[WQ_MAX_SHARDS + 1];  // pool segment bases (words) in the receive buffer
+    uint32_t* e_msg;
+    uint2* info_msg;
+};
+
 __global__ __launch_bounds__(kBlock) void k_ref_resolve(ResolveParams p) {
-    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    if (t >= p.n) return;
-    const uint32_t k = t < p.self_a ? t : t + (p.self_b - p.self_a);  // the sent slot
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= p.n) return;
     const uint32_t m = p.perm[k];
-    if (m == kNone) return;  // the tail of a two-slot message
-    const uint3 ref = p.ref_recv[t];
+    if (m == kNone) return;
+    const uint3 ref = p.ref_recv[k];
     const uint32_t kind = ref.z >> 30, sk = ref.z & kRefSkipNone;
-    if (kind == kRefSelf) {
-        if (ref.y) p.self_w[m] = p.sender[m];
-        put_desc(p.desc_msg, p.e_msg, m, ref.y, kNone, p.self_w + m);
+    if (kind == kRefSelf) {  // OnlySelf: the sender when subscribed (y = 0 or 1), or an empty row
+        p.e_msg[m] = ref.y <= 1u ? ref.y : 0u;
+        p.info_msg[m] = make_uint2(kLocSelf, kNone);
         return;
     }
+    const uint32_t o = seg_find(p.sb, p.G, k);
+    const uint64_t at = p.prb[o] + ref.x;
     const uint32_t skip = sk == kRefSkipNone ? kNone : sk;
-    const uint32_t e = ref.y - (skip != kNone ? 1u : 0u);
-    put_desc(p.desc_msg, p.e_msg, m, e, skip, p.pool + p.pbase[seg_find(p.sseg, p.G, k)] + ref.x);
+    const bool ok = kind == kRefPool && at + ref.y <= p.prb[o + 1] && ref.y && (skip == kNone || skip < ref.y);
+    p.e_msg[m] = ok ? ref.y - (skip != kNone ? 1u : 0u) : 0u;
+    p.info_msg[m] = ok ? make_uint2(kLocPool | (uint32_t)at, skip) : make_uint2(0, kNone);
 }
 
 int attach(wq_router* h, uint32_t G, uint32_t rank) {
@@ -676,41 +699,47 @@ int attach(wq_router* h, uint32_t G, uint32_t rank) {
     if (h->shard) return set_error(h, WQ_E_INVALID, "an exchange is already attached (wq_shard_detach first)");
     h->shard = new (std::nothrow) ShardCtx();
     if (!h->shard) return WQ_E_OOM;
-    h->shard->G = G;
-    h->shard->rank = rank;
+    ShardCtx& sc = *h->shard;
+    sc.G = G;
+    sc.rank = rank;
     // the small exchange vectors live here for the handle's whole attachment: a tick never has to
     // allocate before its first exchange
-    if (h->shard->small.ensure(kSmallBytes) != hipSuccess) {
-        delete h->shard;
-        h->shard = nullptr;
-        return set_error(h, WQ_E_OOM, "hipMalloc of the shard exchange vectors");
+    bool ok = sc.small.ensure(kSmallBytes) == hipSuccess &&
+              hipHostMalloc(&sc.hsmall, kSmallBytes, hipHostMallocDefault) == hipSuccess &&
+              hipStreamCreateWithFlags(&sc.side, hipStreamNonBlocking) == hipSuccess;
+    for (hipEvent_t* e : {&sc.ev_fork, &sc.ev_join, &sc.ev_ready, &sc.ev_done})
+        ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        shard_release(h);
+        return set_error(h, WQ_E_OOM, "shard exchange vectors / stream / events");
     }
+    sc.b1_out.assign(G, 0);
+    sc.b1_in.assign(G, 0);
+    sc.b2_out.assign(G, 0);
+    sc.b2_in.assign(G, 0);
     return WQ_OK;
 }
 
-// The slot tick's CSR from its message-order descriptors (e_msg, desc_msg): per-256-message
-// totals, the tile scan (offsets[M] = P, the counters at kSmallCnt: P, the overflow / error bits),
-// then the rows gathered with their offsets (outputs beyond capacity are not written).
+// The slot tick's CSR from its rows in message order (e_msg, info_msg; per-256-message totals in
+// mtiles): the tile scan (offsets[M] = P, the counters at kCntScan: P, the overflow / error bits),
+// then emit_map_kernel — rows of this shard's own cubes read the table, the others the pools
+// received (outputs beyond capacity are not written).
 int slots_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity) {
     ShardCtx& sc = *h->shard;
     const uint64_t M = sc.last_M;
     hipStream_t s = h->stream;
-    wq_route_counters* cnt = reinterpret_cast<wq_route_counters*>(sc.small.as<char>() + kSmallCnt);
-    WQ_HIP(h, hipMemsetAsync(cnt, 0, sizeof(*cnt), s));
+    wq_route_counters* cnt = reinterpret_cast<wq_route_counters*>(sc.small.as<char>() + kSmallCnt) + kCntScan;
     if (M == 0) {
+        WQ_HIP(h, hipMemsetAsync(cnt, 0, sizeof(*cnt), s));
         WQ_HIP(h, hipMemsetAsync(d_offsets, 0, 4, s));
         return WQ_OK;
     }
     const uint32_t nt = (uint32_t)((M + kBlock - 1) / kBlock);
-    WQ_ALLOC(h, sc.mtiles, (uint64_t)nt * 8);
     uint32_t* tile_total = sc.mtiles.as<uint32_t>();
     uint32_t* tile_prefix = tile_total + nt;
-    hipLaunchKernelGGL(row_tile_sums_kernel, dim3(nt), dim3(kBlock), 0, s, sc.e_msg.as<uint32_t>(), (uint32_t)M,
-                       tile_total);
-    WQ_HIP(h, hipGetLastError());
     TileScanParams tp;
     tp.tile_total = tile_total;
-    tp.tile_F = tile_total;  // no candidate count on this path: F is reported as P
+    tp.tile_F = tile_total;  // F is reported as P on this path
     tp.tile_prefix = tile_prefix;
     tp.n_tiles = nt;
     tp.offsets = d_offsets;
@@ -720,11 +749,23 @@ int slots_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_
     tp.health = h->rws.buf.p ? route_health(h) : nullptr;
     tp.stale = h->tab.stale.as<uint32_t>();  // error bit 8: the table still misses a device batch
     if (int rc = launch_tile_scan(h, tp)) return rc;
-    GatherParams gp{nullptr, sc.desc_msg.as<uint4>(), (uint32_t)M, capacity ? d_peers : nullptr, d_msgs, capacity};
-    gp.e = sc.e_msg.as<uint32_t>();
-    gp.tile_prefix = tile_prefix;
-    gp.offsets = d_offsets;
-    hipLaunchKernelGGL((gather_rows_kernel<16, true>), dim3(nt), dim3(kBlock), 0, s, gp);
+    EmitParams ep;
+    ep.sender = sc.last_sender;
+    ep.pos = nullptr;
+    ep.repl = nullptr;
+    ep.M = (uint32_t)M;
+    ep.t = table_view(h);
+    ep.e = sc.e_msg.as<uint32_t>();
+    ep.tile_prefix = tile_prefix;
+    ep.count_tile = kBlock;
+    ep.offsets = d_offsets;
+    ep.info = sc.info_msg.as<uint2>();
+    ep.peers = capacity ? d_peers : nullptr;
+    ep.msgs = d_msgs;
+    ep.capacity = capacity;
+    ep.n_blocks = nt;
+    ep.pool = sc.G > 1 ? sc.pool_recv.as<uint32_t>() : nullptr;  // pool rows (kLocPool) only at G > 1
+    hipLaunchKernelGGL((emit_map_kernel<16>), dim3((nt + 1) / 2), dim3(kBlock), 0, s, ep);
     WQ_HIP(h, hipGetLastError());
     return WQ_OK;
 }
@@ -735,6 +776,9 @@ int copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_m
     const uint64_t M = sc.last_M, P = sc.last_P;
     hipStream_t s = h->stream;
     if (sc.last_slots) {
+        // the kept rows of this shard's own cubes point into the table: only while it is unchanged
+        if (h->table_gen != sc.last_gen)
+            return set_error(h, WQ_E_INVALID, "sharded copy-out: the table changed since the tick (route again)");
         if (int rc = slots_copy_out(h, d_offsets, d_peers, d_msgs, capacity)) return rc;
         if (P > capacity) return set_error(h, WQ_E_CAPACITY, "sharded tick: output capacity too small (required size in *n_pairs)");
         return WQ_OK;
@@ -766,13 +810,18 @@ void shard_release(wq_router* h) {
     if (!h->shard) return;
     ShardCtx* sc = h->shard;
     if (sc->kind == kXRccl && sc->comm) (void)rccl().CommDestroy(sc->comm);
-    DevBuf* bufs[] = {&sc->recs,     &sc->recv,      &sc->cnt2,     &sc->pc,        &sc->own_off,  &sc->own_peers,
-                      &sc->own_e,    &sc->ret_e,     &sc->ret_off,  &sc->ret_peers, &sc->by_msg,   &sc->tmp,
-                      &sc->small,    &sc->slots,     &sc->perm,     &sc->rslots,    &sc->ocnt,     &sc->hslot,
-                      &sc->plen,     &sc->poff,      &sc->claim,    &sc->lead,      &sc->self_ref, &sc->ref_send,
-                      &sc->ref_recv, &sc->pool_send, &sc->pool_recv, &sc->desc_fill, &sc->desc_msg, &sc->e_msg,
-                      &sc->self_w,   &sc->mtiles};
+    if (sc->side) (void)hipStreamSynchronize(sc->side);
+    DevBuf* bufs[] = {&sc->recs,     &sc->recv,      &sc->cnt2,      &sc->pc,        &sc->own_off,  &sc->own_peers,
+                      &sc->own_e,    &sc->ret_e,     &sc->ret_off,   &sc->ret_peers, &sc->by_msg,   &sc->tmp,
+                      &sc->small,    &sc->slots,     &sc->perm,      &sc->rslots,    &sc->ocnt,     &sc->hslot,
+                      &sc->plen,     &sc->poff,      &sc->claim,     &sc->lead,      &sc->ref_send, &sc->ref_recv,
+                      &sc->pool_send, &sc->pool_recv, &sc->desc_fill, &sc->e_msg,    &sc->info_msg, &sc->mtiles,
+                      &sc->otiles,   &sc->blk};
     for (DevBuf* b : bufs) b->release();
+    if (sc->hsmall) (void)hipHostFree(sc->hsmall);
+    if (sc->side) (void)hipStreamDestroy(sc->side);
+    for (hipEvent_t e : {sc->ev_fork, sc->ev_join, sc->ev_ready, sc->ev_done})
+        if (e) (void)hipEventDestroy(e);
     delete sc;
     h->shard = nullptr;
 }
@@ -993,25 +1042,48 @@ static int shard_exchange_route(wq_router* h, const double* d_pos, const int64_t
     return WQ_OK;
 }
 
-// The slot tick (radius filter off): wq_sharded_route_tick_device's result with
-//   A   {slots, status} per owner                                        (host read 1)
-//   B   the compact slots (20 B per regular message)
-//   C   {pool words, recipients, status} per source                     (host read 2)
-//   D   per slot a 12-byte row reference, and per source ONE copy of every cube its messages hit
-// so a long list crosses xGMI once per (tick, destination) instead of once per message; the
-// ingesting GPU gathers the CSR itself. G = 1 skips the exchanges and reads P back at the end.
-// Local failures keep the collective going: a failed shard step sends zero-sized segments with its
-// status, every shard sees every status and all of them return the error after exchange D.
-static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
-                              const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t* d_offsets,
-                              uint32_t* d_peers, uint32_t* d_msgs, size_t capacity, size_t* n_pairs) {
+// The slot tick (radius filter off) — wq_sharded_route_tick_device's result, built as
+//   own     this shard's own cubes: count_kernel<OWN> over the caller's messages, on a side stream
+//           beside the exchanges (no slot, nothing crosses a link)
+//   X1      {A: slots + status per owner, the slots: 20 B per remote message, budgeted segments}
+//   owner   count the received slots (count_kernel<SLOTS>), claim each (source, cube) once
+//           (k_ref_claim), a 12-byte reference per slot and per source ONE pool of cube lists
+//   X2      {C: pool words + status per source, the references, the pools}
+//   ingest  references -> rows (k_ref_resolve), tile scan, emit_map_kernel over own + pool rows
+//   end     ONE host read: P, every shard's status, the true sizes (the next tick's budgets)
+// so a long list crosses xGMI once per (tick, destination), and the exchanges are enqueued without
+// reading anything back: their sizes are the budgets, fixed on the host before the tick (the
+// previous tick's true sizes + 1/16 + a block; identical on both ends of every pair, since both saw
+// the same sizes). A tick whose sizes outgrow a budget is flagged on the device; the status reaches
+// every shard through C, and all of them redo the tick exactly: A and C exchanged alone first and
+// read back, as the first tick does. Local failures keep the collective going: a failed step sends
+// its status (zero slots / empty pools) and every shard returns the error after X2.
+namespace {
+inline uint32_t whole_blocks(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock * kBlock); }
+inline uint32_t slot_budget(uint64_t n) { return whole_blocks(n + n / 16 + kBlock); }
+inline uint64_t pool_budget(uint64_t n) { return n + n / 16 + 1024; }
+}  // namespace
+
+static int ensure_health(wq_router* h) {
+    RouteWs& rw = h->rws;
+    if (!rw.buf.p) {  // as route_counters lays it out: health words first
+        WQ_ALLOC(h, rw.buf, 128);
+        WQ_HIP(h, hipMemsetAsync(rw.buf.p, 0, 128, h->stream));
+        rw.calls = 0;
+    }
+    return WQ_OK;
+}
+
+static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                     const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t* d_offsets,
+                     uint32_t* d_peers, uint32_t* d_msgs, size_t capacity, size_t* n_pairs, bool exact, int inject,
+                     bool* redo) {
     hipStream_t s = h->stream;
     ShardCtx& sc = *h->shard;
     const uint32_t G = sc.G, me = sc.rank;
+    *redo = false;
     sc.last_ready = false;
     sc.last_slots = true;
-    const int inject = h->shard_inject;
-    h->shard_inject = 0;
     int late = WQ_OK;
     std::string late_msg;
     auto fail = [&](int rc) {
@@ -1021,140 +1093,187 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
         }
         return rc;
     };
-    char* small = sc.small.as<char>();
-    uint32_t* a_send = reinterpret_cast<uint32_t*>(small + kSmallA);
-    uint32_t* a_recv = a_send + 2 * G;
-    unsigned long long* c_send = reinterpret_cast<unsigned long long*>(small + kSmallC);
-    unsigned long long* c_recv = c_send + 4 * G;
     auto alloc = [&](DevBuf& b, size_t bytes) -> int {
         return b.ensure(bytes) == hipSuccess ? WQ_OK : set_error(h, WQ_E_OOM, "hipMalloc (sharded tick workspace)");
     };
+    char* small = sc.small.as<char>();
+    uint32_t* a_send = reinterpret_cast<uint32_t*>(small + kSmallA);
+    uint32_t* a_recv = a_send + 2 * G;
+    uint32_t* c_send = reinterpret_cast<uint32_t*>(small + kSmallC);
+    uint32_t* c_recv = c_send + 2 * G;
+    wq_route_counters* cnts = reinterpret_cast<wq_route_counters*>(small + kSmallCnt);
+    const size_t small_used = kSmallCnt + 4 * sizeof(wq_route_counters);
+    WQ_HIP(h, hipMemsetAsync(small, 0, small_used, s));
+    WQ_HIP(h, hipMemsetAsync(c_send, 0, 16 * G, s));
+    if (int rc = ensure_health(h)) return rc;
+    if (exact) sc.n_exact++;
+    else sc.n_budget++;
+    // host sources of status copies: alive until the end-of-tick read has synchronised the stream
+    std::vector<uint32_t> st_host(2 * G, 0);
+    auto put_status = [&](uint32_t* dst) -> int {
+        for (uint32_t d = 0; d < G; ++d) st_host[2 * d + 1] = status_of(late);
+        WQ_HIP(h, hipMemcpyAsync(dst, st_host.data(), 8 * G, hipMemcpyHostToDevice, s));
+        return WQ_OK;
+    };
 
-    // ---- 1. the M-sized buffers, then the slots grouped by owner ----
-    const uint64_t slot_cap = 2 * (uint64_t)M + 1;
-    WQ_HIP(h, hipMemsetAsync(small, 0, kSmallCnt, s));  // counts and statuses
     if (inject == 1) fail(set_error(h, WQ_E_INVALID, "injected failure at step 1 (test hook)"));
-    if (!late && !fail(alloc(sc.slots, slot_cap * kSlotWords * 4)) && !fail(alloc(sc.perm, slot_cap * 4)) &&
-        !fail(alloc(sc.desc_msg, (M + 1) * 16)) && !fail(alloc(sc.e_msg, (M + 1) * 4)) &&
-        !fail(alloc(sc.self_w, (M + 1) * 4)))
-        fail(launch_shard_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, sc.slots.as<uint32_t>(),
-                                sc.perm.as<uint32_t>(), a_send, 2));
-    // host sources of status copies live until the call's host reads have synchronised the stream
-    std::vector<uint32_t> a_status(2 * G, 0);
-    std::vector<unsigned long long> c_status(4 * G, 0);
-    if (late) {  // nothing to send: zero slots everywhere, and the status
-        for (uint32_t d = 0; d < G; ++d) a_status[2 * d + 1] = status_of(late);
-        WQ_HIP(h, hipMemcpyAsync(a_send, a_status.data(), 8 * G, hipMemcpyHostToDevice, s));
+    // fold in a finished incremental batch first (it may rebuild the table the rows point into)
+    if (!late) fail(table_resolve(h, false));
+    if (!late && G > 1 && h->tab.list.bytes / 4 >= (1ull << 30))
+        fail(set_error(h, WQ_E_CAPACITY, "sharded tick: more than 2^30 list words on one shard"));
+    const TableView tv = table_view(h);
+    const uint32_t nt = (uint32_t)((M + kBlock - 1) / kBlock);
+    if (!late && (fail(alloc(sc.e_msg, (M + 1) * 4)) || fail(alloc(sc.info_msg, (M + 1) * 8)) ||
+                  fail(alloc(sc.mtiles, ((uint64_t)nt * 3 + 4) * 4)))) {
     }
-    std::vector<size_t> eight(G, 8), thirty2(G, 32);
+
+    // ---- own cubes, on the side stream ----
+    bool forked = false;
+    if (!late && M) {
+        WQ_HIP(h, hipEventRecord(sc.ev_fork, s));
+        WQ_HIP(h, hipStreamWaitEvent(sc.side, sc.ev_fork, 0));
+        CountParams cp{};
+        cp.in = RouteIn{d_pos, d_keys, d_world, d_sender, d_repl, (uint32_t)M, (int64_t)h->cube_size};
+        cp.in.own_G = G;
+        cp.in.own_me = me;
+        cp.t = tv;
+        cp.e = sc.e_msg.as<uint32_t>();
+        cp.info = sc.info_msg.as<uint2>();
+        cp.tile_total = sc.mtiles.as<uint32_t>();
+        cp.tile_F = cp.tile_total + 2 * (uint64_t)nt;
+        cp.cnt = cnts + kCntSelf;
+        cp.cnt_next = cnts + kCntScratch;
+        cp.health = route_health(h);
+        cp.n_tiles = nt;
+        const dim3 grid((nt + 1) / 2);  // two tiles per block (grid stride), as launch_route
+        if (G == 1 && d_keys)
+            hipLaunchKernelGGL((count_kernel<true, 1, 8>), grid, dim3(kBlock), 0, sc.side, cp);
+        else if (G == 1)
+            hipLaunchKernelGGL((count_kernel<false, 1, 8>), grid, dim3(kBlock), 0, sc.side, cp);
+        else if (d_keys)
+            hipLaunchKernelGGL((count_kernel<true, 1, 8, 0, false, false, true>), grid, dim3(kBlock), 0, sc.side, cp);
+        else
+            hipLaunchKernelGGL((count_kernel<false, 1, 8, 0, false, false, true>), grid, dim3(kBlock), 0, sc.side, cp);
+        WQ_HIP(h, hipGetLastError());
+        WQ_HIP(h, hipEventRecord(sc.ev_join, sc.side));
+        forked = true;
+    }
+
+    // ---- X1: A + the slots ----
+    std::vector<size_t> eight(G, 8);
+    SlotLayout L{};
+    SegBounds sb{}, rb{};
+    auto set_layout = [&]() -> int {
+        uint64_t so = 0, ro = 0;
+        for (uint32_t d = 0; d < G; ++d) {
+            L.base[d] = (uint32_t)so;
+            L.budget[d] = sc.b1_out[d];
+            sb.b[d] = (uint32_t)so;
+            rb.b[d] = (uint32_t)ro;
+            so += sc.b1_out[d];
+            ro += sc.b1_in[d];
+        }
+        L.base[G] = sb.b[G] = (uint32_t)so;
+        rb.b[G] = (uint32_t)ro;
+        if (so >= (1ull << 31) || ro >= (1ull << 31)) return fatal_receive(h, "sharded tick: more than 2^31 slots");
+        return WQ_OK;
+    };
+    uint64_t Sb = 0, Rb = 0;
     int rc;
     if (G > 1) {
-        Xfer x{{a_send}, {eight.data()}, {a_recv}, {eight.data()}, 1};
-        if ((rc = exchange(h, x))) return rc;
-    }
-    std::vector<uint32_t> av(4 * G);
-    WQ_HIP(h, hipMemcpyAsync(av.data(), a_send, (G > 1 ? 16 : 8) * G, hipMemcpyDeviceToHost, s));
-    WQ_HIP(h, hipStreamSynchronize(s));  // host read 1
-    if (G == 1) av[2] = av[0], av[3] = av[1];
-    std::vector<uint64_t> n_out(G), n_in(G);
-    uint64_t peer_status = 0;
-    uint32_t peer_from = 0;
-    SegBounds sseg, rseg, rrem;
-    sseg.b[0] = rseg.b[0] = rrem.b[0] = 0;
-    uint64_t R = 0, S = 0, Rr = 0;
-    for (uint32_t d = 0; d < G; ++d) {
-        n_out[d] = av[2 * d];
-        n_in[d] = av[2 * G + 2 * d];
-        if (av[2 * G + 2 * d + 1] && !peer_status) {
-            peer_status = av[2 * G + 2 * d + 1];
-            peer_from = d;
-        }
-        S += n_out[d];
-        R += n_in[d];
-        if (d != me) Rr += n_in[d];
-        sseg.b[d + 1] = (uint32_t)S;
-        rseg.b[d + 1] = (uint32_t)R;
-        rrem.b[d + 1] = (uint32_t)Rr;  // the remote slots, own segment left out
-    }
-    if (R >= 0xFFFFFC00ull) return fatal_receive(h, "more than 2^32 - 1024 slots on one owner");
-    const uint64_t n_self = n_in[me], R_remote = R - n_self, S_remote = S - n_out[me];
-
-    // ---- 2. the slots ----
-    const uint32_t* rslots = sc.slots.as<uint32_t>();
-    if (G > 1) {
-        if (alloc(sc.rslots, (R ? R : 1) * kSlotWords * 4)) return fatal_receive(h, "hipMalloc of the received slots");
-        std::vector<size_t> sb(G), rb(G);
-        for (uint32_t d = 0; d < G; ++d) {
-            sb[d] = n_out[d] * kSlotWords * 4;
-            rb[d] = n_in[d] * kSlotWords * 4;
-        }
-        Xfer x{{sc.slots.p}, {sb.data()}, {sc.rslots.p}, {rb.data()}, 1};
-        if ((rc = exchange(h, x))) return rc;
-        rslots = sc.rslots.as<uint32_t>();
-    }
-
-    // ---- 3. the owner: count (local_message.rs:52-86 per slot; own slots resolved in place),
-    //         then the remote slots' claims, pools and references ----
-    if (inject == 3) fail(set_error(h, WQ_E_INVALID, "injected failure at step 3 (test hook)"));
-    // fold in a finished incremental batch first (it may rebuild the table the view points into)
-    if (!late) fail(table_resolve(h, false));
-    const TableView tv = table_view(h);
-    wq_route_counters *cur = nullptr, *nxt = nullptr;
-    if (!late && R) fail(route_counters(h, R, nullptr, &cur, &nxt));
-    if (!late && R) {
-        RouteWs& rw = h->rws;
-        if (!fail(alloc(rw.e, R * 4)) && !fail(alloc(rw.info, R * 8)) &&
-            (!R_remote || (!fail(alloc(sc.ocnt, R_remote * 4)) && !fail(alloc(sc.hslot, R_remote * 4)) &&
-                           !fail(alloc(sc.plen, (R_remote + 1) * 4)) && !fail(alloc(sc.poff, (R_remote + 1) * 4)) &&
-                           !fail(alloc(sc.desc_fill, (R_remote + 1) * 16)) &&
-                           !fail(alloc(sc.ref_send, (R_remote + 1) * 12))))) {
-            SlotCountParams cp{};
-            cp.c.in = RouteIn{nullptr, nullptr, nullptr, nullptr, nullptr, (uint32_t)R, (int64_t)h->cube_size};
-            cp.c.in.slots = rslots;
-            cp.c.t = tv;
-            cp.c.e = rw.e.as<uint32_t>();
-            cp.c.info = rw.info.as<uint2>();
-            cp.c.cnt = cur;
-            cp.c.cnt_next = nxt;
-            cp.c.health = route_health(h);
-            cp.self_lo = rseg.b[me];
-            cp.self_hi = rseg.b[me + 1];
-            cp.perm = sc.perm.as<uint32_t>();
-            cp.self_sent = sseg.b[me];
-            cp.sender = d_sender;
-            cp.desc_msg = sc.desc_msg.as<uint4>();
-            cp.e_msg = sc.e_msg.as<uint32_t>();
-            cp.self_w = sc.self_w.as<uint32_t>();
-            hipLaunchKernelGGL(k_count_slots, dim3((unsigned)((R + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, cp);
-            if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "count launch (sharded tick)"));
-        }
-        uint64_t C = 0;
-        if (!late && R_remote) {  // claim table: load <= 1/2
-            C = 1024;
-            while (C < 2 * R_remote) C <<= 1;
-            if (C > sc.claim_cap) {
-                if (!fail(alloc(sc.claim, C * 8)) && !fail(alloc(sc.lead, C * 4))) {
-                    if (hipMemsetAsync(sc.claim.p, 0, C * 8, s) != hipSuccess) fail(set_error(h, WQ_E_HIP, "memset"));
-                    sc.claim_cap = C;
-                }
-            } else {
-                C = sc.claim_cap;
+        if (exact) {  // the true counts first (A alone, read back): budgets = the counts, whole blocks
+            SlotLayout inf{};
+            for (uint32_t d = 0; d < G; ++d) inf.budget[d] = 0xFFFFFFFFu;
+            if (!late)
+                fail(launch_budget_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, me, inf, nullptr, nullptr,
+                                         a_send, 1));
+            if (late && (rc = put_status(a_send))) return rc;
+            Xfer x{{a_send}, {eight.data()}, {a_recv}, {eight.data()}, 1};
+            if ((rc = exchange(h, x))) return rc;
+            uint32_t* hv = static_cast<uint32_t*>(sc.hsmall);
+            WQ_HIP(h, hipMemcpyAsync(hv, a_send, 16 * G, hipMemcpyDeviceToHost, s));
+            WQ_HIP(h, hipStreamSynchronize(s));
+            for (uint32_t d = 0; d < G; ++d) {
+                sc.b1_out[d] = d == me ? 0u : whole_blocks(hv[2 * d]);
+                sc.b1_in[d] = d == me ? 0u : whole_blocks(hv[2 * G + 2 * d]);
             }
         }
-        if (!late && R_remote) {
+        if ((rc = set_layout())) return rc;
+        Sb = sb.b[G];
+        Rb = rb.b[G];
+        if (alloc(sc.slots, (Sb + 2) * kSlotWords * 4) || alloc(sc.perm, (Sb + 2) * 4) ||
+            alloc(sc.rslots, (Rb + 2) * kSlotWords * 4))
+            return fatal_receive(h, "hipMalloc of the sharded tick's slots");
+        if (!late)
+            fail(launch_budget_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, me, L, sc.slots.as<uint32_t>(),
+                                     sc.perm.as<uint32_t>(), a_send, exact ? 2 : 3));
+        if (late) {  // nothing to send: tail slots everywhere (zero words route to nobody either way)
+            WQ_HIP(h, hipMemsetAsync(sc.slots.p, 0, (Sb + 1) * kSlotWords * 4, s));
+            WQ_HIP(h, hipMemsetAsync(sc.perm.p, 0xFF, (Sb + 1) * 4, s));
+            if (!exact && (rc = put_status(a_send))) return rc;
+        }
+        std::vector<size_t> sbytes(G), rbytes(G);
+        for (uint32_t d = 0; d < G; ++d) {
+            sbytes[d] = (size_t)sc.b1_out[d] * kSlotWords * 4;
+            rbytes[d] = (size_t)sc.b1_in[d] * kSlotWords * 4;
+        }
+        if (exact) {
+            Xfer x{{sc.slots.p}, {sbytes.data()}, {sc.rslots.p}, {rbytes.data()}, 1};
+            if ((rc = exchange(h, x))) return rc;
+        } else {
+            Xfer x{{a_send, sc.slots.p}, {eight.data(), sbytes.data()}, {a_recv, sc.rslots.p},
+                   {eight.data(), rbytes.data()}, 2};
+            if ((rc = exchange(h, x))) return rc;
+        }
+    }
+
+    // ---- the owner: count the received slots (local_message.rs:52-86 per slot), claims, references ----
+    if (inject == 3) fail(set_error(h, WQ_E_INVALID, "injected failure at step 3 (test hook)"));
+    RefOwnerParams rp{};
+    if (G > 1 && (alloc(sc.ref_send, (Rb + 1) * 12) || alloc(sc.plen, (Rb + 1) * 4) || alloc(sc.poff, (Rb + 1) * 4)))
+        return fatal_receive(h, "hipMalloc of the owner's references");
+    if (G > 1 && Rb && !late) {
+        RouteWs& rw = h->rws;
+        const uint32_t nto = (uint32_t)(Rb / kBlock);  // whole blocks
+        if (!fail(alloc(rw.e, Rb * 4)) && !fail(alloc(rw.info, Rb * 8)) && !fail(alloc(sc.otiles, (uint64_t)nto * 8)) &&
+            !fail(alloc(sc.ocnt, Rb * 4)) && !fail(alloc(sc.hslot, Rb * 4)) && !fail(alloc(sc.desc_fill, (Rb + 1) * 16))) {
+            CountParams cp{};
+            cp.in = RouteIn{nullptr, nullptr, nullptr, nullptr, nullptr, (uint32_t)Rb, (int64_t)h->cube_size};
+            cp.in.slots = sc.rslots.as<uint32_t>();
+            cp.t = tv;
+            cp.e = rw.e.as<uint32_t>();
+            cp.info = rw.info.as<uint2>();
+            cp.tile_total = sc.otiles.as<uint32_t>();
+            cp.tile_F = cp.tile_total + nto;
+            cp.cnt = cnts + kCntOwner;
+            cp.cnt_next = cnts + kCntScratch;
+            cp.health = route_health(h);
+            cp.n_tiles = nto;
+            hipLaunchKernelGGL((count_kernel<false, 1, 8, 0, false, true>), dim3((nto + 1) / 2), dim3(kBlock), 0, s, cp);
+            if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "count launch (sharded tick)"));
+        }
+        uint64_t C = 1024;  // claim table: load <= 1/2
+        while (C < 2 * Rb) C <<= 1;
+        if (!late && C > sc.claim_cap) {
+            if (!fail(alloc(sc.claim, C * 8)) && !fail(alloc(sc.lead, C * 4))) {
+                if (hipMemsetAsync(sc.claim.p, 0, C * 8, s) != hipSuccess) fail(set_error(h, WQ_E_HIP, "memset"));
+                sc.claim_cap = C;
+            }
+        }
+        C = sc.claim_cap;
+        if (!late) {
             const uint64_t period = (1ull << kRefClaimTagBits) - 1;
             if (sc.ticks && sc.ticks % period == 0 && hipMemsetAsync(sc.claim.p, 0, sc.claim_cap * 8, s) != hipSuccess)
                 fail(set_error(h, WQ_E_HIP, "memset"));  // the tags wrap: forget them all
-            RefOwnerParams rp{};
             rp.e = rw.e.as<uint32_t>();
             rp.info = rw.info.as<uint2>();
             rp.list = tv.list;
             rp.recs = tv.recs;
-            rp.rrem = rrem;
+            rp.rrem = rb;
             rp.G = G;
-            rp.n_rem = (uint32_t)R_remote;
-            rp.self_lo = rseg.b[me];
-            rp.n_self = (uint32_t)n_self;
+            rp.n_rem = (uint32_t)Rb;
+            rp.self_lo = (uint32_t)Rb;  // no own segment: received slot t is remote slot t
+            rp.n_self = 0;
             rp.tag = (uint32_t)(sc.ticks % period) + 1u;
             rp.claim = sc.claim.as<unsigned long long>();
             rp.lead = sc.lead.as<uint32_t>();
@@ -1166,121 +1285,187 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
             rp.ref_send = sc.ref_send.as<uint3>();
             rp.desc_fill = sc.desc_fill.as<uint4>();
             sc.ticks++;
-            hipLaunchKernelGGL(k_ref_claim, dim3((unsigned)((R_remote + kBlock) / kBlock)), dim3(kBlock), 0, s, rp);
+            hipLaunchKernelGGL(k_ref_claim, dim3((unsigned)((Rb + kBlock) / kBlock)), dim3(kBlock), 0, s, rp);
             if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "claim launch (sharded tick)"));
-            if (!late) fail(scan_excl(h, sc.tmp, sc.plen.as<uint32_t>(), sc.poff.as<uint32_t>(), R_remote + 1));
+            if (!late) fail(scan_excl(h, sc.tmp, sc.plen.as<uint32_t>(), sc.poff.as<uint32_t>(), Rb + 1));
             if (!late) {
-                hipLaunchKernelGGL(k_ref_make, dim3((unsigned)((R_remote + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rp);
+                hipLaunchKernelGGL(k_ref_make, dim3((unsigned)(Rb / kBlock)), dim3(kBlock), 0, s, rp);
                 if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "reference launch (sharded tick)"));
             }
         }
     }
 
-    // ---- 4. pool sizes, then the references and pools (G > 1) ----
-    std::vector<unsigned long long> cv(8 * G, 0);
-    std::vector<uint64_t> pbase(G + 1, 0);
+    // ---- X2: C + the references and pools ----
+    std::vector<uint64_t> pb(G + 1, 0), prb(G + 1, 0);
     uint64_t sent = 0, recvd = 0;
     if (G > 1) {
+        const bool owner_ok = Rb && !late;
         if (!late) {
-            hipLaunchKernelGGL(k_ref_sizes, dim3(1), dim3(64), 0, s, R_remote ? sc.poff.as<uint32_t>() : nullptr, rrem,
-                               G, tv.stale, c_send);
+            CVecParams cv{};
+            cv.a_send = a_send;
+            cv.a_recv = a_recv;
+            cv.poff = owner_ok ? sc.poff.as<uint32_t>() : nullptr;
+            cv.rb = rb;
+            for (uint32_t d = 0; d < G; ++d) cv.b2[d] = exact ? ~0ull : sc.b2_out[d];
+            cv.G = G;
+            cv.stale = tv.stale;
+            cv.cnt = owner_ok ? cnts + kCntOwner : nullptr;
+            cv.c_send = c_send;
+            hipLaunchKernelGGL(k_c_vector, dim3(1), dim3(64), 0, s, cv);
             if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "size launch (sharded tick)"));
         }
-        if (late) {  // nothing routed here: zero sizes and the status
-            for (uint32_t d = 0; d < G; ++d) c_status[4 * d + 2] = status_of(late);
-            WQ_HIP(h, hipMemcpyAsync(c_send, c_status.data(), 32 * G, hipMemcpyHostToDevice, s));
+        if (late) {
+            if ((rc = put_status(c_send))) return rc;
+            WQ_HIP(h, hipMemsetAsync(sc.ref_send.p, 0, (Rb + 1) * 12, s));  // references that route to nobody
         }
-        {
-            Xfer x{{c_send}, {thirty2.data()}, {c_recv}, {thirty2.data()}, 1};
+        if (exact) {  // the true pool sizes first (C alone, read back)
+            Xfer x{{c_send}, {eight.data()}, {c_recv}, {eight.data()}, 1};
             if ((rc = exchange(h, x))) return rc;
-        }
-        WQ_HIP(h, hipMemcpyAsync(cv.data(), c_send, 64 * G, hipMemcpyDeviceToHost, s));
-        WQ_HIP(h, hipStreamSynchronize(s));  // host read 2
-        std::vector<uint64_t> pool_out(G), pool_in(G);
-        uint64_t pool_out_total = 0, pool_in_total = 0;
-        for (uint32_t d = 0; d < G; ++d) {
-            pool_out[d] = cv[4 * d];
-            pool_in[d] = cv[4 * G + 4 * d];
-            const uint64_t st = cv[4 * G + 4 * d + 2];
-            if (st && !peer_status) {
-                peer_status = st;
-                peer_from = d;
+            uint32_t* hv = static_cast<uint32_t*>(sc.hsmall);
+            WQ_HIP(h, hipMemcpyAsync(hv, c_send, 16 * G, hipMemcpyDeviceToHost, s));
+            WQ_HIP(h, hipStreamSynchronize(s));
+            for (uint32_t d = 0; d < G; ++d) {
+                sc.b2_out[d] = d == me ? 0 : hv[2 * d];
+                sc.b2_in[d] = d == me ? 0 : hv[2 * G + 2 * d];
             }
-            pool_out_total += pool_out[d];
-            pbase[d] = pool_in_total;
-            pool_in_total += pool_in[d];
         }
-        pbase[G] = pool_in_total;
-        if (alloc(sc.pool_send, (pool_out_total + 1) * 4)) return fatal_receive(h, "hipMalloc of the pools to send");
-        if (alloc(sc.pool_recv, (pool_in_total + 1) * 4) || alloc(sc.ref_recv, (S_remote + 1) * 12))
-            return fatal_receive(h, "hipMalloc of the references / pools to receive");
-        if (!late && R_remote && pool_out_total) {
-            GatherParams gp{sc.poff.as<uint32_t>(), sc.desc_fill.as<uint4>(), (uint32_t)R_remote,
-                            sc.pool_send.as<uint32_t>(), nullptr, pool_out_total};
-            hipLaunchKernelGGL((gather_rows_kernel<16, false>), dim3((unsigned)((R_remote + kBlock - 1) / kBlock)),
-                               dim3(kBlock), 0, s, gp);
+        for (uint32_t d = 0; d < G; ++d) {
+            pb[d + 1] = pb[d] + sc.b2_out[d];
+            prb[d + 1] = prb[d] + sc.b2_in[d];
+        }
+        if (prb[G] >= (1ull << 30)) return fatal_receive(h, "sharded tick: more than 2^30 pool words to receive");
+        if (alloc(sc.pool_send, (pb[G] + 1) * 4) || alloc(sc.pool_recv, (prb[G] + 1) * 4) ||
+            alloc(sc.ref_recv, (Sb + 1) * 12))
+            return fatal_receive(h, "hipMalloc of the references / pools");
+        if (owner_ok && !late && pb[G]) {
+            const uint32_t nbo = (uint32_t)(Rb / kBlock);
+            if (alloc(sc.blk, (uint64_t)nbo * 16 + 16)) return fatal_receive(h, "hipMalloc of the pool blocks");
+            PoolBlocksParams bp{};
+            bp.poff = sc.poff.as<uint32_t>();
+            bp.rb = rb;
+            for (uint32_t d = 0; d <= G; ++d) bp.pb[d] = pb[d];
+            bp.G = G;
+            bp.nblk = nbo;
+            bp.base = sc.blk.as<uint64_t>();
+            bp.lim = bp.base + nbo;
+            hipLaunchKernelGGL(k_pool_blocks, dim3((nbo + kBlock - 1) / kBlock), dim3(kBlock), 0, s, bp);
+            GatherParams gp{sc.poff.as<uint32_t>(), sc.desc_fill.as<uint4>(), (uint32_t)Rb, sc.pool_send.as<uint32_t>(),
+                            nullptr, pb[G]};
+            gp.blk_base = bp.base;
+            gp.blk_lim = bp.lim;
+            hipLaunchKernelGGL((gather_rows_kernel<16, false>), dim3(nbo), dim3(kBlock), 0, s, gp);
             if (hipGetLastError() != hipSuccess) return fatal_receive(h, "pool gather launch");
         }
         std::vector<size_t> rs(G), rr(G), ps(G), pr(G);
         for (uint32_t d = 0; d < G; ++d) {
-            rs[d] = d == me || late ? 0 : n_in[d] * 12;  // references for the slots d sent here
-            // a shard whose local step failed (a WQ_E_* code in its status) sends no references
-            rr[d] = d == me || (uint32_t)cv[4 * G + 4 * d + 2] != 0 ? 0 : n_out[d] * 12;
-            ps[d] = late ? 0 : pool_out[d] * 4;
-            pr[d] = pool_in[d] * 4;
+            rs[d] = (size_t)sc.b1_in[d] * 12;   // references for the slots d sent here
+            rr[d] = (size_t)sc.b1_out[d] * 12;  // references for the slots sent to d
+            ps[d] = (size_t)sc.b2_out[d] * 4;
+            pr[d] = (size_t)sc.b2_in[d] * 4;
             if (d != me) {
-                sent += 8 + n_out[d] * kSlotWords * 4 + 32 + rs[d] + ps[d];
-                recvd += 8 + n_in[d] * kSlotWords * 4 + 32 + rr[d] + pr[d];
+                sent += 16 + (uint64_t)sc.b1_out[d] * kSlotWords * 4 + rs[d] + ps[d];
+                recvd += 16 + (uint64_t)sc.b1_in[d] * kSlotWords * 4 + rr[d] + pr[d];
             }
         }
-        Xfer x{{sc.ref_send.p, sc.pool_send.p}, {rs.data(), ps.data()}, {sc.ref_recv.p, sc.pool_recv.p},
-               {rr.data(), pr.data()}, 2};
-        if ((rc = exchange(h, x))) return rc;
+        if (exact) {
+            Xfer x{{sc.ref_send.p, sc.pool_send.p}, {rs.data(), ps.data()}, {sc.ref_recv.p, sc.pool_recv.p},
+                   {rr.data(), pr.data()}, 2};
+            if ((rc = exchange(h, x))) return rc;
+        } else {
+            Xfer x{{c_send, sc.ref_send.p, sc.pool_send.p}, {eight.data(), rs.data(), ps.data()},
+                   {c_recv, sc.ref_recv.p, sc.pool_recv.p}, {eight.data(), rr.data(), pr.data()}, 3};
+            if ((rc = exchange(h, x))) return rc;
+        }
     }
     sc.last_sent = sent;
     sc.last_recv = recvd;
+
+    // ---- the ingesting side: rows in message order, then the CSR ----
+    if (forked) WQ_HIP(h, hipStreamWaitEvent(s, sc.ev_join, 0));  // own rows written (remote ones as e = 0)
+    if (!late && G > 1 && Sb) {
+        ResolveParams rv{};
+        rv.perm = sc.perm.as<uint32_t>();
+        rv.ref_recv = sc.ref_recv.as<uint3>();
+        rv.sb = sb;
+        rv.G = G;
+        rv.n = (uint32_t)Sb;
+        for (uint32_t d = 0; d <= G; ++d) rv.prb[d] = prb[d];
+        rv.e_msg = sc.e_msg.as<uint32_t>();
+        rv.info_msg = sc.info_msg.as<uint2>();
+        hipLaunchKernelGGL(k_ref_resolve, dim3((unsigned)((Sb + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rv);
+        WQ_HIP(h, hipGetLastError());
+        // the count pass's per-tile totals held its own rows only
+        hipLaunchKernelGGL(row_tile_sums_kernel, dim3(nt), dim3(kBlock), 0, s, sc.e_msg.as<uint32_t>(), (uint32_t)M,
+                           sc.mtiles.as<uint32_t>());
+        WQ_HIP(h, hipGetLastError());
+    }
+    if (!late) {
+        sc.last_M = M;
+        sc.last_sender = d_sender;
+        sc.last_gen = h->table_gen;
+        if ((rc = slots_copy_out(h, d_offsets, d_peers, d_msgs, capacity))) return rc;
+    }
+
+    // ---- the one host read: P, the statuses, the true sizes ----
+    WQ_HIP(h, hipMemcpyAsync(sc.hsmall, small, small_used, hipMemcpyDeviceToHost, s));
+    WQ_HIP(h, hipStreamSynchronize(s));
+    const char* hs = static_cast<const char*>(sc.hsmall);
+    const uint32_t* ha = reinterpret_cast<const uint32_t*>(hs + kSmallA);
+    const uint32_t* hc = reinterpret_cast<const uint32_t*>(hs + kSmallC);
+    const wq_route_counters* hcnt = reinterpret_cast<const wq_route_counters*>(hs + kSmallCnt);
+    // the global picture (the same on every shard): codes and device bits from every shard's A and C
+    uint32_t code = 0, bits = 0, code_from = 0, bits_from = 0;
+    bool over = false;
+    for (uint32_t d = 0; G > 1 && d < G; ++d) {
+        for (uint32_t st : {ha[2 * G + 2 * d + 1], hc[2 * G + 2 * d + 1]}) {
+            if ((st & kStCodeMask) && !code) code = st & kStCodeMask, code_from = d;
+            if (((st >> 8) & 0xFFFFu) && !bits) bits = (st >> 8) & 0xFFFFu, bits_from = d;
+            over |= (st & kStBudget) != 0;
+        }
+    }
+    if (G > 1 && !code && !over) {  // next tick's budgets from this tick's true sizes
+        for (uint32_t d = 0; d < G; ++d) {
+            sc.b1_out[d] = d == me ? 0u : slot_budget(ha[2 * d]);
+            sc.b1_in[d] = d == me ? 0u : slot_budget(ha[2 * G + 2 * d]);
+            sc.b2_out[d] = d == me ? 0 : pool_budget(hc[2 * d]);
+            sc.b2_in[d] = d == me ? 0 : pool_budget(hc[2 * G + 2 * d]);
+        }
+        sc.budgets = true;
+    }
     if (late) {
         h->err = late_msg;
         return late;
     }
-    if (peer_status) return status_error(h, peer_status, peer_from);
-
-    // ---- 5. the ingesting side: remote references -> descriptors, then the CSR ----
-    if (S_remote) {
-        ResolveParams rp{};
-        rp.perm = sc.perm.as<uint32_t>();
-        rp.sender = d_sender;
-        rp.ref_recv = sc.ref_recv.as<uint3>();
-        rp.self_a = sseg.b[me];
-        rp.self_b = sseg.b[me + 1];
-        rp.sseg = sseg;
-        rp.G = G;
-        rp.n = (uint32_t)S_remote;
-        rp.pool = sc.pool_recv.as<uint32_t>();
-        for (uint32_t d = 0; d <= G; ++d) rp.pbase[d] = pbase[d];
-        rp.desc_msg = sc.desc_msg.as<uint4>();
-        rp.e_msg = sc.e_msg.as<uint32_t>();
-        rp.self_w = sc.self_w.as<uint32_t>();
-        hipLaunchKernelGGL(k_ref_resolve, dim3((unsigned)((S_remote + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rp);
-        WQ_HIP(h, hipGetLastError());
+    if (code) return status_error(h, code, code_from);
+    if (over) {  // every shard saw it: all of them redo the tick exactly
+        sc.budgets = false;
+        *redo = true;
+        return WQ_OK;
     }
-    sc.last_M = M;
-    sc.last_ready = true;
-    if ((rc = slots_copy_out(h, d_offsets, d_peers, d_msgs, capacity))) return rc;
-    // P and the error bits: the message-side tile scan's counters and the count pass's, read once
-    // the tick has run (the one host wait after the exchanges)
-    wq_route_counters c[2];
-    WQ_HIP(h, hipMemcpyAsync(&c[0], small + kSmallCnt, sizeof(c[0]), hipMemcpyDeviceToHost, s));
-    if (cur) WQ_HIP(h, hipMemcpyAsync(&c[1], cur, sizeof(c[1]), hipMemcpyDeviceToHost, s));
-    else c[1] = wq_route_counters{};
-    WQ_HIP(h, hipStreamSynchronize(s));
-    const uint32_t err = c[0].error | c[1].error;
-    const uint64_t P = M ? c[0].n_pairs : 0;
+    if (bits) return status_error(h, (uint64_t)bits << 32, bits_from);
+    const uint32_t err = hcnt[kCntScan].error | hcnt[kCntSelf].error | hcnt[kCntOwner].error;
+    const uint64_t P = M ? hcnt[kCntScan].n_pairs : 0;
     sc.last_P = P;
+    sc.last_ready = true;
     *n_pairs = P;
     if (err) return status_error(h, (uint64_t)err << 32, me);
     if (P > capacity) return set_error(h, WQ_E_CAPACITY, "sharded tick: output capacity too small (required size in *n_pairs)");
     return WQ_OK;
+}
+
+static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                              const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t* d_offsets,
+                              uint32_t* d_peers, uint32_t* d_msgs, size_t capacity, size_t* n_pairs) {
+    ShardCtx& sc = *h->shard;
+    const int inject = h->shard_inject;
+    h->shard_inject = 0;
+    bool redo = false;
+    int rc = slot_tick(h, d_pos, d_keys, d_world, d_sender, d_repl, M, d_offsets, d_peers, d_msgs, capacity, n_pairs,
+                       sc.G > 1 && !sc.budgets, inject, &redo);
+    if (rc == WQ_OK && redo)
+        rc = slot_tick(h, d_pos, d_keys, d_world, d_sender, d_repl, M, d_offsets, d_peers, d_msgs, capacity, n_pairs,
+                       true, 0, &redo);
+    return rc;
 }
 
 int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
@@ -1463,6 +1648,13 @@ int wq_shard_last_bytes(wq_router* h, uint64_t* sent, uint64_t* received) {
     if (!h || !sent || !received) return WQ_E_INVALID;
     *sent = h->shard ? h->shard->last_sent : 0;
     *received = h->shard ? h->shard->last_recv : 0;
+    return WQ_OK;
+}
+
+int wq_shard_tick_stats(wq_router* h, uint64_t* exact, uint64_t* budgeted) {
+    if (!h || !exact || !budgeted) return WQ_E_INVALID;
+    *exact = h->shard ? h->shard->n_exact : 0;
+    *budgeted = h->shard ? h->shard->n_budget : 0;
     return WQ_OK;
 }
 

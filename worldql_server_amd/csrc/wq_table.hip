@@ -289,6 +289,7 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops, bool on_de
     // upload below overwrites it)
     int rc = table_resolve(h, true);
     if (rc) return rc;
+    h->table_gen++;
     if (on_device) {
         h->cur_ops = ops;
     } else {
@@ -407,6 +408,7 @@ int table_remove_peers(wq_router* h, const uint64_t* keys, size_t n_rm) {
     // one in-place pass over every cube's list (wq_delta.hip); the state and any-keys go stale
     if (int rc = table_resolve(h, true)) return rc;
     if (n_rm == 0 || (h->st.n == 0 && !h->dstat_pending)) return WQ_OK;
+    h->table_gen++;
     return table_remove_peers_inplace(h, keys, n_rm);
 }
 

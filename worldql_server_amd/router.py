@@ -54,6 +54,10 @@ def load_library(build_if_missing: bool = True):
         "wq_router_create": ([u16, i32, ctypes.POINTER(vp)], i32),
         "wq_router_create_multi": ([u16, i32, vp, ctypes.POINTER(vp)], i32),
         "wq_multi_info": ([vp, ctypes.POINTER(u32)], i32),
+        "wq_router_create_multi_mode": ([u16, i32, vp, i32, ctypes.POINTER(vp)], i32),
+        "wq_multi_mode": ([vp, ctypes.POINTER(i32)], i32),
+        "wq_route_tick_slices_device": ([vp, vp, i32, vp], i32),
+        "wq_shard_tick_stats": ([vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], i32),
         "wq_router_destroy": ([vp], i32),
         "wq_last_error": ([vp], ctypes.c_char_p),
         "wq_set_stream": ([vp, vp], i32),
@@ -179,14 +183,16 @@ class Router:
             self._check(self.lib.wq_debug_set_hash_bits(self.h, hash_bits))
 
     @classmethod
-    def multi(cls, cube_size: int = 16, devices=(0,)) -> "Router":
-        """One handle over len(devices) GPUs (wq_router_create_multi): the same API, the one-table
-        result, the table sharded by cube hash over the devices (they may repeat)."""
+    def multi(cls, cube_size: int = 16, devices=(0,), mode: str = "cube") -> "Router":
+        """One handle over len(devices) GPUs (wq_router_create_multi_mode): the same API, the one-table
+        result; mode "cube" = the table sharded by cube hash over the devices (they may repeat),
+        "replicate" = every device holds the whole table and routes its own slice."""
         self = cls.__new__(cls)
         self.lib = load_library()
         devs = (ctypes.c_int * len(devices))(*devices)
         h = ctypes.c_void_p()
-        rc = self.lib.wq_router_create_multi(cube_size, len(devices), devs, ctypes.byref(h))
+        m = {"cube": abi.MULTI_CUBE_HASH, "replicate": abi.MULTI_REPLICATE}[mode]
+        rc = self.lib.wq_router_create_multi_mode(cube_size, len(devices), devs, m, ctypes.byref(h))
         if rc != 0:
             raise WQError(rc, self.lib.wq_last_error(None).decode())
         self.h = h
@@ -198,6 +204,31 @@ class Router:
         n = ctypes.c_uint32()
         self._check(self.lib.wq_multi_info(self.h, ctypes.byref(n)))
         return n.value
+
+    def multi_mode(self) -> int:
+        m = ctypes.c_int()
+        self._check(self.lib.wq_multi_mode(self.h, ctypes.byref(m)))
+        return m.value
+
+    def route_slices_device(self, slices, with_msgs: bool = False):
+        """wq_route_tick_slices_device: slices = one (pos_ptr, world_ptr, sender_ptr, repl_ptr, n_msgs
+        [, keys_ptr]) per device of the handle, on that device. Returns a list of abi.SliceView (device
+        pointers into the handle's workspace, valid until its next call)."""
+        G = len(slices)
+        ins = (abi.MsgSlice * G)()
+        for g, sl in enumerate(slices):
+            pos, wo, se, rp, n = sl[:5]
+            keys = sl[5] if len(sl) > 5 else None
+            ins[g] = abi.MsgSlice(None if keys else (pos or None), keys or None, wo or None, se or None, rp or None, n)
+        outs = (abi.SliceView * G)()
+        self._check(self.lib.wq_route_tick_slices_device(self.h, ins, int(with_msgs), outs))
+        return [outs[g] for g in range(G)]
+
+    def shard_tick_stats(self):
+        """(exact, budgeted) slot ticks run on this shard (wq_shard_tick_stats)."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self.lib.wq_shard_tick_stats(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     def _check(self, rc: int):
         if rc != 0:
