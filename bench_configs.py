@@ -358,7 +358,7 @@ def _c3_replicated(a, w, rank, world_size, local_rank, dev, stream, sl):
     t_ms = timed_ticks(lambda: r.route_device(*args, 0), a.steps, stream, dev, world_size, [r])
     r.close()
     t_max_ms, pairs_all = reduce_over_ranks(t_ms, P, dev, world_size)
-    B_all, _ = reduce_over_ranks(0.0, algorithmic_bytes(M, F, P), dev, world_size)
+    _, B_all = reduce_over_ranks(0.0, algorithmic_bytes(M, F, P), dev, world_size)
     del peers, msgs
     return {"t_max_ms": t_max_ms, "pairs_all": int(pairs_all), "B_all": int(B_all), "build_s": build_s,
             "P_rank": P, "M_rank": M}

@@ -3,6 +3,7 @@
 //   sanitize (worldql_server/src/utils/world_names.rs:127-171).
 // Built and run by tests/test_cpp_mirror.py (the run needs a gfx950 GPU; exit code 0 = pass).
 #include <cstdio>
+#include <exception>
 #include <cstdlib>
 #include <memory>
 #include <string>
@@ -192,6 +193,12 @@ static void slices_route(const std::vector<int>& devs) {
     size_t bad = 0, pairs = 0;
     for (size_t g = 0; g < G; ++g) {
         CHECK(v[g].device == devs[g] && v[g].n_msgs == per);
+        if (v[g].n_pairs > 64 * per) {
+            std::fprintf(stderr, "slice %zu: n_msgs %llu n_pairs %llu\n", g, (unsigned long long)v[g].n_msgs,
+                         (unsigned long long)v[g].n_pairs);
+            ++g_fail;
+            return;
+        }
         std::vector<uint32_t> offs(per + 1), peers(v[g].n_pairs);
         CHECK(hipSetDevice(v[g].device) == hipSuccess);
         CHECK(hipMemcpy(offs.data(), v[g].offsets, (per + 1) * 4, hipMemcpyDeviceToHost) == hipSuccess);
@@ -256,10 +263,19 @@ int main(int argc, char** argv) {
         g_mode = mode;
         for (const auto& devs : configs) {
             if (mode == WQ_MULTI_REPLICATE && devs.empty()) continue;  // ran once already
-            area_subscriptions(devs);
-            world_subscriptions(devs);
-            multi_route(devs);
-            slices_route(devs);
+            const char* step = "area_subscriptions";
+            try {
+                area_subscriptions(devs);
+                step = "world_subscriptions";
+                world_subscriptions(devs);
+                step = "multi_route";
+                multi_route(devs);
+                step = "slices_route";
+                slices_route(devs);
+            } catch (const std::exception& e) {
+                std::fprintf(stderr, "FAIL mode %d, %zu devices, %s: %s\n", mode, devs.size(), step, e.what());
+                ++g_fail;
+            }
         }
     }
     std::printf(g_fail ? "FAILED (%d)\n" : "ok\n", g_fail);

@@ -147,7 +147,7 @@ class _DevWords:
     """32-bit words at a device address, for torch.as_tensor (__cuda_array_interface__)."""
 
     def __init__(self, ptr, n):
-        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i4", "data": (ptr, True), "version": 3}
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i4", "data": (ptr, False), "version": 3}
 
 
 def _view_arrays(v):

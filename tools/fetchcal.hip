@@ -75,6 +75,19 @@ __global__ void line_rd(const uint4* __restrict__ a, uint64_t n_lanes, uint32_t*
     if (acc == 0x9e3779b9u) sink[0] = acc;
 }
 
+// per lane: the first 32 B of a random line, then — after that load has returned — bytes 64-95 of
+// the same line: a hit in L2 (TCC_HIT) iff the first request brought the whole 128-B line in
+__global__ void halves_rd(const uint4* __restrict__ a, uint64_t n_lanes, uint32_t* __restrict__ sink) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_lanes) return;
+    const uint64_t line = mix(i * 0x9E3779B97F4A7C15ull + 1) % kLines;
+    const uint4 v0 = a[line * 8], v1 = a[line * 8 + 1];
+    const uint64_t dep = (v0.x ^ v1.y) == 0x9e3779b9u ? 1 : 0;  // the address waits for the data
+    const uint4 w0 = a[(line + dep) * 8 + 4], w1 = a[(line + dep) * 8 + 5];
+    const uint32_t acc = v0.x ^ v1.y ^ w0.z ^ w1.w;
+    if (acc == 0x9e3779b9u) sink[0] = acc;
+}
+
 __global__ void run_rd(const uint32_t* __restrict__ a, uint64_t n_waves, uint32_t* __restrict__ sink) {
     const uint64_t w = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     if (w >= n_waves) return;
@@ -150,6 +163,7 @@ int main(int argc, char** argv) {
         {"line64_rd", 0, n_rand, 64.0 * n_rand},
         {"line128_rd", 0, n_rand, 128.0 * n_rand},
         {"run_rd", 1, n_runs, 256.0 * n_runs},
+        {"halves_rd", 0, n_rand, 64.0 * n_rand},
         {"word4_rd", 2, n_rand, 4.0 * n_rand},
         {"stream16_wr", -1, kBytes / 16, (double)kBytes},
         {"stream4_wr", -1, kBytes / 4, (double)kBytes},
@@ -167,9 +181,10 @@ int main(int argc, char** argv) {
                 case 3: hipLaunchKernelGGL(line_rd<4>, dim3((unsigned)(s.units / 256)), dim3(256), 0, 0, (const uint4*)buf, s.units, sink); break;
                 case 4: hipLaunchKernelGGL(line_rd<8>, dim3((unsigned)(s.units / 256)), dim3(256), 0, 0, (const uint4*)buf, s.units, sink); break;
                 case 5: hipLaunchKernelGGL(run_rd, dim3((unsigned)(s.units * 64 / 256)), dim3(256), 0, 0, (const uint32_t*)buf, s.units, sink); break;
-                case 6: hipLaunchKernelGGL(word4_rd, dim3((unsigned)(s.units / 256)), dim3(256), 0, 0, (const uint32_t*)buf, s.units, sink); break;
-                case 7: hipLaunchKernelGGL(stream16_wr, dim3(grid_stream), dim3(256), 0, 0, (uint4*)buf, s.units); break;
-                case 8: hipLaunchKernelGGL(stream4_wr, dim3(grid_stream), dim3(256), 0, 0, (uint32_t*)buf, s.units); break;
+                case 6: hipLaunchKernelGGL(halves_rd, dim3((unsigned)(s.units / 256)), dim3(256), 0, 0, (const uint4*)buf, s.units, sink); break;
+                case 7: hipLaunchKernelGGL(word4_rd, dim3((unsigned)(s.units / 256)), dim3(256), 0, 0, (const uint32_t*)buf, s.units, sink); break;
+                case 8: hipLaunchKernelGGL(stream16_wr, dim3(grid_stream), dim3(256), 0, 0, (uint4*)buf, s.units); break;
+                case 9: hipLaunchKernelGGL(stream4_wr, dim3(grid_stream), dim3(256), 0, 0, (uint32_t*)buf, s.units); break;
             }
             CHECK(hipGetLastError());
             CHECK(hipEventRecord(e1));

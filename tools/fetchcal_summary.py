@@ -38,16 +38,21 @@ def main():
             r["write_over_requested"] = r["WRITE_SIZE"] * 1024 / req
         if "TCC_EA0_RDREQ_sum" in r:
             r["rdreq_per_distinct_line"] = r["TCC_EA0_RDREQ_sum"] / lines
+            r["rdreq_per_unit"] = r["TCC_EA0_RDREQ_sum"] / r["units"]  # per lane access / per run
             r["rdreq_32B_share"] = r.get("TCC_EA0_RDREQ_32B_sum", 0.0) / max(r["TCC_EA0_RDREQ_sum"], 1.0)
+        if "FETCH_SIZE" in r:
+            r["fetch_per_unit"] = r["FETCH_SIZE"] * 1024 / r["units"]
+        if "TCC_HIT_sum" in r:
+            r["tcc_hit_per_unit"] = r["TCC_HIT_sum"] / r["units"]
     doc = {"source": "tools/fetchcal.hip + tools/fetchcal.sh (rocprofv3 --pmc, one group per pass), buffer "
                      f"{plain['buffer_bytes']} B", "shapes": list(rows.values())}
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
     for r in rows.values():
         print(f"{r['shape']:12s} req {r['requested_bytes']:.3g} B  fetch/req {r.get('fetch_over_requested', float('nan')):.3f}"
-              f"  fetch/line {r.get('fetch_per_distinct_line', float('nan')):.1f}  rdreq/line "
-              f"{r.get('rdreq_per_distinct_line', float('nan')):.2f}  write/req {r.get('write_over_requested', float('nan')):.3f}"
-              f"  {r['requested_GBps']:.0f} GB/s req")
+              f"  fetch/unit {r.get('fetch_per_unit', float('nan')):.1f}  rdreq/unit "
+              f"{r.get('rdreq_per_unit', float('nan')):.2f}  hit/unit {r.get('tcc_hit_per_unit', float('nan')):.2f}"
+              f"  write/req {r.get('write_over_requested', float('nan')):.3f}  {r['requested_GBps']:.0f} GB/s req")
 
 
 if __name__ == "__main__":

@@ -34,6 +34,10 @@ def main():
     ap.add_argument("--hot-peers", type=int, default=0,
                     help="skew: one extra cube with this many subscribers ...")
     ap.add_argument("--hot-frac", type=float, default=0.0, help="... that this fraction of the messages hit")
+    ap.add_argument("--ticks", type=int, default=0,
+                    help="then time this many slot-form ticks of all G shards on the one GPU (barrier + sync "
+                         "around them): wall / G bounds the mean local work per shard (every shard's kernels "
+                         "and the hub copies share the one GPU)")
     a = ap.parse_args()
     import torch
     from worldql_server_amd import synth_ext
@@ -57,6 +61,8 @@ def main():
     routers = [Router(16, 0) for _ in range(G)]
     res = {"slots": [None] * G, "expanded": [None] * G}
     errors = []
+    bar = threading.Barrier(G)
+    timed = {"t": 0.0}
 
     def body(rank):
         try:
@@ -81,6 +87,23 @@ def main():
                 assert rc == 0, rc
                 sent, recvd = r.shard_last_bytes()
                 res[form][rank] = {"messages": n, "pairs": int(P), "sent_bytes": int(sent), "recv_bytes": int(recvd)}
+            if a.ticks:
+                r.set_shard_form(False)
+                for _ in range(2):  # warm: budgets set
+                    r.sharded_route_device(pos.data_ptr(), wo.data_ptr(), se.data_ptr(), rp.data_ptr(), n,
+                                           offs.data_ptr(), peers.data_ptr(), None, cap)
+                torch.cuda.synchronize(dev)
+                bar.wait()
+                t1 = time.perf_counter()
+                for _ in range(a.ticks):
+                    rc, _ = r.sharded_route_device(pos.data_ptr(), wo.data_ptr(), se.data_ptr(), rp.data_ptr(), n,
+                                                   offs.data_ptr(), peers.data_ptr(), None, cap)
+                    assert rc == 0, rc
+                torch.cuda.synchronize(dev)
+                bar.wait()
+                if rank == 0:
+                    timed["t"] = (time.perf_counter() - t1) / a.ticks
+                res["slots"][rank]["tick_stats"] = r.shard_tick_stats()
         except Exception as e:  # noqa: BLE001
             errors.append(repr(e))
 
@@ -103,6 +126,12 @@ def main():
                      "recv_bytes_per_gpu_mean": float(np.mean(r_)), "recv_bytes_per_gpu_max": int(max(r_)),
                      "per_shard": res[form]}
     out["slots_vs_expanded"] = out["slots"]["sent_bytes_per_gpu_mean"] / out["expanded"]["sent_bytes_per_gpu_mean"]
+    if a.ticks:
+        out["one_gpu_tick_ms"] = timed["t"] * 1e3
+        out["mean_local_work_per_shard_ms_upper"] = timed["t"] * 1e3 / G
+        out["timed_ticks"] = a.ticks
+        out["note_timing"] = ("all G shards' kernels and hub copies run on ONE GPU: the G-shard tick's wall time / G is "
+                              "an upper bound on one shard's local work (pairs max / mean in per_shard)")
     print(json.dumps({k: v for k, v in out.items() if k not in ("slots", "expanded")}))
     print(json.dumps({f: {k: v for k, v in out[f].items() if k != "per_shard"} for f in ("slots", "expanded")}))
     if a.out:

@@ -170,12 +170,15 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
 
     // ---- B: rounds of two 16-byte loads per pending message ----
     const uint4* recs4 = reinterpret_cast<const uint4*>(tv.recs);
+    // probe rounds read the dense headers when the table has them (not FULL: that reads whole lines)
+    const uint4* hdr4 = FULL ? nullptr : tv.hdr;
     uint4 c0[IPT], c1[IPT];
     uint4 pc[IPT][FULL ? 6 : 1];  // FULL: the inline peers (chunks 2-7) ride along in the first round
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
-        c0[i] = recs4[(uint64_t)sl[i] * 8];
-        c1[i] = (DBG & 1) ? c0[i] : recs4[(uint64_t)sl[i] * 8 + 1];
+        const uint4* hp = hdr4 ? hdr4 + (uint64_t)sl[i] * 2 : recs4 + (uint64_t)sl[i] * 8;
+        c0[i] = hp[0];
+        c1[i] = (DBG & 1) ? c0[i] : hp[1];
         if (FULL)
 #pragma unroll
             for (int q = 0; q < 6; ++q) pc[i][q] = recs4[(uint64_t)sl[i] * 8 + 2 + q];
@@ -254,8 +257,9 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
         for (int i = 0; i < IPT; ++i) {
             if (st[i] == kStDone) continue;
             const uint32_t q = st[i] == kStProbe ? 0u : vc[i];  // vc <= 6: chunks q, q+1 <= 7
-            c0[i] = recs4[(uint64_t)sl[i] * 8 + q];
-            c1[i] = recs4[(uint64_t)sl[i] * 8 + q + 1];
+            const uint4* hp = (hdr4 && q == 0) ? hdr4 + (uint64_t)sl[i] * 2 : recs4 + (uint64_t)sl[i] * 8 + q;
+            c0[i] = hp[0];
+            c1[i] = hp[1];
             if (FULL && st[i] == kStProbe)
 #pragma unroll
                 for (int c = 0; c < 6; ++c) pc[i][c] = recs4[(uint64_t)sl[i] * 8 + 2 + c];

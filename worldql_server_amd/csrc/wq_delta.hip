@@ -1393,6 +1393,7 @@ int table_resolve(wq_router* h, bool blocking) {
     }
     h->n_delta_fallbacks++;
     h->table_gen++;
+    h->tab.hdr_ok = false;
     h->cur_ops = pd.ops;
     return table_rebuild_batch(h, pd.n);
 }

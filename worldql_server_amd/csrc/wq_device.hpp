@@ -223,6 +223,9 @@ struct TableView {
     uint32_t n_pbox;            // peers [0, n_pbox) have a box; others hold no record cube
     const uint32_t* pbox_valid; // device word: 0 once an update could not keep the boxes
     const uint32_t* stale;      // device word: non-zero while an incremental batch awaits re-application
+    // dense copy of every record's first 32 bytes (key, count, list offset, signature) at the same
+    // slot index, 4 per 128-B line; nullptr: the count pass probes the records themselves
+    const uint4* hdr = nullptr;
 };
 
 // ---- per-peer boxes: a fast "certainly not subscribed" for long lists ---------------------

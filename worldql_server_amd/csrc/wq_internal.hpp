@@ -70,6 +70,10 @@ struct Table {
     // u32: non-zero while the last incremental batch could not be applied on the device (the
     // next host call re-applies it); route kernels report error bit 8 meanwhile
     DevBuf stale;
+    // dense record headers (TableView::hdr): 32 B per record slot, refreshed by every full build;
+    // off (hdr_ok false) from the first in-place change until the next build
+    DevBuf hdr;
+    bool hdr_ok = false;
 };
 
 // The last incremental batch (wq_delta.hip), in flight: its status and stat deltas arrive in
@@ -197,6 +201,7 @@ inline TableView table_view(const wq_router* h) {
     v.pbox = h->tab.n_pbox ? h->tab.pbox.as<uint32_t>() : nullptr;
     v.pbox_valid = h->tab.n_pbox ? h->tab.pbox.as<uint32_t>() + (uint64_t)kBoxWords * h->tab.n_pbox : nullptr;
     v.stale = h->tab.stale.as<uint32_t>();
+    v.hdr = h->tab.hdr_ok ? h->tab.hdr.as<uint4>() : nullptr;
     return v;
 }
 // Sticky {error OR, overflow OR} words of every route / global call since the last

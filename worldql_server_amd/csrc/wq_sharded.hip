@@ -1395,9 +1395,11 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
         hipLaunchKernelGGL(k_ref_resolve, dim3((unsigned)((Sb + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rv);
         WQ_HIP(h, hipGetLastError());
         // the count pass's per-tile totals held its own rows only
-        hipLaunchKernelGGL(row_tile_sums_kernel, dim3(nt), dim3(kBlock), 0, s, sc.e_msg.as<uint32_t>(), (uint32_t)M,
-                           sc.mtiles.as<uint32_t>());
-        WQ_HIP(h, hipGetLastError());
+        if (M) {
+            hipLaunchKernelGGL(row_tile_sums_kernel, dim3(nt), dim3(kBlock), 0, s, sc.e_msg.as<uint32_t>(),
+                               (uint32_t)M, sc.mtiles.as<uint32_t>());
+            WQ_HIP(h, hipGetLastError());
+        }
     }
     if (!late) {
         sc.last_M = M;

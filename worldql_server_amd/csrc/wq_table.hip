@@ -22,6 +22,7 @@
 
 #include <algorithm>
 
+#include <cstdlib>
 #include "table_prims.hpp"
 
 namespace wq {
@@ -291,6 +292,7 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops, bool on_de
     if (rc) return rc;
     h->table_gen++;
     if (on_device) {
+    h->tab.hdr_ok = false;
         h->cur_ops = ops;
     } else {
         WQ_ALLOC(h, h->d_ops, n_ops * sizeof(wq_op));
@@ -409,7 +411,15 @@ int table_remove_peers(wq_router* h, const uint64_t* keys, size_t n_rm) {
     if (int rc = table_resolve(h, true)) return rc;
     if (n_rm == 0 || (h->st.n == 0 && !h->dstat_pending)) return WQ_OK;
     h->table_gen++;
+    h->tab.hdr_ok = false;
     return table_remove_peers_inplace(h, keys, n_rm);
+}
+
+__global__ void k_hdr_fill(const uint4* __restrict__ recs, uint64_t n, uint4* __restrict__ hdr) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    hdr[2 * i] = recs[8 * i];
+    hdr[2 * i + 1] = recs[8 * i + 1];
 }
 
 // Per-cube lists, slot table and the (world, peer) "any" keys from the sorted state.
@@ -504,6 +514,15 @@ int table_rebuild_derived(wq_router* h) {
                                t.pbox.as<uint32_t>());
             t.n_pbox = (uint32_t)cap;
         }
+    }
+    // dense headers (WQ_HDR=1, experiment): the records' first 32 bytes at the same slot index
+    t.hdr_ok = false;
+    static const bool want_hdr = getenv("WQ_HDR") && atoi(getenv("WQ_HDR")) != 0;
+    if (want_hdr) {
+        WQ_ALLOC(h, t.hdr, rcap * 32);
+        hipLaunchKernelGGL(k_hdr_fill, dim3(grid_for(rcap)), dim3(kBlock), 0, s, t.recs.as<uint4>(), rcap,
+                           t.hdr.as<uint4>());
+        t.hdr_ok = true;
     }
     t.n_cubes = n_cubes;
     t.n_recs = n_cubes;
