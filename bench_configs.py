@@ -29,7 +29,8 @@ import numpy as np
 import bench
 from bench import HBM_PEAK_GBS, METRIC, algorithmic_bytes, reduce_over_ranks, roofline, timed_ticks
 
-PMC_C3 = "r03_pmc_route_c3.json"  # rocprofv3 --pmc summary of the C3 tick (tools/pmc_route.sh)
+PMC_C3 = "r04_pmc_route_c3.json"  # rocprofv3 --pmc summary of the C3 tick (tools/pmc_route.sh; x2 calibrated:
+                                   # profiles/r04_fetch_calibration.json)
 
 
 def run(a, rank, world_size, local_rank, dev):
@@ -615,7 +616,7 @@ def run_c4(a, rank, world_size, local_rank, dev):
                  "generate_s": round(gen_s, 1)},
                 {"bound": "hbm", "achieved": B / (t_max_ms / steps / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
                  "unit": "GB/s", "frac": B / (t_max_ms / steps / 1e3) / 1e9 / HBM_PEAK_GBS,
-                 "traffic": _pmc_tick_traffic("r02_pmc_c4.json", a.scale) if world_size == 1 else None,
+                 "traffic": _pmc_tick_traffic("r04_pmc_c4.json", a.scale) if world_size == 1 else None,
                  "kernel": "whole tick (incremental update + route); route launch alone below",
                  "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
                 "synthetic (splitmix64, SURVEY.md §8(d) C4 generator)")
@@ -709,7 +710,7 @@ def run_c5(a, rank, world_size, local_rank, dev):
                  "parallelism": "1 GPU", "table_build_s": round(build_s, 3), "generate_s": round(gen_s, 1)},
                 {"bound": "hbm", "achieved": B / (res["t_ms"] / steps / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
                  "unit": "GB/s", "frac": B / (res["t_ms"] / steps / 1e3) / 1e9 / HBM_PEAK_GBS,
-                 "traffic": _pmc_tick_traffic("r03_pmc_c5.json", a.scale),
+                 "traffic": _pmc_tick_traffic("r04_pmc_c5.json", a.scale),
                  "kernel": "whole tick (incremental update + positions + radius route); route launches alone below",
                  "kernel_avg_us": k_avg_s * 1e6, "algorithmic_bytes": B},
                 "synthetic (splitmix64, SURVEY.md §8(d) C5 generator)")

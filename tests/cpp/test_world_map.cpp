@@ -190,22 +190,28 @@ static void slices_route(const std::vector<int>& devs) {
                              static_cast<const uint32_t*>(ds), static_cast<const uint8_t*>(dr), per};
     }
     const std::vector<wq_slice_view> v = wm.route_slices(in);
+    // the views point into the handle's workspace until its next call: copy every slice out first
+    std::vector<std::vector<uint32_t>> all_offs(G), all_peers(G);
+    for (size_t g = 0; g < G; ++g) {
+        CHECK(v[g].device == devs[g] && v[g].n_msgs == per && v[g].n_pairs <= 64 * per);
+        all_offs[g].resize(per + 1);
+        all_peers[g].resize(v[g].n_pairs <= 64 * per ? v[g].n_pairs : 0);
+        CHECK(hipSetDevice(v[g].device) == hipSuccess);
+        CHECK(hipMemcpy(all_offs[g].data(), v[g].offsets, (per + 1) * 4, hipMemcpyDeviceToHost) == hipSuccess);
+        if (!all_peers[g].empty())
+            CHECK(hipMemcpy(all_peers[g].data(), v[g].peers, all_peers[g].size() * 4, hipMemcpyDeviceToHost) ==
+                  hipSuccess);
+        CHECK(all_offs[g][per] == all_peers[g].size());
+    }
     size_t bad = 0, pairs = 0;
     for (size_t g = 0; g < G; ++g) {
-        CHECK(v[g].device == devs[g] && v[g].n_msgs == per);
-        if (v[g].n_pairs > 64 * per) {
-            std::fprintf(stderr, "slice %zu: n_msgs %llu n_pairs %llu\n", g, (unsigned long long)v[g].n_msgs,
-                         (unsigned long long)v[g].n_pairs);
-            ++g_fail;
-            return;
-        }
-        std::vector<uint32_t> offs(per + 1), peers(v[g].n_pairs);
-        CHECK(hipSetDevice(v[g].device) == hipSuccess);
-        CHECK(hipMemcpy(offs.data(), v[g].offsets, (per + 1) * 4, hipMemcpyDeviceToHost) == hipSuccess);
-        if (!peers.empty())
-            CHECK(hipMemcpy(peers.data(), v[g].peers, peers.size() * 4, hipMemcpyDeviceToHost) == hipSuccess);
-        CHECK(offs[per] == v[g].n_pairs);
+        const std::vector<uint32_t>& offs = all_offs[g];
+        const std::vector<uint32_t>& peers = all_peers[g];
         for (size_t i = 0; i < per && bad < 5; ++i) {
+            if (offs[i] > offs[i + 1] || offs[i + 1] > peers.size()) {
+                ++bad;
+                continue;
+            }
             std::vector<uint32_t> want;
             for (uint32_t p : map.get_subscribed_peers(Vector3{pos[g][3 * i], pos[g][3 * i + 1], pos[g][3 * i + 2]})) {
                 const bool keep = repl[g][i] == WQ_REPL_INCLUDING_SELF ? true
