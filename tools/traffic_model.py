@@ -54,7 +54,8 @@ def load(name: str):
 
 def main():
     out = {}
-    for name, ex in (("r02_pmc_route.json", ""), ("r04_pmc_route_c3.json", "tick_kernel")):
+    for name, ex in (("r02_pmc_route.json", ""), ("r04_pmc_route_c3.json", "tick_kernel"),
+                     ("r04_pmc_route_c3_hdr.json", "tick_kernel")):
         d = load(name)
         if d:
             out[name] = route_tick_traffic(d, ex)

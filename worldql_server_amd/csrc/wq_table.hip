@@ -291,8 +291,8 @@ int table_apply_segment(wq_router* h, const wq_op* ops, size_t n_ops, bool on_de
     int rc = table_resolve(h, true);
     if (rc) return rc;
     h->table_gen++;
+    h->tab.hdr_ok = false;  // an in-place batch leaves the dense headers behind; a rebuild refills them
     if (on_device) {
-    h->tab.hdr_ok = false;
         h->cur_ops = ops;
     } else {
         WQ_ALLOC(h, h->d_ops, n_ops * sizeof(wq_op));
