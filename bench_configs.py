@@ -7,8 +7,9 @@ the timed region; a tick's timed work is everything the tick does on the GPU.
   c1  the reference's CPU-sized case (1k peers, 10k messages): GPU tick beside cpu_ref_1t and
       cpu_server_faithful_1t (the broadcast_to scan).
   c3  1M peers x 3x3x3 (S = 27M), 10M messages/tick, 90% from 256 Zipf-weighted Gaussian hotspots.
-      N = 1: the whole configuration on one GPU. N > 1: strong scaling through the cube-hash sharded
-      path (worldql_server_amd/sharded.py; every rank ingests M/N messages, RCCL all-to-all).
+      N = 1: the whole configuration on one GPU. N > 1: strong scaling, every rank routes M/N
+      messages — headline the replicated table (no exchange), beside it the cube-hash sharded tick
+      over RCCL (extra.cube_hash; --shard cube makes it the headline).
   c4  8 worlds x 50k peers per GPU (weak scaling; 8 GPUs = the 64 worlds of C4, world-sharded, no
       message exchange). A tick = that tick's AreaUnsubscribe/AreaSubscribe churn (5% of peers move
       by N(0,16)^3) applied incrementally on the device (wq_apply_ops_device), then one message per
@@ -22,6 +23,7 @@ from __future__ import annotations
 
 import json
 import os
+import sys
 import time
 
 import numpy as np
@@ -493,10 +495,23 @@ def _run_c3_multi(a, w, rank, world_size, local_rank, dev, gen_s):
             dog = threading.Timer(300.0, bail)
             dog.daemon = True
             dog.start()
-        if f == "replicate":
-            res[f] = _c3_replicated(a, w, rank, world_size, local_rank, dev, stream, sl)
-        else:
-            res[f] = _c3_cube(a, w, rank, world_size, local_rank, dev, stream, sl, owner_form=not a.no_extra)
+        try:
+            if f == "replicate":
+                res[f] = _c3_replicated(a, w, rank, world_size, local_rank, dev, stream, sl)
+            else:
+                res[f] = _c3_cube(a, w, rank, world_size, local_rank, dev, stream, sl, owner_form=not a.no_extra)
+        except Exception as e:  # noqa: BLE001
+            if i == 0:
+                raise
+            # the second form failed on this rank: its peers may be inside a collective that will never
+            # complete, so this rank reports (rank 0: the headline line, the error under extra) and
+            # leaves; a peer still waiting leaves through its own watchdog
+            print(f"rank {rank}: {f} form failed: {e!r}", file=sys.stderr, flush=True)
+            if rank == 0:
+                out = line()
+                out.setdefault("extra", {})["cube_hash" if f == "cube" else "replicated_table"] = {"error": repr(e)}
+                print(json.dumps(out), flush=True)
+            os._exit(0)
         if dog:
             dog.cancel()
     if "replicate" in res and "cube" in res:
