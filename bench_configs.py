@@ -492,7 +492,7 @@ def _run_c3_multi(a, w, rank, world_size, local_rank, dev, gen_s):
                 if rank == 0:
                     print(json.dumps(line()), flush=True)
                 os._exit(0)
-            dog = threading.Timer(300.0, bail)
+            dog = threading.Timer(120.0, bail)  # the cube form takes ~10 s when it works
             dog.daemon = True
             dog.start()
         try:
