@@ -345,20 +345,22 @@ int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_
                                  size_t n_msgs, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs,
                                  size_t capacity, size_t* n_pairs);
 int wq_sharded_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity);
-/* What crosses between GPUs in a sharded tick (radius filter off): each message as one 20-byte slot
- * to its owner (two for a key without a packed form), and back a 12-byte row reference per slot plus,
- * per (owner, ingesting shard), ONE copy of every cube list those messages hit — not the expanded
- * (message, peer) pairs (C3: a hotspot list of ~500 peers is hit by thousands of messages a tick).
- * The ingesting GPU expands the rows itself. With the radius filter on, every message's surviving
- * peers differ, so the pairs return expanded (4 bytes per pair).
+/* What crosses between GPUs in a sharded tick: each message as one 20-byte slot to its owner (two
+ * for a key without a packed form), and back a 12-byte row reference per slot plus, per (owner,
+ * ingesting shard), ONE copy of every cube list those messages hit — not the expanded (message,
+ * peer) pairs (C3: a hotspot list of ~500 peers is hit by thousands of messages a tick). The
+ * ingesting GPU expands the rows itself; with the radius filter on it also filters them there, where
+ * the message positions are (every shard holds every peer position), so a hot cube costs its owner
+ * one list copy per ingesting shard, however many messages hit it.
  * wq_shard_last_bytes: bytes this shard sent to / received from OTHER shards in its latest sharded
  * tick (the xGMI volume; the self segment is not counted). */
 int wq_shard_last_bytes(wq_router* h, uint64_t* sent, uint64_t* received);
 /* Slot ticks run exactly (the sizes read back twice: the first tick, or a redo after a tick outgrew
  * its budgets) and on budgets (one host read per tick, at its end), on this shard so far. */
 int wq_shard_tick_stats(wq_router* h, uint64_t* exact, uint64_t* budgeted);
-/* Test / tuning hook: 1 = the sharded tick returns expanded pairs even with the radius filter off
- * (the earlier form), 0 = row references and pools (default). Results are identical. */
+/* Test / tuning hook: 1 = the sharded tick sends 40-byte records and returns expanded pairs (the
+ * earlier form; the owner filters by radius), 0 = slots, row references and pools (default).
+ * Results are identical. */
 int wq_debug_set_shard_form(wq_router* h, int expanded);
 /* Test hook: the next sharded tick on this handle fails locally at step 1 (grouping its messages)
  * or 3 (routing what it owns) with WQ_E_INVALID, as a real local failure would: it still completes

@@ -52,6 +52,40 @@ def test_c5_radius_scaled_vs_oracle():
     _same(r.route(pos, w, s, rp), o.route(pos, w, s, rp))
 
 
+def test_radius_unknown_replication_codes():
+    """Every replication code, unknown ones included (replication.rs:34-43: ExceptSelf), through the
+    radius filter's inline-mask and long-list paths. Codes >= 3 once lost their recipients in the
+    inline path (a miscompiled switch in repl_keeps, route_emit.hpp)."""
+    c5 = synth_ext.config_c5(scale=0.004)
+    ops = c5.initial_ops()
+    r, o = mk_router(), orc.COracle(16)
+    r.apply_ops(ops)
+    o.apply_ops(ops)
+    # a dense cluster on top: lists longer than the 24 inline peers
+    rng = np.random.default_rng(5)
+    n0 = len(c5.pos)
+    centre = rng.normal(0.0, 6.0, (200, 3))
+    nb = np.array([[dx, dy, dz] for dx in (-1, 0, 1) for dy in (-1, 0, 1) for dz in (-1, 0, 1)], np.float64)
+    sub = (centre[:, None, :] + 16.0 * nb[None]).reshape(-1, 3)
+    extra = abi.ops_array(np.zeros(len(sub), np.uint32), np.repeat(np.arange(n0, n0 + 200, dtype=np.uint32), 27),
+                          np.zeros(len(sub), np.uint8), pos=sub)
+    r.apply_ops(extra)
+    o.apply_ops(extra)
+    pp = np.concatenate([c5.pos, centre + rng.uniform(-4.0, 4.0, centre.shape)])
+    r.set_peer_positions(pp)
+    r.set_radius(c5.radius)
+    pos, w, s, _ = c5.messages()
+    M = len(w)
+    pos = np.concatenate([pos, centre[rng.integers(0, 200, 2000)] + rng.uniform(-8, 8, (2000, 3))])
+    s = np.concatenate([s, rng.integers(0, n0 + 200, 2000).astype(np.uint32)])
+    w = np.zeros(len(s), np.uint32)
+    for codes in ((0, 1, 2, 3), (3, 4, 255)):
+        rp = np.array(codes, np.uint8)[rng.integers(0, len(codes), len(s))]
+        P = _same(r.route(pos, w, s, rp), o.route_radius(pos, w, s, rp, pp, c5.radius))
+        assert P > 0
+    assert M > 0
+
+
 def test_radius_boundary_long_lists_and_missing_positions():
     r, o = mk_router(), orc.COracle(16)
     rng = synth.SplitMix64(99)

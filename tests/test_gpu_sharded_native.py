@@ -592,3 +592,83 @@ def test_copy_out_after_a_table_change_is_refused():
     for r in routers:
         r.close()
     hub.close()
+
+
+def _radius_workload(seed=21):
+    """Peers around their subscription centres (positions jittered off them), most in a sparse box
+    (cube lists of a few peers: rows short enough for a survivor mask) plus a dense cluster (lists
+    longer than a record's 24 inline peers: rows re-filtered from the pool), mixed replication."""
+    rng = np.random.default_rng(seed)
+    sparse = rng.uniform(-200.0, 200.0, (2500, 3))
+    dense = rng.normal(0.0, 10.0, (500, 3))
+    centre = np.concatenate([sparse, dense])
+    n = len(centre)
+    nb = np.array([[dx, dy, dz] for dx in (-1, 0, 1) for dy in (-1, 0, 1) for dz in (-1, 0, 1)], np.float64)
+    sub = (centre[:, None, :] + 16.0 * nb[None]).reshape(-1, 3)
+    ops = abi.ops_array(np.zeros(len(sub), np.uint32), np.repeat(np.arange(n, dtype=np.uint32), 27),
+                        np.zeros(len(sub), np.uint8), pos=sub)
+    peer_pos = centre + rng.uniform(-6.0, 6.0, centre.shape)
+    M = 12000
+    src = rng.integers(0, n, M)
+    mpos = centre[src] + rng.uniform(-12.0, 12.0, (M, 3))
+    sender = rng.integers(0, n, M).astype(np.uint32)
+    sender[: M // 3] = src[: M // 3]  # a third sent by a peer subscribed where it speaks
+    repl = rng.integers(0, 4, M).astype(np.uint8)  # 3: an unknown code (ExceptSelf)
+    un = ops[rng.choice(len(ops), 3000, replace=False)].copy()
+    un["kind"] = abi.OP_UNSUBSCRIBE
+    return ops, un, peer_pos, mpos, np.zeros(M, np.uint32), sender, repl
+
+
+@pytest.mark.parametrize("G,form", [(1, "slots"), (2, "slots"), (3, "slots"), (2, "expanded")])
+def test_hub_radius_ticks_vs_whole_table_oracle(G, form):
+    """The radius filter through the sharded tick (C5 over G GPUs): the slot form filters the pool
+    rows on the ingesting GPU (short rows as survivor masks, long ones re-filtered by the emit) and
+    its own cubes with count_radius_kernel; both forms against the whole-table oracle, per message."""
+    import torch
+    from worldql_server_amd.router import Hub, Router
+    ops, churn, peer_pos, mpos, world, sender, repl = _radius_workload()
+    radius = 14.0
+    M = len(world)
+    w = type("W", (), {"pos": mpos, "world": world, "sender": sender, "repl": repl, "cube_size": 16})
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    results, errors = [None] * G, []
+
+    def body(rank):
+        try:
+            r = routers[rank]
+            r.attach_hub(hub, rank)
+            r.set_shard_form(form == "expanded")
+            r.set_peer_positions(peer_pos)
+            r.set_radius(radius)
+            lo, hi = _slice(M, G, rank)
+            r.sharded_apply_ops(ops)
+            first = _tick(r, w, lo, hi, dev, cap=5)  # too small: WQ_E_CAPACITY, then copy_out
+            r.sharded_apply_ops(churn)
+            second = _tick(r, w, lo, hi, dev)
+            results[rank] = (first, second)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=body, args=(k,)) for k in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    assert not errors, errors
+    o = orc.COracle(16)
+    o.apply_ops(ops)
+    want1 = o.route_radius(mpos, world, sender, repl, peer_pos, radius)[:2]
+    o.apply_ops(churn)
+    want2 = o.route_radius(mpos, world, sender, repl, peer_pos, radius)[:2]
+    lens = np.diff(want1[0].astype(np.int64))
+    assert lens.max() > 24 and (lens[lens > 0] <= 24).mean() > 0.3  # both row kinds occur
+    for rank in range(G):
+        lo, hi = _slice(M, G, rank)
+        for got, (wo_, wp_) in zip(results[rank], (want1, want2)):
+            want = (wo_[lo:hi + 1] - wo_[lo], wp_[wo_[lo]:wo_[hi]])
+            _check(got, want, hi - lo)
+    for r in routers:
+        r.close()
+    hub.close()

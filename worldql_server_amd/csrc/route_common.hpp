@@ -103,5 +103,8 @@ struct RouteIn {
 // info.x of a row the sharded tick's owner shipped back: word offset into the received cube-list
 // pool (both locator flags set; only ever decoded when EmitParams::pool is set)
 constexpr uint32_t kLocPool = 0xC0000000u;
+// ... with the radius filter on: info.y of a pool row of <= kInline peers = kPoolShort | length << 24 |
+// survivor mask (emit_row_img stages it like an inline record); a longer row's info.y is its length
+constexpr uint32_t kPoolShort = 0x80000000u;
 
 }  // namespace wq

@@ -56,10 +56,17 @@ struct EmitOut {
     uint64_t capacity;
     const double* pos;     // message positions (radius mode)
     const uint8_t* repl;   // replication codes (radius mode)
+    const uint32_t* pool = nullptr;  // radius mode in the sharded tick: rows with kLocPool read here
 };
 
+// Replication filter for one candidate (local_message.rs:60-86; replication.rs:34-43: every unknown
+// code is ExceptSelf). Branch-free on purpose: written as nested selects, it was lowered to a switch
+// whose unknown-code leaf inside count_radius_kernel's unrolled inline loop tested the radius
+// against a stale register instead of the peer (codes >= 3 lost their recipients; ROCm 7.2 clang,
+// gfx950) — tests/test_gpu_c345.py::test_radius_unknown_replication_codes.
 __device__ __forceinline__ bool repl_keeps(uint8_t rp, uint32_t peer, uint32_t me) {
-    return rp == WQ_REPL_INCLUDING_SELF ? true : rp == WQ_REPL_ONLY_SELF ? (peer == me) : (peer != me);
+    const bool including = rp == WQ_REPL_INCLUDING_SELF, only = rp == WQ_REPL_ONLY_SELF;
+    return including | (only == (peer == me));
 }
 
 // Row-local exclusive scan of e over the block's 256 threads; returns this thread's start and
@@ -94,6 +101,8 @@ __device__ __forceinline__ uint32_t row_scan(uint32_t e, uint32_t* wave_tot, uin
 //     is re-filtered chunk by chunk with a block-wide compaction;
 //   OnlySelf: the sender, by its own lane.
 // Every thread of the block must call it (it contains barriers); it ends with a barrier.
+constexpr uint32_t kSlPool = 0x80000000u;  // emit_row_img, radius mode: sl is a pool word offset
+
 template <int STAGE, int U = 8, bool RADIUS = false>
 __device__ __forceinline__ void emit_row_img(uint32_t* op, uint8_t* om, EmitQueue& q_, const TableView& tv, const EmitOut& o, uint32_t m0,
                                          uint32_t e, uint2 inf, uint32_t st, uint64_t g0, uint32_t T) {
@@ -102,13 +111,21 @@ __device__ __forceinline__ void emit_row_img(uint32_t* op, uint8_t* om, EmitQueu
     if (tid == 0) q_.n_gq = 0;
     lds_barrier();
     uint32_t sl = kNone, cnt = 0, skip = kNone;  // radius mode: skip holds the survivor mask
-    const bool self = !RADIUS && e && (inf.x & kLocSelf);
+    // OnlySelf rows; in radius mode only the sharded tick's (count_radius folds OnlySelf into masks)
+    const bool self = e && (RADIUS ? (inf.x & kLocPool) == kLocSelf : (inf.x & kLocSelf) != 0);
     const uint32_t self_peer = self ? o.sender[m0 + tid] : 0u;
     if (e && !self) {
-        if (inf.x & kLocGlobal) {
+        // radius mode: a row of the sharded tick's received pools (kLocPool | word offset): a short one
+        // is staged like an inline record (sl = kSlPool | offset), a longer one re-filtered from the pool
+        const bool from_pool = RADIUS && (inf.x & kLocPool) == kLocPool;
+        if (from_pool && (inf.y & kPoolShort)) {
+            sl = kSlPool | (inf.x & ~kLocPool);
+            cnt = (inf.y >> 24) & 0x1Fu;
+            skip = inf.y & kSkipNone24;
+        } else if (inf.x & kLocGlobal) {
             const uint32_t q = atomicAdd(&q_.n_gq, 1u);
-            q_.gq_j[q] = tid;
-            q_.gq_off[q] = (inf.x & ~kLocGlobal) + 1;
+            q_.gq_j[q] = tid | (from_pool ? 0x100u : 0u);
+            q_.gq_off[q] = from_pool ? (inf.x & ~kLocPool) : (inf.x & ~kLocGlobal) + 1;
             q_.gq_skip[q] = inf.y;
             q_.gq_e[q] = e;
             q_.gq_st[q] = st;
@@ -146,8 +163,18 @@ __device__ __forceinline__ void emit_row_img(uint32_t* op, uint8_t* om, EmitQueu
                 q_cnt[u] = __shfl(cnt, src, 64);
                 q_skip[u] = __shfl(skip, src, 64);
                 q_st[u] = __shfl(st, src, 64);
-                if (part < 6 && qs != kNone && 4u * part < q_cnt[u]) v[u] = recs4[(uint64_t)qs * 8 + 2 + part];
-                else q_cnt[u] = 0;  // nothing to stage from this lane
+                if (part < 6 && qs != kNone && 4u * part < q_cnt[u]) {
+                    if (RADIUS && (qs & kSlPool)) {  // a short pool row: its words, none past its end
+                        const uint32_t* pw = o.pool + (qs & ~kSlPool) + 4u * part;
+                        const uint32_t i0 = 4u * part;
+                        v[u] = make_uint4(pw[0], i0 + 1 < q_cnt[u] ? pw[1] : 0u, i0 + 2 < q_cnt[u] ? pw[2] : 0u,
+                                          i0 + 3 < q_cnt[u] ? pw[3] : 0u);
+                    } else {
+                        v[u] = recs4[(uint64_t)qs * 8 + 2 + part];
+                    }
+                } else {
+                    q_cnt[u] = 0;  // nothing to stage from this lane
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -176,16 +203,17 @@ __device__ __forceinline__ void emit_row_img(uint32_t* op, uint8_t* om, EmitQueu
             if (RADIUS) {
                 // re-filter each long list chunk by chunk, compacting survivors block-wide
                 for (uint32_t q = 0; q < n_gq; ++q) {
-                    const uint32_t j = q_.gq_j[q], s0 = lead + q_.gq_st[q], ej = q_.gq_e[q];
+                    const uint32_t jq = q_.gq_j[q], j = jq & 0xFFu, s0 = lead + q_.gq_st[q], ej = q_.gq_e[q];
                     if (s0 >= w1 || s0 + ej <= w0) continue;  // block-uniform
                     const uint32_t off = q_.gq_off[q], len = q_.gq_skip[q];
+                    const uint32_t* src = (jq & 0x100u) ? o.pool : tv.list;
                     const uint32_t m = m0 + j, me = o.sender[m];
                     const uint8_t rp = o.repl[m];
                     const double mx = o.pos[3ull * m], my = o.pos[3ull * m + 1], mz = o.pos[3ull * m + 2];
                     uint32_t run = 0;
                     for (uint32_t b = 0; b < len; b += kBlock) {
                         const uint32_t i = b + tid;
-                        const uint32_t peer = i < len ? tv.list[off + i] : 0u;
+                        const uint32_t peer = i < len ? src[off + i] : 0u;
                         const bool ok = i < len && repl_keeps(rp, peer, me) && within_radius(tv, mx, my, mz, peer);
                         uint32_t tot;
                         const uint32_t at = row_scan(ok ? 1u : 0u, q_.scan_tot, &tot);
@@ -391,12 +419,12 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(EmitParams p) {
     if (m < p.M) p.offsets[m] = g + st;
     if (!p.peers) return;  // counts-only call: offsets are all that is asked for
     if (!RADIUS && T > (uint32_t)STAGE) {  // block-uniform: heavy fan-out, no windows
-        direct_meta(sm, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl}, m, e, inf, st);
+        direct_meta(sm, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl, p.pool}, m, e, inf, st);
         lds_barrier();
-        emit_direct<16>(sm, p.t, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl}, m0, g, T);
+        emit_direct<16>(sm, p.t, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl, p.pool}, m0, g, T);
         return;
     }
-    emit_row<STAGE, U, RADIUS>(sm, p.t, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl}, m0, e, inf,
+    emit_row<STAGE, U, RADIUS>(sm, p.t, EmitOut{p.sender, p.peers, p.msgs, p.capacity, p.pos, p.repl, p.pool}, m0, e, inf,
                                st, g, T);
 }
 

@@ -28,6 +28,9 @@ __device__ __forceinline__ uint32_t count_list_radius(const TableView& tv, const
 }
 
 // Lane per message; one block = one 256-message tile (tile_total per block, count_tile = 256).
+// OWN (the sharded tick's ingesting GPU): only the messages whose cube this shard owns are counted;
+// the others get e = 0 and an empty locator here (their rows come back from their owners).
+template <bool OWN = false>
 __global__ __launch_bounds__(kBlock) void count_radius_kernel(CountParams p) {
     __shared__ uint64_t wave_F[kWaves];
     __shared__ uint64_t wave_E[kWaves];
@@ -40,7 +43,7 @@ __global__ __launch_bounds__(kBlock) void count_radius_kernel(CountParams p) {
         p.cnt_next->error = 0;
     }
     const uint32_t m = blockIdx.x * kBlock + tid;
-    const bool valid = m < p.in.M;
+    bool valid = m < p.in.M;
     const uint32_t mm = valid ? m : 0;
     const double mx = p.in.pos[3ull * mm], my = p.in.pos[3ull * mm + 1], mz = p.in.pos[3ull * mm + 2];
     const uint32_t w = p.in.world[mm], me = p.in.sender[mm];
@@ -51,6 +54,7 @@ __global__ __launch_bounds__(kBlock) void count_radius_kernel(CountParams p) {
     uint64_t pk = 0;
     uint32_t ext = 0;
     const bool reg = pack_key(w, kx, ky, kz, tv.sf, &pk, &ext);
+    if (OWN) valid = valid && shard_of(w, kx, ky, kz, p.in.own_G) == p.in.own_me;
     uint32_t e = 0, cnt = 0;
     uint2 info = make_uint2(0, kNone);
     if (valid && !reg) {  // full-key slot table: the list is walked from `list`
@@ -106,7 +110,7 @@ __global__ __launch_bounds__(kBlock) void count_radius_kernel(CountParams p) {
             info = make_uint2(sl, (cnt << 24) | mask);
         }
     }
-    if (valid) {
+    if (m < p.in.M) {
         p.e[m] = e;
         p.info[m] = info;
     }

@@ -251,7 +251,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     cp.cnt_next = nxt;
     cp.health = route_health(h);
     if (radius)
-        hipLaunchKernelGGL(count_radius_kernel, dim3(n_count), dim3(kBlock), 0, s, cp);
+        hipLaunchKernelGGL(count_radius_kernel<false>, dim3(n_count), dim3(kBlock), 0, s, cp);
     else
         {
         // two count tiles per block (grid stride): C3's 39,063 short blocks turn over less (with

@@ -39,6 +39,7 @@
 #include "route_count.hpp"
 #include "route_emit.hpp"
 #include "route_gather.hpp"
+#include "route_radius.hpp"
 #include "route_scan.hpp"
 
 namespace wq {
@@ -221,6 +222,9 @@ struct ShardCtx {
     bool last_slots = false;  // the latest tick was a slot tick (copy_out = scan + emit of its rows)
     uint64_t last_gen = 0;    // its table generation: its own-cube rows point into the table
     const uint32_t* last_sender = nullptr;  // its d_sender (OnlySelf rows read the sender)
+    const double* last_pos = nullptr;       // radius filter on: its positions and replication codes
+    const uint8_t* last_repl = nullptr;     // (the emit re-filters list and pool rows)
+    bool last_radius = false;
 };
 
 namespace {
@@ -672,8 +676,19 @@ struct ResolveParams {
     uint64_t prb[WQ_MAX_SHARDS + 1];  // pool segment bases (words) in the receive buffer
     uint32_t* e_msg;
     uint2* info_msg;
+    // RADIUS: the pool rows are filtered here, where the message positions and every peer's position
+    // are (the owner has neither the message position nor a reason to need it)
+    const uint32_t* pool = nullptr;
+    const double* pos = nullptr;
+    const uint32_t* sender = nullptr;
+    const uint8_t* repl = nullptr;
+    TableView tv{};
 };
 
+// RADIUS: a pool row keeps its full length (the emit re-filters it, as count_radius_kernel's list
+// rows) and e counts the candidates within the radius that replication keeps; an OnlySelf row the
+// sender, if subscribed and within the radius of its own message.
+template <bool RADIUS>
 __global__ __launch_bounds__(kBlock) void k_ref_resolve(ResolveParams p) {
     const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
     if (k >= p.n) return;
@@ -682,7 +697,12 @@ __global__ __launch_bounds__(kBlock) void k_ref_resolve(ResolveParams p) {
     const uint3 ref = p.ref_recv[k];
     const uint32_t kind = ref.z >> 30, sk = ref.z & kRefSkipNone;
     if (kind == kRefSelf) {  // OnlySelf: the sender when subscribed (y = 0 or 1), or an empty row
-        p.e_msg[m] = ref.y <= 1u ? ref.y : 0u;
+        uint32_t e = ref.y <= 1u ? ref.y : 0u;
+        if (RADIUS && e) {
+            const uint32_t me = p.sender[m];
+            e = within_radius(p.tv, p.pos[3ull * m], p.pos[3ull * m + 1], p.pos[3ull * m + 2], me) ? 1u : 0u;
+        }
+        p.e_msg[m] = e;
         p.info_msg[m] = make_uint2(kLocSelf, kNone);
         return;
     }
@@ -690,6 +710,29 @@ __global__ __launch_bounds__(kBlock) void k_ref_resolve(ResolveParams p) {
     const uint64_t at = p.prb[o] + ref.x;
     const uint32_t skip = sk == kRefSkipNone ? kNone : sk;
     const bool ok = kind == kRefPool && at + ref.y <= p.prb[o + 1] && ref.y && (skip == kNone || skip < ref.y);
+    if (RADIUS) {
+        uint32_t e = 0, mask = 0;
+        const uint32_t len = ref.y;
+        if (ok) {
+            const uint32_t me = p.sender[m];
+            const uint8_t rp = p.repl[m];
+            const double mx = p.pos[3ull * m], my = p.pos[3ull * m + 1], mz = p.pos[3ull * m + 2];
+            const uint32_t* row = p.pool + at;
+            for (uint32_t i = 0; i < len; ++i) {
+                const uint32_t q = row[i];
+                const bool keep = repl_keeps(rp, q, me) && within_radius(p.tv, mx, my, mz, q);
+                e += keep ? 1u : 0u;
+                if (keep && i < (uint32_t)kInline) mask |= 1u << i;
+            }
+        }
+        p.e_msg[m] = e;
+        // a short row carries its survivor mask (staged like an inline record's, kPoolShort), a long
+        // one its length (re-filtered by the emit)
+        p.info_msg[m] = !e ? make_uint2(0, kNone)
+                       : len <= (uint32_t)kInline ? make_uint2(kLocPool | (uint32_t)at, kPoolShort | (len << 24) | mask)
+                                                  : make_uint2(kLocPool | (uint32_t)at, len);
+        return;
+    }
     p.e_msg[m] = ok ? ref.y - (skip != kNone ? 1u : 0u) : 0u;
     p.info_msg[m] = ok ? make_uint2(kLocPool | (uint32_t)at, skip) : make_uint2(0, kNone);
 }
@@ -751,8 +794,8 @@ int slots_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_
     if (int rc = launch_tile_scan(h, tp)) return rc;
     EmitParams ep;
     ep.sender = sc.last_sender;
-    ep.pos = nullptr;
-    ep.repl = nullptr;
+    ep.pos = sc.last_radius ? sc.last_pos : nullptr;
+    ep.repl = sc.last_radius ? sc.last_repl : nullptr;
     ep.M = (uint32_t)M;
     ep.t = table_view(h);
     ep.e = sc.e_msg.as<uint32_t>();
@@ -765,7 +808,10 @@ int slots_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_
     ep.capacity = capacity;
     ep.n_blocks = nt;
     ep.pool = sc.G > 1 ? sc.pool_recv.as<uint32_t>() : nullptr;  // pool rows (kLocPool) only at G > 1
-    hipLaunchKernelGGL((emit_map_kernel<16>), dim3((nt + 1) / 2), dim3(kBlock), 0, s, ep);
+    if (sc.last_radius)  // the radius filter's emit: masks of inline rows, list and pool rows re-filtered
+        hipLaunchKernelGGL((emit_kernel<4096, 2, true>), dim3(nt), dim3(kBlock), 0, s, ep);
+    else
+        hipLaunchKernelGGL((emit_map_kernel<16>), dim3((nt + 1) / 2), dim3(kBlock), 0, s, ep);
     WQ_HIP(h, hipGetLastError());
     return WQ_OK;
 }
@@ -1117,6 +1163,9 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
     };
 
     if (inject == 1) fail(set_error(h, WQ_E_INVALID, "injected failure at step 1 (test hook)"));
+    // the radius filter (C5): own cubes by count_radius_kernel, remote rows filtered where they land
+    const bool radius = h->radius > 0.0;
+    if (radius && M && !d_pos && !late) fail(set_error(h, WQ_E_INVALID, "the radius filter needs message positions"));
     // fold in a finished incremental batch first (it may rebuild the table the rows point into)
     if (!late) fail(table_resolve(h, false));
     if (!late && G > 1 && h->tab.list.bytes / 4 >= (1ull << 30))
@@ -1146,7 +1195,11 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
         cp.health = route_health(h);
         cp.n_tiles = nt;
         const dim3 grid((nt + 1) / 2);  // two tiles per block (grid stride), as launch_route
-        if (G == 1 && d_keys)
+        if (radius && G == 1)
+            hipLaunchKernelGGL(count_radius_kernel<false>, dim3(nt), dim3(kBlock), 0, sc.side, cp);
+        else if (radius)
+            hipLaunchKernelGGL(count_radius_kernel<true>, dim3(nt), dim3(kBlock), 0, sc.side, cp);
+        else if (G == 1 && d_keys)
             hipLaunchKernelGGL((count_kernel<true, 1, 8>), grid, dim3(kBlock), 0, sc.side, cp);
         else if (G == 1)
             hipLaunchKernelGGL((count_kernel<false, 1, 8>), grid, dim3(kBlock), 0, sc.side, cp);
@@ -1392,7 +1445,17 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
         for (uint32_t d = 0; d <= G; ++d) rv.prb[d] = prb[d];
         rv.e_msg = sc.e_msg.as<uint32_t>();
         rv.info_msg = sc.info_msg.as<uint2>();
-        hipLaunchKernelGGL(k_ref_resolve, dim3((unsigned)((Sb + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rv);
+        const dim3 rg((unsigned)((Sb + kBlock - 1) / kBlock));
+        if (radius) {
+            rv.pool = sc.pool_recv.as<uint32_t>();
+            rv.pos = d_pos;
+            rv.sender = d_sender;
+            rv.repl = d_repl;
+            rv.tv = tv;
+            hipLaunchKernelGGL(k_ref_resolve<true>, rg, dim3(kBlock), 0, s, rv);
+        } else {
+            hipLaunchKernelGGL(k_ref_resolve<false>, rg, dim3(kBlock), 0, s, rv);
+        }
         WQ_HIP(h, hipGetLastError());
         // the count pass's per-tile totals held its own rows only
         if (M) {
@@ -1404,6 +1467,9 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
     if (!late) {
         sc.last_M = M;
         sc.last_sender = d_sender;
+        sc.last_pos = d_pos;
+        sc.last_repl = d_repl;
+        sc.last_radius = radius;
         sc.last_gen = h->table_gen;
         if ((rc = slots_copy_out(h, d_offsets, d_peers, d_msgs, capacity))) return rc;
     }
@@ -1481,7 +1547,7 @@ int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_
     if (capacity > 0xFFFFFFFFull) capacity = 0xFFFFFFFFull;
     hipStream_t s = h->stream;
     *n_pairs = 0;
-    if (h->shard && !(h->radius > 0.0) && !h->shard_expanded)
+    if (h->shard && !h->shard_expanded)
         return sharded_tick_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs,
                                   capacity, n_pairs);
     if (!h->shard) {  // G = 1 without an exchange: the single-GPU tick, P read back
