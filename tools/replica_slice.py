@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--out", default="")
+    ap.add_argument("--skip-full", action="store_true", help="skip the N = 1 line (profiling one slice size)")
     a = ap.parse_args()
     import torch
     import bench
@@ -42,7 +43,7 @@ def main():
     build_s = time.perf_counter() - t0
     res = {"workload": "C3, replicated table (27M subscriptions on the one GPU), one rank's message slice",
            "table_build_s": round(build_s, 3), "per_n": {}}
-    for n in [1] + [x for x in a.n if x > 1]:
+    for n in ([] if a.skip_full else [1]) + [x for x in a.n if x > 1]:
         lo, hi = a.rank * M_all // n, (a.rank + 1) * M_all // n
         M = hi - lo
         pos = torch.from_numpy(w.pos[lo:hi]).to(dev)
