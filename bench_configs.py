@@ -17,7 +17,7 @@ the timed region; a tick's timed work is everything the tick does on the GPU.
   c5  1M entities moving U[-4,4)^3 per tick in U[-1024,1024)^3, 3x3x3 subscriptions, one message
       each; a tick = the subscription diff of the move (incremental), the new peer positions, and the
       route with the exact radius filter r = 16. N = 1: one GPU. N > 1: strong scaling by cube hash
-      (message positions travel in the records to the owners; every rank holds all positions).
+      (the slot tick: owners return rows and pools, every rank holds all positions and filters).
 """
 from __future__ import annotations
 
@@ -822,8 +822,8 @@ def _cpu_c5_sample(init, tick_ops, pos_after, radius, seconds):
 def _run_c5_sharded(a, rank, world_size, local_rank, dev):
     """C5 over G GPUs by cube hash (strong scaling) through the C ABI's sharded tick: every rank
     applies the churn ops of the cubes it owns (wq_apply_ops_device on its slice of the op stream)
-    and holds every entity's position; it ingests 1/G of the messages, whose records carry their
-    positions to the owners (RCCL), which route them with the radius filter; pairs come back."""
+    and holds every entity's position; it ingests 1/G of the messages: 20-byte slots to the owners
+    (RCCL), row references + cube-list pools back, filtered by radius on the ingesting GPU."""
     import torch
     from worldql_server_amd import synth_ext
     from worldql_server_amd.router import Router
@@ -880,7 +880,8 @@ def _run_c5_sharded(a, rank, world_size, local_rank, dev):
     t_max_ms, pairs_all = reduce_over_ranks(t_ms, state["P"], dev, world_size)
     out = _line(a, world_size, pairs_all / (t_max_ms / 1e3), t_max_ms / a.steps, "strong",
                 f"C5 over {world_size} GPUs by cube hash: 1M entities, incremental churn on the owners, "
-                "message positions to the owners by RCCL (wq_sharded_route_tick_device), exact radius filter r=16"
+                "slots to the owners and cube-list pools back by RCCL (wq_sharded_route_tick_device), exact radius "
+                "filter r=16 on the ingesting GPU"
                 + ("" if a.scale == 1.0 else f" (scaled {a.scale})"),
                 {"messages_per_tick": N, "messages_per_gpu": M, "entities": N,
                  "pairs_per_tick": int(pairs_all) // a.steps,
