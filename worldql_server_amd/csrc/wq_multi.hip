@@ -222,6 +222,10 @@ int tick_into(wq_router* h, uint32_t g, const SliceIn& x, bool msgs) {
                 rc = wq_sharded_copy_out(s, reinterpret_cast<uint32_t*>(d2), reinterpret_cast<uint32_t*>(d2 + op2),
                                          msgs ? reinterpret_cast<uint32_t*>(d2 + om2) : nullptr, c2);
                 if (rc == WQ_OK) rc = clear_staging_overflow(s);
+                // the copy-out is enqueued, not finished: the slices' views are read as soon as the
+                // call returns (wq_route_tick_slices_device is synchronous), so wait for it here
+                if (rc == WQ_OK && hipStreamSynchronize(s->stream) != hipSuccess)
+                    rc = set_error(s, WQ_E_HIP, "sharded copy-out");
             }
             return rc;
         }

@@ -93,7 +93,8 @@ const Cfg kCfgs[] = {
 #undef WQ_CFG3
 #undef WQ_CFG3H
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
-constexpr int kCfgHeavy = 10;  // the default shape under wq_set_fanout_hint >= WQ_HEAVY_FANOUT (emit_map_kernel)
+constexpr int kCfgHeavy = 10;
+constexpr uint32_t kShortTickTiles = 12288;  // 256-message tiles up to which a tick is "short" (above)  // the default shape under wq_set_fanout_hint >= WQ_HEAVY_FANOUT (emit_map_kernel)
 
 }  // namespace
 
@@ -256,8 +257,11 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         {
         // two count tiles per block (grid stride): C3's 39,063 short blocks turn over less (with
         // two emit blocks per workgroup, 1,294-1,303 vs 1,320-1,328 us per tick on one box; 3 or 4
-        // no better). WQ_DEBUG_COUNT_TPB overrides (diagnostics)
-        static const uint32_t tpb = getenv("WQ_DEBUG_COUNT_TPB") ? (uint32_t)std::max(1, atoi(getenv("WQ_DEBUG_COUNT_TPB"))) : 2u;
+        // no better); a tick of a few rounds of resident blocks (an 8-GPU rank's replicated C3
+        // slice: 4,883 tiles) is faster with one (212-213 vs 221-222 us, with one emit block per
+        // workgroup too; 2.5M messages 383-384 vs 389-390). WQ_DEBUG_COUNT_TPB overrides (diagnostics)
+        static const uint32_t tpb_env = getenv("WQ_DEBUG_COUNT_TPB") ? (uint32_t)std::max(1, atoi(getenv("WQ_DEBUG_COUNT_TPB"))) : 0u;
+        const uint32_t tpb = tpb_env ? tpb_env : (n_count <= kShortTickTiles ? 1u : 2u);
         cp.n_tiles = n_count;
         cfg.count(cp, s, (n_count + tpb - 1) / tpb);
     }
@@ -300,8 +304,10 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     else if (cfg.emit_heavy == 116) {
         // diagnostics only: extra LDS per block caps the emit's blocks per CU (occupancy sweeps)
         static const size_t emit_lds = getenv("WQ_DEBUG_EMIT_LDS") ? strtoull(getenv("WQ_DEBUG_EMIT_LDS"), nullptr, 10) : 0;
-        // two 256-message blocks per workgroup (grid stride, see the count above); WQ_DEBUG_EMIT_BPB overrides
-        static const uint32_t bpb = getenv("WQ_DEBUG_EMIT_BPB") ? (uint32_t)std::max(1, atoi(getenv("WQ_DEBUG_EMIT_BPB"))) : 2u;
+        // two 256-message blocks per workgroup (grid stride, see the count above; one for a short
+        // tick); WQ_DEBUG_EMIT_BPB overrides
+        static const uint32_t bpb_env = getenv("WQ_DEBUG_EMIT_BPB") ? (uint32_t)std::max(1, atoi(getenv("WQ_DEBUG_EMIT_BPB"))) : 0u;
+        const uint32_t bpb = bpb_env ? bpb_env : (eg.x <= kShortTickTiles ? 1u : 2u);
         ep.n_blocks = eg.x;
         hipLaunchKernelGGL((emit_map_kernel<16>), dim3((eg.x + bpb - 1) / bpb), dim3(kBlock), emit_lds, s, ep);
     }
