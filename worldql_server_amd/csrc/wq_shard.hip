@@ -314,25 +314,33 @@ __global__ void __launch_bounds__(kBlock) slot_count_kernel(ShardIn in, uint32_t
     __syncthreads();
     const uint32_t m0 = blockIdx.x * kShardTile + threadIdx.x;
     const int lane = threadIdx.x & 63;
+    // every message's owner first (all loads of the lane in flight together), then the histogram:
+    // interleaved with the ballot loops, each message's loads waited for the previous message's
+    bool valid[kShardIPT];
+    uint32_t own[kShardIPT], wt[kShardIPT];
 #pragma unroll
     for (int i = 0; i < kShardIPT; ++i) {
         const uint32_t m = m0 + i * kBlock;
-        bool valid = m < in.M;
-        uint32_t own = 0xFFFFFFFFu, wt = 0;
-        if (valid) {
+        valid[i] = m < in.M;
+        own[i] = 0xFFFFFFFFu;
+        wt[i] = 0;
+        if (valid[i]) {
             int64_t x, y, z;
             msg_key<RAW>(in, m, x, y, z);
             const uint32_t w = in.world[m];
-            own = shard_of(w, x, y, z, in.G);
-            wt = msg_weight<RAW, true>(in, w, x, y, z);
-            valid = own != in.me;
+            own[i] = shard_of(w, x, y, z, in.G);
+            wt[i] = msg_weight<RAW, true>(in, w, x, y, z);
+            valid[i] = own[i] != in.me;
         }
-        const uint64_t wide = __ballot(valid && wt == 2);
-        uint64_t todo = __ballot(valid);
+    }
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint64_t wide = __ballot(valid[i] && wt[i] == 2);
+        uint64_t todo = __ballot(valid[i]);
         while (todo) {
             const int leader = __ffsll((unsigned long long)todo) - 1;
-            const uint32_t d = __shfl(own, leader, 64);
-            const uint64_t mask = __ballot(valid && own == d);
+            const uint32_t d = __shfl(own[i], leader, 64);
+            const uint64_t mask = __ballot(valid[i] && own[i] == d);
             if (lane == leader) atomicAdd(&cnt[d], (uint32_t)(__popcll(mask) + __popcll(mask & wide)));
             todo &= ~mask;
         }
@@ -394,6 +402,8 @@ __global__ void __launch_bounds__(kBlock)
     uint64_t pk[kShardIPT];
     uint32_t ext[kShardIPT], own[kShardIPT], rank[kShardIPT];
     bool reg[kShardIPT], go[kShardIPT];
+    uint32_t wrd[kShardIPT], snd[kShardIPT], rpl[kShardIPT];
+    // every message's key, owner and slot words first (all loads in flight together), then the ranks
 #pragma unroll
     for (int i = 0; i < kShardIPT; ++i) {
         const uint32_t m = m0 + i * kBlock;
@@ -401,13 +411,19 @@ __global__ void __launch_bounds__(kBlock)
         own[i] = 0xFFFFFFFFu;
         rank[i] = 0;
         reg[i] = true;
+        wrd[i] = snd[i] = rpl[i] = 0;
         if (go[i]) {
             msg_key<RAW>(in, m, kx[i], ky[i], kz[i]);
-            const uint32_t w = in.world[m];
-            own[i] = shard_of(w, kx[i], ky[i], kz[i], in.G);
-            reg[i] = pack_key(w, kx[i], ky[i], kz[i], in.sf, &pk[i], &ext[i]);
+            wrd[i] = in.world[m];
+            snd[i] = in.sender[m];
+            rpl[i] = in.repl[m];
+            own[i] = shard_of(wrd[i], kx[i], ky[i], kz[i], in.G);
+            reg[i] = pack_key(wrd[i], kx[i], ky[i], kz[i], in.sf, &pk[i], &ext[i]);
             go[i] = own[i] != in.me;
         }
+    }
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
         const uint64_t wide = __ballot(go[i] && !reg[i]);
         uint64_t todo = __ballot(go[i]);
         while (todo) {
@@ -439,19 +455,19 @@ __global__ void __launch_bounds__(kBlock)
         if (j + (reg[i] ? 1u : 2u) > L.budget[d]) continue;    // over budget: the tick is redone exactly
         const uint32_t slot = L.base[d] + j;
         uint32_t* o = out + (uint64_t)kSlotWords * slot;
-        const uint32_t rp = in.repl[m];
+        const uint32_t rp = rpl[i];
         if (reg[i]) {
             o[0] = (uint32_t)pk[i];
             o[1] = (uint32_t)(pk[i] >> 32);
             o[2] = ext[i];
-            o[3] = in.sender[m];
+            o[3] = snd[i];
             o[4] = rp | (kSlotReg << 8);
             perm[slot] = m;
         } else {
             o[0] = (uint32_t)(uint64_t)kx[i];
             o[1] = (uint32_t)((uint64_t)kx[i] >> 32);
-            o[2] = in.world[m];
-            o[3] = in.sender[m];
+            o[2] = wrd[i];
+            o[3] = snd[i];
             o[4] = rp | (kSlotHead << 8);
             o[5] = (uint32_t)(uint64_t)ky[i];
             o[6] = (uint32_t)((uint64_t)ky[i] >> 32);

@@ -518,9 +518,11 @@ struct RefOwnerParams {
     uint4* desc_fill;      // pool rows: the claiming slot copies its cube's peers
 };
 
-__device__ __forceinline__ uint32_t slot_cnt(const uint2 inf, uint32_t e, const uint32_t* list) {
+__device__ __forceinline__ uint32_t slot_cnt(const uint2 inf, uint32_t e) {
     if (inf.x & kLocSelf) return e;
-    if (inf.x & kLocGlobal) return list[inf.x & ~kLocGlobal];
+    // a list row: e is the count less the sender's entry when the row skips it (finish_message),
+    // so no read of the list's count word is needed
+    if (inf.x & kLocGlobal) return e + (inf.y != kNone ? 1u : 0u);
     return inf.y == kNone ? 0u : inf.y >> 24;  // inline record, or no subscriber at all
 }
 
@@ -533,7 +535,7 @@ __global__ __launch_bounds__(kBlock) void k_ref_claim(RefOwnerParams p) {
     const uint32_t i = t < p.self_lo ? t : t + p.n_self;  // the received slot
     const uint32_t s = seg_find(p.rrem, p.G, t);
     const uint2 inf = p.info[i];
-    const uint32_t cnt = slot_cnt(inf, p.e[i], p.list);
+    const uint32_t cnt = slot_cnt(inf, p.e[i]);
     bool leader = false;
     uint64_t hs = 0;
     if (!(inf.x & kLocSelf) && cnt) {
