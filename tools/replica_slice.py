@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--out", default="")
     ap.add_argument("--skip-full", action="store_true", help="skip the N = 1 line (profiling one slice size)")
+    ap.add_argument("--cfg", type=int, default=0, help="route config (wq_debug_set_route_config; 0 = default)")
     a = ap.parse_args()
     import torch
     import bench
@@ -38,6 +39,8 @@ def main():
     r = Router(w.cube_size, 0)
     stream = torch.cuda.Stream(device=dev)
     r.set_stream(stream.cuda_stream)
+    if a.cfg:
+        r.set_route_config(a.cfg)
     t0 = time.perf_counter()
     r.apply_ops(w.ops)
     build_s = time.perf_counter() - t0
