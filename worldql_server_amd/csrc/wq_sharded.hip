@@ -1151,8 +1151,8 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
     uint32_t* c_recv = c_send + 2 * G;
     wq_route_counters* cnts = reinterpret_cast<wq_route_counters*>(small + kSmallCnt);
     const size_t small_used = kSmallCnt + 4 * sizeof(wq_route_counters);
-    WQ_HIP(h, hipMemsetAsync(small, 0, small_used, s));
-    WQ_HIP(h, hipMemsetAsync(c_send, 0, 16 * G, s));
+    static_assert(kSmallC + 16 * WQ_MAX_SHARDS <= kSmallCnt, "the C vectors lie inside the zeroed span");
+    WQ_HIP(h, hipMemsetAsync(small, 0, small_used, s));  // A, C (both directions) and the counters
     if (int rc = ensure_health(h)) return rc;
     if (exact) sc.n_exact++;
     else sc.n_budget++;
