@@ -672,3 +672,58 @@ def test_hub_radius_ticks_vs_whole_table_oracle(G, form):
     for r in routers:
         r.close()
     hub.close()
+
+
+@pytest.mark.parametrize("form", ["slots", "expanded"])
+def test_hub_radius_irregular_keys_vs_whole_table_oracle(form):
+    """The radius filter on keys without a packed form (two slots on the wire, slot-table cubes on the
+    owner: coordinates beyond +-2^23 cubes, +-inf, a world id >= 2^24 - 1) — and the collective
+    error when a shard gives raw keys instead of the positions the filter needs."""
+    import torch
+    from worldql_server_amd.router import Hub, Router, WQError
+    w, keys, key_ops = _irregular_workload()
+    M, G, radius = len(w.world), 3, 20.0
+    peer_pos = np.random.default_rng(5).uniform(-48.0, 48.0, (1500, 3))
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    results, errors = [None] * G, []
+
+    def body(rank):
+        try:
+            r = routers[rank]
+            r.attach_hub(hub, rank)
+            r.set_shard_form(form == "expanded")
+            r.set_peer_positions(peer_pos)
+            r.set_radius(radius)
+            lo, hi = _slice(M, G, rank)
+            r.sharded_apply_ops(w.ops)
+            by_pos = _tick(r, w, lo, hi, dev)
+            try:  # raw keys, no positions: every shard's tick fails, after the collective
+                rc_key = _tick(r, w, lo, hi, dev, keys=keys)[0]
+            except WQError as e:
+                rc_key = e.code
+            results[rank] = (by_pos, rc_key)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=body, args=(k,)) for k in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    assert not errors, errors
+    o = orc.COracle(16)
+    o.apply_ops(w.ops)
+    wo_, wp_ = o.route_radius(w.pos, w.world, w.sender, w.repl, peer_pos, radius)[:2]
+    total = 0
+    for rank in range(G):
+        lo, hi = _slice(M, G, rank)
+        by_pos, rc_key = results[rank]
+        _check(by_pos, (wo_[lo:hi + 1] - wo_[lo], wp_[wo_[lo]:wo_[hi]]), hi - lo)
+        total += len(by_pos[2])
+        assert rc_key == abi.WQ_E_INVALID
+    assert total > 0
+    for r in routers:
+        r.close()
+    hub.close()

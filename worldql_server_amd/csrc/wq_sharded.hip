@@ -1038,6 +1038,9 @@ static int shard_exchange_route(wq_router* h, const double* d_pos, const int64_t
     uint32_t* cnt_recv = cnt_send + G;
     WQ_HIP(h, hipMemsetAsync(cnt_send, 0, 4 * G, s));
     if (inject == 1) fail(set_error(h, WQ_E_INVALID, "injected failure at step 1 (test hook)"));
+    // as the slot tick and the single-GPU tick: the radius filter needs the message positions
+    if (h->radius > 0.0 && M && !d_pos && !late)
+        fail(set_error(h, WQ_E_INVALID, "the radius filter needs message positions"));
     int rc = late ? late : sc.recs.ensure((M ? M : 1) * sizeof(wq_msg_rec)) == hipSuccess
                  ? WQ_OK
                  : set_error(h, WQ_E_OOM, "hipMalloc of the sharded tick's records");
