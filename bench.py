@@ -239,9 +239,9 @@ def main():
     rehearse = os.environ.get("WQ_BENCH_ONE_GPU") == "1"
     if rehearse:
         local_rank = 0
+    torch.cuda.set_device(local_rank)  # before the process group: RCCL's barrier uses the current device
     if world_size > 1:
         dist.init_process_group("gloo" if rehearse else "nccl", init_method="env://")
-    torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
     if a.config != "c2":
