@@ -9,6 +9,7 @@ import argparse
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -31,22 +32,26 @@ def _mtime(p):
     return os.path.getmtime(p) if os.path.exists(p) else 0.0
 
 
+def _jobs() -> int:
+    """Parallel compiles: MAX_JOBS when set (16 on the GPU boxes), else the CPUs, at most 8."""
+    env = os.environ.get("MAX_JOBS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return max(1, min(8, os.cpu_count() or 1))
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(BUILD, exist_ok=True)
     hdr_t = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
     hdr_t = max(hdr_t, _mtime(os.path.join(ROOT, "include", "wq_router.h")))
-    objs = []
+    objs, cmds = [], []
     relink = force or not os.path.exists(LIB)
     for src in SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(BUILD, src.replace(".hip", ".o"))
         objs.append(o)
         if force or _mtime(o) < max(_mtime(s), hdr_t):
-            cmd = [HIPCC, *FLAGS, "-I", os.path.join(ROOT, "include"), "-c", s, "-o", o]
-            if verbose:
-                print(" ".join(cmd), flush=True)
-            subprocess.check_call(cmd)
-            relink = True
+            cmds.append([HIPCC, *FLAGS, "-I", os.path.join(ROOT, "include"), "-c", s, "-o", o])
     # host-only C++ (the wire codec): g++, no device code
     codec_h = _mtime(os.path.join(ROOT, "include", "wq_codec.h"))
     for src in HOST_SOURCES:
@@ -54,11 +59,18 @@ def build(force: bool = False, verbose: bool = False) -> str:
         o = os.path.join(BUILD, src.replace(".cpp", ".o"))
         objs.append(o)
         if force or _mtime(o) < max(_mtime(s), codec_h):
-            cmd = [CXX, *HOST_FLAGS, "-I", os.path.join(ROOT, "include"), "-c", s, "-o", o]
+            cmds.append([CXX, *HOST_FLAGS, "-I", os.path.join(ROOT, "include"), "-c", s, "-o", o])
+    if cmds:
+        relink = True
+        for c in cmds:
             if verbose:
-                print(" ".join(cmd), flush=True)
-            subprocess.check_call(cmd)
-            relink = True
+                print(" ".join(c), flush=True)
+        # the translation units compile independently (wq_route / wq_sharded dominate)
+        with ThreadPoolExecutor(max_workers=min(_jobs(), len(cmds))) as pool:
+            rcs = list(pool.map(lambda c: subprocess.call(c), cmds))
+        for c, rc in zip(cmds, rcs):
+            if rc != 0:
+                raise subprocess.CalledProcessError(rc, c)
     if relink or any(_mtime(o) > _mtime(LIB) for o in objs):
         cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-pthread", "-o", LIB, *objs, "-ldl"]
         if verbose:
