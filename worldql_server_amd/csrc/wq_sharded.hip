@@ -527,22 +527,54 @@ __device__ __forceinline__ uint32_t slot_cnt(const uint2 inf, uint32_t e) {
 }
 
 // (owner, remote slots) the cube's peer count and the claim of the slot's (source, cube) pair: the
-// first claimer ships the cube's peers in that source's pool, the others point at them.
+// first claimer ships the cube's peers in that source's pool, the others point at them. The block's
+// slots first meet in an LDS table, so each distinct pair of the block claims once in global memory:
+// C3's hot cubes put thousands of a source's slots on one claim word, and device-scope atomics on
+// one word serialise.
+constexpr uint32_t kClaimLds = 2 * kBlock;  // LDS table slots (a block has at most kBlock keys)
+constexpr unsigned long long kClaimEmpty = ~0ull;
+
 __global__ __launch_bounds__(kBlock) void k_ref_claim(RefOwnerParams p) {
+    __shared__ unsigned long long lkey[kClaimLds];
+    __shared__ uint32_t lres[kClaimLds];  // the pair's claim slot | leader bit 31 (set by its representative)
     const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    for (uint32_t k = threadIdx.x; k < kClaimLds; k += kBlock) lkey[k] = kClaimEmpty;
     if (t == p.n_rem) p.plen[t] = 0;
-    if (t >= p.n_rem) return;
+    const bool live = t < p.n_rem;
     const uint32_t i = t < p.self_lo ? t : t + p.n_self;  // the received slot
-    const uint32_t s = seg_find(p.rrem, p.G, t);
-    const uint2 inf = p.info[i];
-    const uint32_t cnt = slot_cnt(inf, p.e[i]);
-    bool leader = false;
+    uint2 inf = make_uint2(kLocSelf, kNone);
+    uint32_t cnt = 0, s = 0;
+    if (live) {
+        s = seg_find(p.rrem, p.G, t);
+        inf = p.info[i];
+        cnt = slot_cnt(inf, p.e[i]);
+    }
+    const bool claims = live && !(inf.x & kLocSelf) && cnt;
+    const unsigned long long pair = ((unsigned long long)s << 32) | inf.x;  // s < G: never kClaimEmpty
+    __syncthreads();
+    // the block's table: the thread that inserts a pair represents it
+    bool rep = false;
+    uint32_t lh = 0;
+    if (claims) {
+        uint64_t hv = pair * 0x9E3779B97F4A7C15ull;
+        lh = (uint32_t)(hv >> 40) & (kClaimLds - 1);
+        for (;;) {
+            const unsigned long long old = atomicCAS(&lkey[lh], kClaimEmpty, pair);
+            if (old == kClaimEmpty) {
+                rep = true;
+                break;
+            }
+            if (old == pair) break;
+            lh = (lh + 1) & (kClaimLds - 1);
+        }
+    }
     uint64_t hs = 0;
-    if (!(inf.x & kLocSelf) && cnt) {
-        const unsigned long long key = ((unsigned long long)p.tag << 38) | ((unsigned long long)s << 32) | inf.x;
+    if (rep) {
+        const unsigned long long key = ((unsigned long long)p.tag << 38) | pair;
         uint64_t hv = ((uint64_t)inf.x | ((uint64_t)s << 32)) * 0x9E3779B97F4A7C15ull;
         hv ^= hv >> 29;
         hs = hv & p.cmask;
+        bool leader = false;
         for (;;) {
             unsigned long long v = __hip_atomic_load(p.claim + hs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if ((v >> 38) != p.tag) {  // a previous tick's word: free
@@ -557,6 +589,15 @@ __global__ __launch_bounds__(kBlock) void k_ref_claim(RefOwnerParams p) {
             if ((v >> 38) == p.tag) hs = (hs + 1) & p.cmask;
         }
         if (leader) p.lead[hs] = t;
+        lres[lh] = (uint32_t)hs | (leader ? 0x80000000u : 0u);
+    }
+    __syncthreads();
+    if (!live) return;
+    bool leader = false;
+    if (claims) {
+        const uint32_t r = lres[lh];
+        hs = r & 0x7FFFFFFFu;
+        leader = rep && (r >> 31);
     }
     p.cnt[t] = cnt;
     p.hslot[t] = (uint32_t)hs;
