@@ -136,6 +136,49 @@ def test_hub_sharded_ticks_vs_whole_table_oracle(G, form):
     hub.close()
 
 
+@pytest.mark.parametrize("n_peers", [40, 600])
+def test_hub_hot_cubes_vs_whole_table_oracle(n_peers):
+    """Every message in a few dozen (world, cube) buckets: a block of the owner's received slots holds
+    the same (source, cube) pair many times over, so the per-block LDS claim table (k_ref_claim)
+    deduplicates nearly every slot before the global claims. 40 peers: the rows are inline records;
+    600: long lists."""
+    import torch
+    from worldql_server_amd.router import Hub, Router
+    G = 3
+    w = synth.uniform_box(13, n_peers, 30000, 20.0, neighbourhood=True, repl_mode="mixed", n_worlds=3)
+    M = len(w.world)
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    results, errors = [None] * G, []
+
+    def body(rank):
+        try:
+            r = routers[rank]
+            r.attach_hub(hub, rank)
+            lo, hi = _slice(M, G, rank)
+            r.sharded_apply_ops(w.ops)
+            cap = 256 * (hi - lo) + 64  # above the 161 recipients of the busiest message
+            results[rank] = (_tick(r, w, lo, hi, dev, cap=cap), _tick(r, w, lo, hi, dev, cap=cap))
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=body, args=(k,)) for k in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    assert not errors, errors
+    for rank in range(G):
+        lo, hi = _slice(M, G, rank)
+        want = _expected([w.ops], w, lo, hi)
+        for got in results[rank]:  # the exact first tick, then a budgeted one
+            _check(got, want, hi - lo)
+    for r in routers:
+        r.close()
+    hub.close()
+
+
 @pytest.mark.parametrize("G", [1, 2, 3])
 def test_hub_owner_form_vs_whole_table_oracle(G):
     """wq_sharded_route_owner_device: the pairs stay on their owner; across the shards every message of
