@@ -64,7 +64,8 @@ constexpr uint32_t kStDone = 0, kStProbe = 1, kStVerify = 2;
 template <bool RAW_KEYS, int IPT, int DBG = 0, bool FULL = false, bool SLOTS = false, bool OWN = false>
 __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& tv, uint32_t m0,
                                            uint32_t (&e_out)[IPT], uint2 (&inf_out)[IPT], uint64_t& F_local,
-                                           uint32_t& E_local, uint4 (*peers_out)[6] = nullptr) {
+                                           uint32_t& E_local, uint4 (*peers_out)[6] = nullptr,
+                                           uint32_t* owner_out = nullptr) {
     const int tid = threadIdx.x;
 
     // ---- A: inputs (all loads first), quantise (kernel 1), packed key, home slot ----
@@ -136,7 +137,13 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
                 z = coord_clamp_dev(__longlong_as_double((long long)in_c[i][2]), tv.sf, in.si);
             }
             reg = pack_key(w, x, y, z, tv.sf, &pk[i], &ext[i]);
-            if (OWN) valid = valid && shard_of(w, x, y, z, in.own_G) == in.own_me;
+            if (OWN) {
+                const uint32_t ow = shard_of(w, x, y, z, in.own_G);
+                valid = valid && ow == in.own_me;
+                // OWN callers that also group the other shards' messages (wq_sharded.hip
+                // own_count_hist_kernel): the owner, bit 31 = a two-slot (unpacked) key
+                if (owner_out) owner_out[i] = ow | (reg ? 0u : 0x80000000u);
+            }
         }
         // lanes with nothing to probe read a dummy line spread by message index (never one shared
         // line: a chip-wide hot line serialises on its L2 channel)

@@ -630,7 +630,8 @@ int launch_shard_slots(wq_router* h, const double* d_pos, const int64_t* d_keys,
 // phases: 1 = the counts only (histogram + scan), 2 = the scatter and padding after them, 3 = both.
 int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
                         const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, uint32_t me,
-                        const SlotLayout& L, uint32_t* d_slots, uint32_t* d_perm, uint32_t* d_a, int phases) {
+                        const SlotLayout& L, uint32_t* d_slots, uint32_t* d_perm, uint32_t* d_a, int phases,
+                        bool hist_ready) {
     hipStream_t s = h->stream;
     ShardIn in;
     in.pos = d_pos;
@@ -648,7 +649,9 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
     if (M && (phases & 1)) {
         WQ_ALLOC(h, h->shard_hist, (uint64_t)in.nblk * G * 4);
         uint32_t* hist = h->shard_hist.as<uint32_t>();
-        if (d_keys)
+        if (hist_ready) {
+            // the caller's own-cube count wrote it (wq_sharded.hip own_count_hist_kernel)
+        } else if (d_keys)
             hipLaunchKernelGGL((slot_count_kernel<true>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist);
         else
             hipLaunchKernelGGL((slot_count_kernel<false>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist);
@@ -678,6 +681,8 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
     }
     return WQ_OK;
 }
+
+uint32_t budget_slot_tile() { return kShardTile; }
 
 int launch_op_owner(wq_router* h, const wq_op* d_ops, size_t n, uint32_t G, uint32_t* d_owner) {
     if (n == 0) return WQ_OK;

@@ -48,7 +48,9 @@ int launch_shard_messages(wq_router* h, const double* d_pos, const int64_t* d_ke
                           uint32_t* d_counts);
 int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
                         const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, uint32_t me,
-                        const SlotLayout& L, uint32_t* d_slots, uint32_t* d_perm, uint32_t* d_a, int phases);
+                        const SlotLayout& L, uint32_t* d_slots, uint32_t* d_perm, uint32_t* d_a, int phases,
+                        bool hist_ready = false);
+uint32_t budget_slot_tile();
 int launch_route_records(wq_router* h, const wq_msg_rec* d_recs, size_t M, uint32_t* d_offsets, uint32_t* d_peers,
                          uint32_t* d_msgs, size_t capacity);
 int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
@@ -780,6 +782,77 @@ __global__ __launch_bounds__(kBlock) void k_ref_resolve(ResolveParams p) {
     p.info_msg[m] = ok ? make_uint2(kLocPool | (uint32_t)at, skip) : make_uint2(0, kNone);
 }
 
+// (ingesting GPU, G > 1, no radius) the own-cube count and the slot grouping's owner histogram in
+// ONE pass over the messages (both quantise every message): block b takes the kHistTiles count
+// tiles of histogram tile b (launch_budget_slots' 4 x 256 messages), counts its own cubes' messages
+// as count_kernel<OWN> does, and adds every other message's slot weight (2 for an unpacked key) to
+// its owner's column, hist[d * nblk + b], as slot_count_kernel would.
+constexpr uint32_t kHistTiles = 4;
+
+template <bool RAW>
+__global__ __launch_bounds__(kBlock, 8) void own_count_hist_kernel(CountParams p, uint32_t nblk,
+                                                                   uint32_t* __restrict__ hist) {
+    __shared__ uint64_t wave_F[kWaves];
+    __shared__ uint64_t wave_E[kWaves];
+    __shared__ uint32_t hcnt[WQ_MAX_SHARDS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t G = p.in.own_G;
+    for (uint32_t d = tid; d < G; d += kBlock) hcnt[d] = 0;
+    if (blockIdx.x == 0 && tid == 0) {
+        p.cnt_next->n_pairs = 0;
+        p.cnt_next->n_candidates = 0;
+        p.cnt_next->overflow = 0;
+        p.cnt_next->error = 0;
+    }
+    __syncthreads();
+    for (uint32_t k = 0; k < kHistTiles; ++k) {
+        const uint32_t blk = blockIdx.x * kHistTiles + k;  // block-uniform
+        if (blk >= p.n_tiles) break;
+        const uint32_t m0 = blk * kBlock, m = m0 + tid;
+        uint64_t F_local = 0;
+        uint32_t E_local = 0;
+        uint32_t e_out[1], own[1];
+        uint2 inf_out[1];
+        count_rows<RAW, 1, 0, false, false, true>(p.in, p.t, m0, e_out, inf_out, F_local, E_local, nullptr, own);
+        if (m < p.in.M) {
+            p.e[m] = e_out[0];
+            p.info[m] = inf_out[0];
+        }
+        // the other shards' messages, one LDS add per distinct owner in the wave
+        const uint32_t ow = own[0] & 0x7FFFFFFFu;
+        const bool rem = m < p.in.M && ow != p.in.own_me;
+        const uint64_t wide = __ballot(rem && (own[0] >> 31));
+        uint64_t todo = __ballot(rem);
+        while (todo) {
+            const int leader = __ffsll((unsigned long long)todo) - 1;
+            const uint32_t d = __shfl(ow, leader, 64);
+            const uint64_t mask = __ballot(rem && ow == d);
+            if (lane == leader) atomicAdd(&hcnt[d], (uint32_t)(__popcll(mask) + __popcll(mask & wide)));
+            todo &= ~mask;
+        }
+        const uint64_t Fw = wave_sum_u64(F_local);
+        const uint64_t Ew = wave_sum_u64(E_local);
+        if (lane == 0) {
+            wave_F[wave] = Fw;
+            wave_E[wave] = Ew;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint64_t Fb = 0, Eb = 0;
+#pragma unroll
+            for (int u = 0; u < kWaves; ++u) {
+                Fb += wave_F[u];
+                Eb += wave_E[u];
+            }
+            p.tile_F[blk] = Fb > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Fb;
+            p.tile_total[blk] = Eb > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Eb;
+            if (Eb > 0xFFFFFFFFull) flag_route(p.cnt, p.health, 2u, 0u);
+        }
+        __syncthreads();  // the next tile rewrites wave_F / wave_E
+    }
+    for (uint32_t d = tid; d < G; d += kBlock) hist[(uint64_t)d * nblk + blockIdx.x] = hcnt[d];
+}
+
 int attach(wq_router* h, uint32_t G, uint32_t rank) {
     if (!h || G == 0 || G > WQ_MAX_SHARDS || rank >= G) return WQ_E_INVALID;
     if (h->shard) return set_error(h, WQ_E_INVALID, "an exchange is already attached (wq_shard_detach first)");
@@ -1222,9 +1295,37 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
                   fail(alloc(sc.mtiles, ((uint64_t)nt * 3 + 4) * 4)))) {
     }
 
-    // ---- own cubes, on the side stream ----
-    bool forked = false;
-    if (!late && M) {
+    // ---- own cubes: with G > 1 (no radius) in one pass with the slot grouping's owner histogram on
+    // the tick's stream, else on the side stream beside the exchanges ----
+    bool forked = false, hist_ready = false;
+    static const bool two_pass = getenv("WQ_DEBUG_NO_OWN_HIST") != nullptr;  // diagnostics
+    const bool fuse = G > 1 && !radius && budget_slot_tile() == kHistTiles * kBlock && !two_pass;
+    if (!late && M && fuse) {
+        const uint32_t nblk = (uint32_t)((M + kHistTiles * kBlock - 1) / (kHistTiles * kBlock));
+        if (!fail(alloc(h->shard_hist, (uint64_t)nblk * G * 4))) {
+            CountParams cp{};
+            cp.in = RouteIn{d_pos, d_keys, d_world, d_sender, d_repl, (uint32_t)M, (int64_t)h->cube_size};
+            cp.in.own_G = G;
+            cp.in.own_me = me;
+            cp.t = tv;
+            cp.e = sc.e_msg.as<uint32_t>();
+            cp.info = sc.info_msg.as<uint2>();
+            cp.tile_total = sc.mtiles.as<uint32_t>();
+            cp.tile_F = cp.tile_total + 2 * (uint64_t)nt;
+            cp.cnt = cnts + kCntSelf;
+            cp.cnt_next = cnts + kCntScratch;
+            cp.health = route_health(h);
+            cp.n_tiles = nt;
+            if (d_keys)
+                hipLaunchKernelGGL(own_count_hist_kernel<true>, dim3(nblk), dim3(kBlock), 0, s, cp, nblk,
+                                   h->shard_hist.as<uint32_t>());
+            else
+                hipLaunchKernelGGL(own_count_hist_kernel<false>, dim3(nblk), dim3(kBlock), 0, s, cp, nblk,
+                                   h->shard_hist.as<uint32_t>());
+            WQ_HIP(h, hipGetLastError());
+            hist_ready = true;
+        }
+    } else if (!late && M) {
         WQ_HIP(h, hipEventRecord(sc.ev_fork, s));
         WQ_HIP(h, hipStreamWaitEvent(sc.side, sc.ev_fork, 0));
         CountParams cp{};
@@ -1285,7 +1386,7 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
             for (uint32_t d = 0; d < G; ++d) inf.budget[d] = 0xFFFFFFFFu;
             if (!late)
                 fail(launch_budget_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, me, inf, nullptr, nullptr,
-                                         a_send, 1));
+                                         a_send, 1, hist_ready));
             if (late && (rc = put_status(a_send))) return rc;
             Xfer x{{a_send}, {eight.data()}, {a_recv}, {eight.data()}, 1};
             if ((rc = exchange(h, x))) return rc;
@@ -1305,7 +1406,7 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
             return fatal_receive(h, "hipMalloc of the sharded tick's slots");
         if (!late)
             fail(launch_budget_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, me, L, sc.slots.as<uint32_t>(),
-                                     sc.perm.as<uint32_t>(), a_send, exact ? 2 : 3));
+                                     sc.perm.as<uint32_t>(), a_send, exact ? 2 : 3, hist_ready));
         if (late) {  // nothing to send: tail slots everywhere (zero words route to nobody either way)
             WQ_HIP(h, hipMemsetAsync(sc.slots.p, 0, (Sb + 1) * kSlotWords * 4, s));
             WQ_HIP(h, hipMemsetAsync(sc.perm.p, 0xFF, (Sb + 1) * 4, s));
