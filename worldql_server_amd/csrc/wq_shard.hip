@@ -349,14 +349,14 @@ __global__ void __launch_bounds__(kBlock) slot_count_kernel(ShardIn in, uint32_t
     for (uint32_t d = threadIdx.x; d < in.G; d += kBlock) counts[(uint64_t)d * in.nblk + blockIdx.x] = cnt[d];
 }
 
-// (b2) one block: per owner, the exclusive scan of its column of block counts (in place); the
-// owner's total and the budget bit to a[2d], a[2d + 1].
+// (b2) one block per owner d (the columns are independent): the exclusive scan of its column of
+// block counts (in place); the owner's total and the budget bit to a[2d], a[2d + 1].
 __global__ void __launch_bounds__(kScanThreads1)
     slot_scan_kernel(uint32_t* __restrict__ v, uint32_t nblk, uint32_t G, SlotLayout L, uint32_t* __restrict__ a) {
     __shared__ uint32_t wsum[kScanThreads1 / 64];
     __shared__ uint32_t carry_s;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (uint32_t d = 0; d < G; ++d) {
+    for (uint32_t d = blockIdx.x; d < G; d += gridDim.x) {
         uint32_t* col = v + (uint64_t)d * nblk;
         if (threadIdx.x == 0) carry_s = 0;
         __syncthreads();
@@ -656,7 +656,7 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
         else
             hipLaunchKernelGGL((slot_count_kernel<false>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist);
         WQ_HIP(h, hipGetLastError());
-        hipLaunchKernelGGL(slot_scan_kernel, dim3(1), dim3(kScanThreads1), 0, s, hist, in.nblk, G, L, d_a);
+        hipLaunchKernelGGL(slot_scan_kernel, dim3(G), dim3(kScanThreads1), 0, s, hist, in.nblk, G, L, d_a);
         WQ_HIP(h, hipGetLastError());
     } else if (phases & 1) {
         WQ_HIP(h, hipMemsetAsync(d_a, 0, 8 * G, s));
