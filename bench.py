@@ -5,6 +5,12 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+--gpus N > 1 without a launcher (no WORLD_SIZE in the environment): this process makes no GPU call,
+starts N ranks of itself (RANK / LOCAL_RANK / WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free port), passes
+rank 0's line through and exits with the first non-zero rank status. Under a launcher, --gpus must
+equal WORLD_SIZE (exit status 2 otherwise). Exit status 3: the headline line was printed but the
+second multi-GPU form (extra.cube_hash / extra.replicated_table) failed or hung.
+
 Headline workload: SURVEY.md §8(d) C3, the configuration north_star's target is quoted on — 1M peers
 each subscribed to a 3x3x3 neighbourhood (27M subscriptions), 10M LocalMessages per tick, 90% from
 256 Zipf-weighted Gaussian hotspots, cube_size 16, ExceptSelf, synthetic (splitmix64).
@@ -40,7 +46,8 @@ METRIC = "routed msg→peer pairs/sec per tick at 1/2/4/8 GPUs; % HBM roofline"
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of the run; default WORLD_SIZE under a launcher, else 1")
     ap.add_argument("--config", choices=["c1", "c2", "c3", "c4", "c5"], default=None,
                     help="default: the headline, C3 (north_star's 1M peers / 10M messages per tick) with the C2 "
                          "line nested under extra.c2 at N = 1; c1..c5 = one SURVEY.md §8(d) config alone")
@@ -146,16 +153,64 @@ def cube_workload(rank: int, world_size: int, scale: float = 1.0):
     return w, lo, hi
 
 
-def reduce_over_ranks(t_ms: float, pairs: int, dev, world_size: int):
-    """(max over ranks of the timed region, sum over ranks of pairs per tick)."""
+def allreduce(vals, op: str, dev, world_size: int) -> list:
+    """All-reduce a few float64 values over the ranks ("max" or "sum"). RCCL takes device tensors;
+    gloo (the one-GPU rehearsal) takes host tensors — a device tensor handed to gloo is read by its
+    own copy, unordered with the stream that wrote it (how an N = 2 rehearsal once summed bytes to 0)."""
     import torch
     import torch.distributed as dist
-    t = torch.tensor([t_ms], dtype=torch.float64, device=dev)
-    p = torch.tensor([float(pairs)], dtype=torch.float64, device=dev)
-    if world_size > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(p, op=dist.ReduceOp.SUM)
-    return float(t.item()), float(p.item())
+    vals = [float(v) for v in vals]
+    if world_size == 1:
+        return vals
+    on_dev = dist.get_backend() == "nccl"
+    t = torch.tensor(vals, dtype=torch.float64, device=dev if on_dev else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    return t.cpu().tolist()
+
+
+def reduce_over_ranks(t_ms: float, pairs: int, dev, world_size: int):
+    """(max over ranks of the timed region, sum over ranks of pairs per tick)."""
+    (t,) = allreduce([t_ms], "max", dev, world_size)
+    (p,) = allreduce([pairs], "sum", dev, world_size)
+    return t, p
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """--gpus N > 1 without a launcher: N ranks of this script, one per GPU, started from a process
+    that has made no GPU call (it never imports torch). Returns the exit status: 0, or the first
+    non-zero rank status (the other ranks are then stopped)."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with status {rc}; stopping the others",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return status
 
 
 def _oracle_router(w):
@@ -228,6 +283,12 @@ def cpu_baseline_mt(w, threads: int) -> dict:
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ:
+        if a.gpus is not None and a.gpus > 1:
+            sys.exit(launch_ranks(a.gpus))
+    elif a.gpus is not None and a.gpus != int(os.environ["WORLD_SIZE"]):
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}", file=sys.stderr, flush=True)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 

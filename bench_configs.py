@@ -360,8 +360,9 @@ def _c3_replicated(a, w, rank, world_size, local_rank, dev, stream, sl):
     assert c["overflow"] == 0 and c["error"] == 0, c
     t_ms = timed_ticks(lambda: r.route_device(*args, 0), a.steps, stream, dev, world_size, [r])
     r.close()
-    t_max_ms, pairs_all = reduce_over_ranks(t_ms, P, dev, world_size)
-    _, B_all = reduce_over_ranks(0.0, algorithmic_bytes(M, F, P), dev, world_size)
+    (t_max_ms,) = bench.allreduce([t_ms], "max", dev, world_size)
+    pairs_all, B_all = bench.allreduce([P, algorithmic_bytes(M, F, P)], "sum", dev, world_size)
+    assert B_all > 0 and pairs_all >= 0, (B_all, pairs_all)
     del peers, msgs
     return {"t_max_ms": t_max_ms, "pairs_all": int(pairs_all), "B_all": int(B_all), "build_s": build_s,
             "P_rank": P, "M_rank": M}
@@ -491,7 +492,8 @@ def _run_c3_multi(a, w, rank, world_size, local_rank, dev, gen_s):
             def bail():
                 if rank == 0:
                     print(json.dumps(line()), flush=True)
-                os._exit(0)
+                print(f"rank {rank}: the {f} form did not finish in 120 s", file=sys.stderr, flush=True)
+                os._exit(3)  # the headline stands, the run does not pass as clean
             dog = threading.Timer(120.0, bail)  # the cube form takes ~10 s when it works
             dog.daemon = True
             dog.start()
@@ -511,7 +513,7 @@ def _run_c3_multi(a, w, rank, world_size, local_rank, dev, gen_s):
                 out = line()
                 out.setdefault("extra", {})["cube_hash" if f == "cube" else "replicated_table"] = {"error": repr(e)}
                 print(json.dumps(out), flush=True)
-            os._exit(0)
+            os._exit(3)  # the headline line stands; the failed form makes the run's status non-zero
         if dog:
             dog.cancel()
     if "replicate" in res and "cube" in res:

@@ -130,7 +130,9 @@ int wq_multi_mode(wq_router* h, int* mode);
 /* The scaling form of a multi-GPU tick: every device routes the messages it ingested and keeps its
  * CSR (no pair crosses to devices[0]). in[g] = the messages on devices[g] (device pointers there,
  * complete before the call; keys or positions as wq_route_tick); out[g] = views into the handle's
- * workspace on devices[g], valid until the next call on the handle: offsets[n_msgs + 1] (from 0),
+ * workspace on devices[g] (a staging of their own), valid until the next wq_route_tick_slices_device
+ * call on the handle or its destruction — every other call (routes, queries, op batches) leaves
+ * them intact: offsets[n_msgs + 1] (from 0),
  * peers[n_pairs], msgs[n_pairs] (the index within the slice; NULL unless with_msgs). Per message
  * the recipients are exactly wq_route_tick's for the same message on one table. Synchronous. */
 typedef struct wq_msg_slice {

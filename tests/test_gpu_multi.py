@@ -192,6 +192,81 @@ def test_multi_slices_stay_on_their_devices(G, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
+def test_multi_slice_views_survive_other_calls(mode):
+    """the views of wq_route_tick_slices_device live in a staging of their own, so every
+    other call on the handle — a full route, the read-only queries (area_map.rs:33-67), stats, a
+    GlobalMessage, even an op batch — leaves them intact until the next slices call."""
+    import torch
+    from worldql_server_amd.router import Router
+    w, churn = _workload()
+    G = 3
+    r = Router.multi(16, [0] * G, mode=mode)
+    o = orc.COracle(16)
+    r.apply_ops(w.ops)
+    o.apply_ops(w.ops)
+    sl = _dev_slices(w, G, torch.device("cuda:0"))
+    views = r.route_slices_device([(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), hi - lo)
+                                   for lo, hi, t in sl], with_msgs=True)
+    want = [o.route(w.pos[lo:hi], w.world[lo:hi], w.sender[lo:hi], w.repl[lo:hi])[:2] for lo, hi, _ in sl]
+    # everything else the handle offers, in between
+    r.route(w.pos[::-1].copy(), w.world[::-1].copy(), w.sender[::-1].copy(), w.repl[::-1].copy(), with_msgs=True)
+    ops = w.ops[::41]
+    r.is_subscribed(ops["world"], ops["peer"], False, ops["pos"])
+    r.is_subscribed_any(np.zeros(50, np.uint32), np.arange(50, dtype=np.uint32))
+    r.world_peers(1)
+    r.stats()
+    r.route_global(np.array([0, 1], np.uint32), np.array([1, 2], np.uint32), np.array([0, 0], np.uint8))
+    r.apply_ops(churn)
+    torch.cuda.synchronize()
+    for (lo, hi, _), v, (w_offs, w_peers) in zip(sl, views, want):
+        offs, peers, msgs = _view_arrays(v)
+        assert (offs == w_offs).all() and (peers == w_peers).all()
+        assert (msgs == np.repeat(np.arange(hi - lo, dtype=np.uint32), np.diff(w_offs.astype(np.int64)))).all()
+    r.close()
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_multi_device_batches_back_to_back(mode):
+    """device batches issued back to back, each larger than the last (the handle's
+    staging grows while the sub-handles may still copy the previous batch out of it), each caller
+    buffer rewritten on the handle's stream right after its call; the table must end as the oracle's."""
+    import torch
+    from worldql_server_amd.router import Router
+    w, churn = _workload()
+    G = 3
+    r = Router.multi(16, [0] * G, mode=mode)
+    stream = torch.cuda.Stream()
+    r.set_stream(stream.cuda_stream)
+    o = orc.COracle(16)
+    r.apply_ops(w.ops)
+    o.apply_ops(w.ops)
+    sub_unsub = churn[churn["kind"] != abi.OP_REMOVE_PEER]
+    rng = np.random.default_rng(7)
+    more = w.ops[rng.choice(len(w.ops), 6000, replace=False)].copy()
+    more["kind"] = abi.OP_UNSUBSCRIBE
+    more["kind"][::2] = abi.OP_SUBSCRIBE
+    more["peer"] = rng.integers(0, 2500, len(more))
+    allops = abi.concat_ops([sub_unsub, more])
+    bounds = [0, 100, 400, 1200, 3000, len(allops)]
+    dev = torch.device("cuda:0")
+    with torch.cuda.stream(stream):
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            part = np.ascontiguousarray(allops[a:b])
+            d = torch.from_numpy(part.view(np.uint8).copy()).to(dev, non_blocking=False)
+            stream.synchronize()
+            r.apply_ops_device(d.data_ptr(), len(part))
+            d.fill_(0xAB)  # the caller reuses its buffer as soon as its stream has passed the call
+            o.apply_ops(part)
+    stream.synchronize()
+    want_offs, want_peers, _ = o.route(w.pos, w.world, w.sender, w.repl)
+    offs, peers, _ = r.route(w.pos, w.world, w.sender, w.repl)
+    assert (offs == want_offs).all() and (peers == want_peers).all()
+    assert r.route_health() == (0, 0)
+    assert r.stats()["n_entries"] == o.counts()[0]
+    r.close()
+
+
+@pytest.mark.parametrize("mode", MODES)
 def test_multi_device_batches(mode):
     """wq_apply_ops_device on a multi handle keeps the single-GPU contract: a valid batch
     is applied (cube hash: partitioned by owner on devices[0]; replicate: on every replica,

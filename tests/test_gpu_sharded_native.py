@@ -319,10 +319,14 @@ def _run_procs(G, mode):
     return dict(out)
 
 
-def test_callback_exchange_gloo_two_processes():
-    res = _run_procs(2, "callback")
-    assert [res[k][0] for k in range(2)] == ["ok", "ok"], res
-    assert res[0][1] + res[1][1] > 0
+@pytest.mark.parametrize("G", [2, 3])
+def test_callback_exchange_gloo_processes(G):
+    """The native slot tick across G processes (one per shard, all on cuda:0) whose exchange is the
+    caller's own gloo all-to-all (wq_shard_attach_exchange) — the multi-process form of the product
+    path, as one process per GPU runs it."""
+    res = _run_procs(G, "callback")
+    assert [res[k][0] for k in range(G)] == ["ok"] * G, res
+    assert sum(res[k][1] for k in range(G)) > 0
 
 
 def test_rccl_exchange_one_rank():
@@ -588,6 +592,67 @@ def test_hub_budgeted_ticks_grow_and_redo():
             _check(g, _expected([w.ops], w, a, b), b - a)
         # tick 1 exact; 2 budgeted; 3 budgeted, outgrown, redone exact; 4 and 5 budgeted
         assert (exact, budgeted) == (2, 4), (exact, budgeted)
+    for r in routers:
+        r.close()
+    hub.close()
+
+
+def test_hub_segment_exactly_at_its_budget():
+    """a (source, owner) segment whose slot count equals its budget exactly — every
+    slot fit — must keep its last slot (slot_pad_kernel pads from the count, not from budget - 1).
+    Shard 0 ingests messages that shard 1 owns: 512 on the first (exact: budget = whole blocks of the
+    count = 512) tick, then 1,024 = slot_budget(512) on a budgeted tick; each checked per message."""
+    import torch
+    from worldql_server_amd.router import Hub, Router
+    G = 2
+    rng = np.random.default_rng(47)
+    n_peers = 400
+    centre = rng.uniform(-40.0, 40.0, (n_peers, 3))
+    nb = np.array([[dx, dy, dz] for dx in (-1, 0, 1) for dy in (-1, 0, 1) for dz in (-1, 0, 1)], np.float64)
+    sub = (centre[:, None, :] + 16.0 * nb[None]).reshape(-1, 3)
+    ops = abi.ops_array(np.zeros(len(sub), np.uint32), np.repeat(np.arange(n_peers, dtype=np.uint32), 27),
+                        np.zeros(len(sub), np.uint8), pos=sub)
+    cand = rng.uniform(-56.0, 56.0, (20000, 3))
+    probe = Router(16, 0)
+    owner = probe.shard_ops(abi.ops_array(np.zeros(len(cand), np.uint32), np.zeros(len(cand), np.uint32),
+                                          np.zeros(len(cand), np.uint8), pos=cand), G)
+    probe.close()
+    remote = cand[owner == 1]
+    local = cand[owner == 0]
+    assert len(remote) >= 1536 + 300 and len(local) >= 100
+
+    def msgs(pos):
+        n = len(pos)
+        return type("W", (), {"pos": np.ascontiguousarray(pos), "world": np.zeros(n, np.uint32),
+                              "sender": rng.integers(0, n_peers, n).astype(np.uint32),
+                              "repl": rng.integers(0, 3, n).astype(np.uint8), "cube_size": 16})
+    # shard 0: 512 remote (+ own) then 1,024 remote (+ own); shard 1: its own slices
+    t0 = [msgs(np.concatenate([remote[:512], local[:100]])), msgs(np.concatenate([local[100:150], remote[512:1536]]))]
+    t1 = [msgs(remote[1536:1736]), msgs(remote[1736:1836])]
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    results = [None] * G
+
+    def body(rank):
+        r = routers[rank]
+        r.attach_hub(hub, rank)
+        r.sharded_apply_ops(ops)
+        ticks = t0 if rank == 0 else t1
+        got = [_tick(r, w, 0, len(w.world), dev) for w in ticks]
+        results[rank] = (got, r.shard_tick_stats())
+
+    _run_shards(G, body)
+    for rank in range(G):
+        got, stats = results[rank]
+        # the first tick exact, the second on budgets (a pool that outgrew its budget would redo it
+        # exactly, with the slot segment again exactly full)
+        assert stats[1] == 1 and stats[0] >= 1, stats
+        for g, w in zip(got, t0 if rank == 0 else t1):
+            M = len(w.world)
+            want = _expected([ops], w, 0, M)
+            assert np.diff(want[0].astype(np.int64)).astype(bool).mean() > 0.5  # most messages have recipients
+            _check(g, want, M)
     for r in routers:
         r.close()
     hub.close()

@@ -50,7 +50,14 @@ struct MultiCtx {
     // (two, alternating: a sub-handle may re-apply its previous batch at its next call)
     std::vector<DevBuf> in, out, ops0, ops1;
     std::vector<uint64_t> cap, P;
+    // wq_route_tick_slices_device's outputs: their own staging, so the views it returns survive every
+    // other call on the handle (routes, queries, op batches) until the next slices call
+    std::vector<DevBuf> vout;
+    std::vector<uint64_t> vcap, vP;
     std::vector<uint32_t> flip;
+    // per sub-handle, recorded on its stream after it copied a device op batch out of m.part: the
+    // next write of m.part (on the handle's stream) waits for every one of them
+    std::vector<hipEvent_t> copied;
     bool any_dirty = true;  // the merged any-keys need rebuilding (an op was applied since)
     DevBuf tmp, cnt, part;  // devices[0] scratch: the any-key merge, the device op partition
     hipEvent_t ready = nullptr;
@@ -193,16 +200,19 @@ int clear_staging_overflow(wq_router* s) {
 // One sub-handle's part of a tick: its messages routed into its output staging (offsets, peers,
 // msgs), grown when the pairs outgrow it. m.P[g] = its pairs. Cube hash: the sharded tick (every
 // sub-handle takes part: it is collective); replicate: the single-GPU tick on the replica.
-int tick_into(wq_router* h, uint32_t g, const SliceIn& x, bool msgs) {
+int tick_into(wq_router* h, uint32_t g, const SliceIn& x, bool msgs, bool view) {
     MultiCtx& m = *h->multi;
     wq_router* s = m.sub[g];
-    if (!m.cap[g]) m.cap[g] = 16 * x.M + 1024;
+    DevBuf& ob = view ? m.vout[g] : m.out[g];
+    uint64_t& capr = view ? m.vcap[g] : m.cap[g];
+    uint64_t& Pr = view ? m.vP[g] : m.P[g];
+    if (!capr) capr = 16 * x.M + 1024;
     for (int attempt = 0; attempt < 3; ++attempt) {
-        const uint64_t cap = m.cap[g];
+        const uint64_t cap = capr;
         size_t op, om;
         out_layout(x.M, cap, &op, &om);
-        WQ_ALLOC(s, m.out[g], om + (msgs ? cap * 4 : 0) + kAlign);
-        char* dout = m.out[g].as<char>();
+        WQ_ALLOC(s, ob, om + (msgs ? cap * 4 : 0) + kAlign);
+        char* dout = ob.as<char>();
         uint32_t* d_off = reinterpret_cast<uint32_t*>(dout);
         uint32_t* d_peers = reinterpret_cast<uint32_t*>(dout + op);
         uint32_t* d_msgs = msgs ? reinterpret_cast<uint32_t*>(dout + om) : nullptr;
@@ -210,15 +220,15 @@ int tick_into(wq_router* h, uint32_t g, const SliceIn& x, bool msgs) {
             size_t P = 0;
             int rc = wq_sharded_route_tick_device(s, x.pos, x.keys, x.world, x.sender, x.repl, x.M, d_off, d_peers,
                                                   d_msgs, cap, &P);
-            m.P[g] = P;
+            Pr = P;
             if (rc == WQ_E_CAPACITY && P > cap && P <= 0xFFFFFFFFull) {
                 // the staging was short: grow it and copy the kept result out again (no re-exchange)
-                m.cap[g] = P + P / 4 + 1024;
-                const uint64_t c2 = m.cap[g];
+                capr = P + P / 4 + 1024;
+                const uint64_t c2 = capr;
                 size_t op2, om2;
                 out_layout(x.M, c2, &op2, &om2);
-                WQ_ALLOC(s, m.out[g], om2 + (msgs ? c2 * 4 : 0) + kAlign);
-                char* d2 = m.out[g].as<char>();
+                WQ_ALLOC(s, ob, om2 + (msgs ? c2 * 4 : 0) + kAlign);
+                char* d2 = ob.as<char>();
                 rc = wq_sharded_copy_out(s, reinterpret_cast<uint32_t*>(d2), reinterpret_cast<uint32_t*>(d2 + op2),
                                          msgs ? reinterpret_cast<uint32_t*>(d2 + om2) : nullptr, c2);
                 if (rc == WQ_OK) rc = clear_staging_overflow(s);
@@ -240,13 +250,13 @@ int tick_into(wq_router* h, uint32_t g, const SliceIn& x, bool msgs) {
         if (c.error & 4u) return set_error(s, WQ_E_TIMEOUT, "route look-back spin gave up");
         if (c.error & 8u) return set_error(s, WQ_E_INVALID, "a replica's table still misses a device batch");
         if (c.error) return set_error(s, WQ_E_CAPACITY, "more than 2^32-1 pairs in one tick");
-        m.P[g] = c.n_pairs;
+        Pr = c.n_pairs;
         // the next tick's shape from this one's fan-out, as the host-array tick does (a replica's
         // device ticks are read back here anyway)
         if (s->fanout_auto && x.M >= 256) s->heavy_fanout = (double)c.n_pairs >= WQ_HEAVY_FANOUT * (double)x.M;
         if (c.n_pairs <= cap) return WQ_OK;
         if (c.n_pairs > 0xFFFFFFFFull) return set_error(s, WQ_E_CAPACITY, "more than 2^32-1 pairs in one tick");
-        m.cap[g] = c.n_pairs + c.n_pairs / 4 + 1024;  // short: grow the staging and route again
+        capr = c.n_pairs + c.n_pairs / 4 + 1024;  // short: grow the staging and route again
         if (int r2 = clear_staging_overflow(s)) return r2;
     }
     return set_error(s, WQ_E_CAPACITY, "replica staging kept growing");
@@ -284,8 +294,8 @@ int shard_copy_back(wq_router* h, uint32_t g, uint64_t lo, uint64_t Mg, uint64_t
     return WQ_OK;
 }
 
-// A device op batch (on devices[0]) to sub-handle g: copied to its alternating staging buffer on
-// its own stream after the caller's stream has produced it, then applied (asynchronously).
+// A device op batch (m.part on devices[0]) to sub-handle g: copied to its alternating staging
+// buffer on its own stream after the handle's stream has produced it, then applied (asynchronously).
 int apply_staged(wq_router* h, uint32_t g, const wq_op* src, size_t n) {
     MultiCtx& m = *h->multi;
     wq_router* s = m.sub[g];
@@ -297,6 +307,7 @@ int apply_staged(wq_router* h, uint32_t g, const wq_op* src, size_t n) {
         WQ_HIP(s, hipMemcpyAsync(st.p, src, n * sizeof(wq_op), hipMemcpyDeviceToDevice, s->stream));
     else
         WQ_HIP(s, hipMemcpyPeerAsync(st.p, m.dev[g], src, h->device, n * sizeof(wq_op), s->stream));
+    WQ_HIP(s, hipEventRecord(m.copied[g], s->stream));  // src (m.part) may be rewritten after this
     return wq_apply_ops_device(s, st.as<wq_op>(), n);
 }
 
@@ -392,15 +403,25 @@ int multi_apply_ops_device(wq_router* h, const wq_op* d_ops, size_t n) {
     if (n >= 0xFFFFFFFFull) return set_error(h, WQ_E_INVALID, "device op batch larger than 2^32 - 1 ops");
     m.any_dirty = true;
     hipStream_t st = h->stream;
+    // m.part is read by the sub-handles' copies of the previous batch: order this batch's writes of it
+    // after them (and wait for them on the host before the buffer may be reallocated)
+    const bool grow = n * sizeof(wq_op) > m.part.bytes;
+    for (uint32_t g = 0; g < G; ++g) {
+        if (grow) WQ_HIP(h, hipEventSynchronize(m.copied[g]));
+        WQ_HIP(h, hipStreamWaitEvent(st, m.copied[g], 0));
+    }
+    WQ_ALLOC(h, m.part, n * sizeof(wq_op));
     if (m.mode == WQ_MULTI_REPLICATE) {
+        // the caller's batch is read once, on the caller's stream; the replicas copy the handle's
+        // staging (so the caller may reuse d_ops as soon as its stream has passed this call)
+        WQ_HIP(h, hipMemcpyAsync(m.part.p, d_ops, n * sizeof(wq_op), hipMemcpyDeviceToDevice, st));
         WQ_HIP(h, hipEventRecord(m.ready, st));
-        return run_all(h, [&](uint32_t g) { return apply_staged(h, g, d_ops, n); });
+        return run_all(h, [&](uint32_t g) { return apply_staged(h, g, m.part.as<wq_op>(), n); });
     }
     WQ_ALLOC(h, h->key32_a, n * 4);
     WQ_ALLOC(h, h->key32_b, n * 4);
     WQ_ALLOC(h, h->idx_a, n * 4);
     WQ_ALLOC(h, h->idx_b, n * 4);
-    WQ_ALLOC(h, m.part, n * sizeof(wq_op));
     WQ_ALLOC(h, m.cnt, 4 * (WQ_MAX_SHARDS + 1));
     uint32_t* owner = h->key32_a.as<uint32_t>();
     uint32_t* cnt = m.cnt.as<uint32_t>();
@@ -472,7 +493,7 @@ int multi_route_tick(wq_router* h, const double* pos, const int64_t* keys, const
                   use_keys ? reinterpret_cast<const int64_t*>(din) : nullptr,
                   reinterpret_cast<const uint32_t*>(din + o_w), reinterpret_cast<const uint32_t*>(din + o_s),
                   reinterpret_cast<const uint8_t*>(din + o_r), Mg};
-        return tick_into(h, g, x, msgs != nullptr);
+        return tick_into(h, g, x, msgs != nullptr, false);
     });
     if (rc) return rc;
     std::vector<uint64_t> base(G + 1, 0);
@@ -511,18 +532,18 @@ int multi_route_slices(wq_router* h, const wq_msg_slice* in, int with_msgs, wq_s
     int rc = run_all(h, [&](uint32_t g) -> int {
         const wq_msg_slice& x = in[g];
         SliceIn si{x.d_keys ? nullptr : x.d_pos, x.d_keys, x.d_world, x.d_sender, x.d_repl, x.n_msgs};
-        return tick_into(h, g, si, with_msgs != 0);
+        return tick_into(h, g, si, with_msgs != 0, true);
     });
     if (rc) return rc;
     for (uint32_t g = 0; g < m.G; ++g) {
         size_t op, om;
-        out_layout(in[g].n_msgs, m.cap[g], &op, &om);
-        const char* d = m.out[g].as<char>();
+        out_layout(in[g].n_msgs, m.vcap[g], &op, &om);
+        const char* d = m.vout[g].as<char>();
         wq_slice_view& v = out[g];
         v.device = m.dev[g];
         v.pad_ = 0;
         v.n_msgs = in[g].n_msgs;
-        v.n_pairs = m.P[g];
+        v.n_pairs = m.vP[g];
         v.offsets = reinterpret_cast<const uint32_t*>(d);
         v.peers = reinterpret_cast<const uint32_t*>(d + op);
         v.msgs = with_msgs ? reinterpret_cast<const uint32_t*>(d + om) : nullptr;
@@ -619,6 +640,8 @@ void multi_release(wq_router* h) {
         if (m->sub[g]) (void)hipStreamSynchronize(m->sub[g]->stream);
         m->in[g].release();
         m->out[g].release();
+        m->vout[g].release();
+        if (m->copied[g]) (void)hipEventDestroy(m->copied[g]);
         m->ops0[g].release();
         m->ops1[g].release();
         if (m->sub[g]) wq_router_destroy(m->sub[g]);
@@ -659,6 +682,10 @@ extern "C" int wq_router_create_multi_mode(uint16_t cube_size, int n_gpus, const
     m->sub.assign(G, nullptr);
     m->in.resize(G);
     m->out.resize(G);
+    m->vout.resize(G);
+    m->vcap.assign(G, 0);
+    m->vP.assign(G, 0);
+    m->copied.assign(G, nullptr);
     m->ops0.resize(G);
     m->ops1.resize(G);
     m->cap.assign(G, 0);
@@ -669,6 +696,11 @@ extern "C" int wq_router_create_multi_mode(uint16_t cube_size, int n_gpus, const
     if (rc == WQ_OK && mode == WQ_MULTI_CUBE_HASH) rc = wq_hub_create(G, &m->hub);
     for (uint32_t g = 0; g < G && rc == WQ_OK; ++g) {
         rc = wq_router_create(cube_size, devices[g], &m->sub[g]);
+        if (rc == WQ_OK) {  // recorded on sub-handle g's stream: created on its device
+            (void)hipSetDevice(devices[g]);
+            if (hipEventCreateWithFlags(&m->copied[g], hipEventDisableTiming) != hipSuccess) rc = WQ_E_HIP;
+            else (void)hipEventRecord(m->copied[g], m->sub[g]->stream);  // complete from the start
+        }
         if (rc == WQ_OK && mode == WQ_MULTI_CUBE_HASH) rc = wq_shard_attach_hub(m->sub[g], m->hub, g);
         if (rc) h->err = std::string("device ") + std::to_string(g) + ": " + wq_last_error(m->sub[g]);
     }

@@ -93,8 +93,8 @@ const Cfg kCfgs[] = {
 #undef WQ_CFG3
 #undef WQ_CFG3H
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
-constexpr int kCfgHeavy = 10;
-constexpr uint32_t kShortTickTiles = 12288;  // 256-message tiles up to which a tick is "short" (above)  // the default shape under wq_set_fanout_hint >= WQ_HEAVY_FANOUT (emit_map_kernel)
+constexpr int kCfgHeavy = 10;                // the default shape under wq_set_fanout_hint >= WQ_HEAVY_FANOUT (emit_map_kernel)
+constexpr uint32_t kShortTickTiles = 12288;  // 256-message tiles up to which a tick is "short" (above)
 
 }  // namespace
 

@@ -489,7 +489,9 @@ __global__ void __launch_bounds__(kBlock)
     const uint32_t d = blockIdx.y;
     if (d >= G) return;
     const uint32_t B = L.budget[d], n = a[2 * d];
-    const uint32_t from = n < B ? n : (B ? B - 1 : 0);
+    // n == B: every slot fit, nothing of the segment is overwritten; n > B: the last slot may be a
+    // head whose tail did not fit, so it becomes a tail too (the tick is redone)
+    const uint32_t from = n <= B ? n : (B ? B - 1 : 0);
     for (uint32_t j = from + blockIdx.x * kBlock + threadIdx.x; j < B; j += gridDim.x * kBlock) {
         const uint32_t slot = L.base[d] + j;
         uint32_t* o = out + (uint64_t)kSlotWords * slot;

@@ -213,7 +213,7 @@ class Router:
     def route_slices_device(self, slices, with_msgs: bool = False):
         """wq_route_tick_slices_device: slices = one (pos_ptr, world_ptr, sender_ptr, repl_ptr, n_msgs
         [, keys_ptr]) per device of the handle, on that device. Returns a list of abi.SliceView (device
-        pointers into the handle's workspace, valid until its next call)."""
+        pointers into the handle's workspace, valid until its next route_slices_device call)."""
         G = len(slices)
         ins = (abi.MsgSlice * G)()
         for g, sl in enumerate(slices):
@@ -331,7 +331,7 @@ class Router:
                                                   connected_ptr or None, n_peers, peer_offsets_ptr,
                                                   msgs_out_ptr or None))
 
-    # ---- multi-GPU (cube-hash ownership; driven by sharded.py) ----
+    # ---- multi-GPU (cube-hash ownership: wq_sharded.hip) ----
     def shard_ops(self, ops: np.ndarray, n_shards: int) -> np.ndarray:
         """Owner shard of each op (abi.SHARD_ALL for REMOVE_PEER)."""
         ops = np.ascontiguousarray(ops, dtype=abi.OP_DTYPE)
