@@ -430,6 +430,11 @@ int wq_debug_update_counts(wq_router* h, uint64_t* incremental, uint64_t* rebuil
 /* ---- tuning hook: select a compiled route-kernel shape (messages per thread, expansion chunk);
  * 0 is the default. Results are identical for every shape. */
 int wq_debug_set_route_config(wq_router* h, int cfg);
+/* ---- tuning hook: the heavy-fan-out tick (count / scan / emit) in `chunks` pipelined chunks — the
+ * chunks' counts on a side stream, each chunk's scan and emit on the launch stream as soon as its
+ * count is done (0 = the default; 1 = one chunk). Applies to ticks of >= 2 chunks of at most 8,192
+ * count tiles each. Results are identical for every value. */
+int wq_debug_set_route_chunks(wq_router* h, int chunks);
 /* The tick shape the next default-config tick takes (heavy_fanout = count / scan / emit) and
  * whether it is still chosen automatically (no hint set, or reset by a negative hint). */
 int wq_debug_route_shape(wq_router* h, int* heavy_fanout, int* fanout_auto);

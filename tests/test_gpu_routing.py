@@ -405,3 +405,48 @@ def test_auto_fanout_shape_from_host_ticks():
     assert r.route_shape() == (True, False)  # the caller's hint holds
     r.set_fanout_hint(-1.0)
     assert r.route_shape()[1] is True  # a negative hint hands the choice back
+
+
+@pytest.mark.parametrize("chunks", [2, 3, 7])
+def test_pipelined_heavy_tick_is_identical(chunks):
+    """wq_debug_set_route_chunks: the heavy tick in pipelined chunks (counts on a side stream, each
+    chunk's scan carrying {P, F} into the next, its emit writing msgs from the chunk's first message)
+    gives the oracle's CSR and msgs, and the same counters as one chunk — host arrays, device arrays,
+    a capacity too small, and a tick too short to chunk."""
+    import torch
+    from worldql_server_amd import synth_ext
+    w = synth_ext.config_c3(scale=0.02)  # 200k hotspot messages, 782 count tiles
+    M = len(w.world)
+    repl = synth.stream(3, 99).below(3, M).astype(np.uint8)
+    r = mk_router(16)
+    r.apply_ops(w.ops)
+    r.set_fanout_hint(40.0)
+    o = orc.COracle(16)
+    o.apply_ops(w.ops)
+    r.set_route_chunks(chunks)
+    P = _compare(r, o, w.pos, w.world, w.sender, repl)
+    _compare(r, o, w.pos[:300], w.world[:300], w.sender[:300], repl[:300])  # 2 tiles: one chunk
+    dev = torch.device("cuda:0")
+    t = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (w.pos, w.world.view(np.int32),
+                                                                      w.sender.view(np.int32), repl)]
+    got = {}
+    for c in (1, chunks):
+        r.set_route_chunks(c)
+        for cap in (P + 64, P // 3):
+            offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
+            peers = torch.full((P + 64,), -1, dtype=torch.int32, device=dev)
+            msgs = torch.full((P + 64,), -1, dtype=torch.int32, device=dev)
+            cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize()
+            r.route_device(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), M, offs.data_ptr(),
+                           peers.data_ptr(), msgs.data_ptr(), cap, cnt.data_ptr())
+            torch.cuda.synchronize()
+            k = cnt.cpu().numpy().view(abi.COUNTERS_DTYPE)[0]
+            got[(c, cap)] = (offs.cpu().numpy(), peers.cpu().numpy(), msgs.cpu().numpy(), int(k["n_pairs"]),
+                             int(k["n_candidates"]), int(k["overflow"]), int(k["error"]))
+        r.route_health()
+    for cap in (P + 64, P // 3):
+        a, b = got[(1, cap)], got[(chunks, cap)]
+        assert a[3:] == b[3:] and a[3] == P, (a[3:], b[3:])
+        assert (a[0] == b[0]).all() and (a[1] == b[1]).all() and (a[2] == b[2]).all()
+    assert got[(1, P // 3)][5] == 1  # the short capacity is reported, the kept prefix identical

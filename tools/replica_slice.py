@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--skip-full", action="store_true", help="skip the N = 1 line (profiling one slice size)")
     ap.add_argument("--cfg", type=int, default=0, help="route config (wq_debug_set_route_config; 0 = default)")
+    ap.add_argument("--chunks", type=int, default=0, help="pipelined heavy-tick chunks (wq_debug_set_route_chunks)")
     a = ap.parse_args()
     import torch
     import bench
@@ -41,6 +42,8 @@ def main():
     r.set_stream(stream.cuda_stream)
     if a.cfg:
         r.set_route_config(a.cfg)
+    if a.chunks:
+        r.set_route_chunks(a.chunks)
     t0 = time.perf_counter()
     r.apply_ops(w.ops)
     build_s = time.perf_counter() - t0

@@ -22,6 +22,7 @@ struct EmitParams {
     uint32_t* msgs;
     uint64_t capacity;
     uint32_t n_blocks = 0;  // emit_map_kernel: 256-message blocks (grid stride when > gridDim.x)
+    uint32_t msg_base = 0;  // emit_map_kernel: msgs[] = msg_base + the message's index here (a chunk's first message)
     // emit_map_kernel in the sharded tick: rows whose info.x carries kLocPool read the received
     // cube-list pool at that word offset (wq_sharded.hip); nullptr everywhere else
     const uint32_t* pool = nullptr;
@@ -586,7 +587,7 @@ __global__ __launch_bounds__(kBlock) void emit_map_kernel(EmitParams p) {
             const uint64_t o = (uint64_t)g + r;
             if (r < T && o < p.capacity) {
                 p.peers[o] = peer[u];
-                if (p.msgs) p.msgs[o] = m0 + own[u];
+                if (p.msgs) p.msgs[o] = p.msg_base + m0 + own[u];
             }
         }
         lds_barrier();  // the next window rewrites the map

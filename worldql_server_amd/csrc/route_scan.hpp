@@ -27,6 +27,11 @@ struct TileScanParams {
     wq_route_counters* cnt;
     uint32_t* health;  // sticky {error, overflow} words (flag_route)
     const uint32_t* stale = nullptr;  // the table's stale word (check_stale)
+    // a tick scanned in chunks (wq_route.hip's pipelined heavy tick): bit 0 = start from carry[0..1]
+    // ({P, F} of the chunks before), bit 1 = hand {P, F} on in carry (not the last chunk: no
+    // offsets[M], no counters)
+    uint64_t* carry = nullptr;
+    uint32_t chunk = 0;
 };
 
 // Inclusive wave64 prefix sum of u32 by DPP row shifts and row broadcasts (no LDS round trips).
@@ -54,7 +59,11 @@ static __global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScan
     __shared__ uint64_t s_tot[kScanWaves];
     __shared__ uint64_t s_F[kScanWaves];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint64_t carry = 0, F = 0;
+    uint64_t carry = 0, F = 0, F0 = 0;
+    if (p.chunk & 1u) {
+        carry = p.carry[0];
+        F0 = p.carry[1];
+    }
     for (uint32_t base = 0; base < p.n_tiles; base += kScanThreads * kScanRows) {
         const uint32_t c0 = base + (uint32_t)wave * (64 * kScanRows) + lane;
         uint32_t v[kScanRows];
@@ -100,9 +109,14 @@ static __global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScan
     if (lane == 0) s_F[wave] = F;
     __syncthreads();
     if (tid == 0) {
-        uint64_t Ft = 0;
+        uint64_t Ft = F0;
 #pragma unroll
         for (int u = 0; u < kScanWaves; ++u) Ft += s_F[u];
+        if (p.chunk & 2u) {  // a chunk before the last: {P, F} so far to the next chunk's scan
+            p.carry[0] = carry;
+            p.carry[1] = Ft;
+            return;
+        }
         p.cnt->n_candidates = Ft;
         const uint64_t P = carry;
         p.offsets[p.M] = (uint32_t)P;

@@ -110,6 +110,12 @@ struct RouteWs {
     DevBuf scan_tmp;  // rocPRIM temporary storage of the many-tile scan (launch_tile_scan)
     uint64_t agg_zeroed = 0;
     uint64_t* stamps = nullptr;  // wq_debug_set_timeline
+    // the pipelined heavy tick (wq_route.hip, short ticks): count chunks on `side` while the launch
+    // stream scans and emits the previous chunk; {P, F} carried across the chunks' scans
+    hipStream_t side = nullptr;
+    hipEvent_t ev_in = nullptr;
+    std::vector<hipEvent_t> cev;
+    DevBuf carry;
     uint64_t calls = 0;
     wq_route_counters* last = nullptr;  // counters of the most recent call (device)
 };
@@ -161,6 +167,7 @@ struct wq_router {
     // sharded ticks (wq_shard.hip): owner histograms, unpacked received records
     wq::DevBuf shard_hist, rec_keys, rec_w, rec_s, rec_r;
     int route_cfg = 0;  // route kernel shapes (wq_route.hip kCfgs)
+    uint32_t route_chunks = 0;  // wq_debug_set_route_chunks: chunks of the pipelined heavy tick (0 = default)
     bool heavy_fanout = false;  // wq_set_fanout_hint: default shape -> kCfgHeavy
     bool fanout_auto = true;    // until wq_set_fanout_hint: wq_route_tick sets heavy_fanout from its P / M
     // host-pointer convenience buffers

@@ -241,6 +241,102 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     uint32_t* tile_prefix = tile_total + n_count;
     uint32_t* tile_F = tile_prefix + n_count;
 
+    // Pipelined heavy tick: the messages in C chunks of whole count tiles; the chunks' counts run
+    // back to back on a side stream while the launch stream scans and emits the chunks before them
+    // (the scans carry {P, F} from chunk to chunk), so a latency-bound count overlaps a
+    // bandwidth-bound emit. WQ_ROUTE_CHUNKS sets C (1 = the plain three launches).
+    static const uint32_t chunks_env =
+        getenv("WQ_ROUTE_CHUNKS") ? (uint32_t)std::max(1, atoi(getenv("WQ_ROUTE_CHUNKS"))) : 1u;
+    const uint32_t want = h->route_chunks ? h->route_chunks : chunks_env;
+    const uint32_t nchunk = (!radius && cfg.emit_heavy == 116 && count_tile == (uint32_t)kBlock && want > 1 &&
+                             n_count >= 2 * want && (n_count + want - 1) / want <= kScanOneBlockMax)
+                                ? want
+                                : 1u;
+    if (nchunk > 1) {
+        if (!rw.side) WQ_HIP(h, hipStreamCreateWithFlags(&rw.side, hipStreamNonBlocking));
+        if (!rw.ev_in) WQ_HIP(h, hipEventCreateWithFlags(&rw.ev_in, hipEventDisableTiming));
+        while (rw.cev.size() < nchunk) {
+            hipEvent_t ev;
+            WQ_HIP(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            rw.cev.push_back(ev);
+        }
+        WQ_ALLOC(h, rw.carry, 16);
+        // the side stream starts where the caller's stream is: inputs complete, the previous tick's
+        // emit (which read e / info) done
+        WQ_HIP(h, hipEventRecord(rw.ev_in, s));
+        WQ_HIP(h, hipStreamWaitEvent(rw.side, rw.ev_in, 0));
+        auto bounds = [&](uint32_t c, uint32_t* t0, uint32_t* t1, uint64_t* lo, uint64_t* hi) {
+            *t0 = (uint32_t)((uint64_t)n_count * c / nchunk);
+            *t1 = (uint32_t)((uint64_t)n_count * (c + 1) / nchunk);
+            *lo = (uint64_t)*t0 * kBlock;
+            *hi = std::min<uint64_t>(M, (uint64_t)*t1 * kBlock);
+        };
+        for (uint32_t c = 0; c < nchunk; ++c) {
+            uint32_t t0, t1;
+            uint64_t lo, hi;
+            bounds(c, &t0, &t1, &lo, &hi);
+            CountParams cp;
+            cp.in = RouteIn{d_pos ? d_pos + 3 * lo : nullptr, d_keys ? d_keys + 3 * lo : nullptr, d_world + lo,
+                            d_sender + lo, d_repl + lo, (uint32_t)(hi - lo), (int64_t)h->cube_size};
+            cp.t = tv;
+            cp.e = rw.e.as<uint32_t>() + lo;
+            cp.info = rw.info.as<uint2>() + lo;
+            cp.tile_total = tile_total + t0;
+            cp.tile_F = tile_F + t0;
+            cp.cnt = cur;
+            cp.cnt_next = nxt;
+            cp.health = route_health(h);
+            cp.n_tiles = t1 - t0;
+            cfg.count(cp, rw.side, t1 - t0);
+            WQ_HIP(h, hipGetLastError());
+            WQ_HIP(h, hipEventRecord(rw.cev[c], rw.side));
+        }
+        for (uint32_t c = 0; c < nchunk; ++c) {
+            uint32_t t0, t1;
+            uint64_t lo, hi;
+            bounds(c, &t0, &t1, &lo, &hi);
+            WQ_HIP(h, hipStreamWaitEvent(s, rw.cev[c], 0));
+            TileScanParams sp;
+            sp.tile_total = tile_total + t0;
+            sp.tile_F = tile_F + t0;
+            sp.tile_prefix = tile_prefix + t0;
+            sp.n_tiles = t1 - t0;
+            sp.offsets = d_offsets;
+            sp.M = (uint32_t)M;
+            sp.capacity = capacity;
+            sp.cnt = cur;
+            sp.health = route_health(h);
+            sp.stale = tv.stale;
+            sp.carry = rw.carry.as<uint64_t>();
+            sp.chunk = (c > 0 ? 1u : 0u) | (c + 1 < nchunk ? 2u : 0u);
+            hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, sp);
+            EmitParams ep;
+            ep.sender = d_sender + lo;
+            ep.pos = d_pos ? d_pos + 3 * lo : nullptr;
+            ep.repl = d_repl + lo;
+            ep.M = (uint32_t)(hi - lo);
+            ep.t = tv;
+            ep.e = rw.e.as<uint32_t>() + lo;
+            ep.tile_prefix = tile_prefix + t0;
+            ep.count_tile = count_tile;
+            ep.offsets = d_offsets + lo;
+            ep.info = rw.info.as<uint2>() + lo;
+            ep.peers = capacity ? d_peers : nullptr;
+            ep.msgs = d_msgs;
+            ep.capacity = capacity;
+            ep.n_blocks = t1 - t0;
+            ep.msg_base = (uint32_t)lo;
+            hipLaunchKernelGGL((emit_map_kernel<16>), dim3(t1 - t0), dim3(kBlock), 0, s, ep);
+            WQ_HIP(h, hipGetLastError());
+        }
+        if (pr.enabled) {
+            WQ_HIP(h, hipEventRecord(pr.stop[pr.used], s));
+            pr.used++;
+        }
+        rw.calls++;
+        return WQ_OK;
+    }
+
     CountParams cp;
     cp.in = in;
     cp.t = tv;

@@ -143,9 +143,13 @@ int wq_router_destroy(wq_router* h) {
                       &h->cube_start, &h->rws.buf, &h->rws.info, &h->rws.e, &h->rws.tiles,
                       &h->h_in, &h->h_out, &h->tab.recs, &h->tab.rclaim, &h->tab.pbox, &h->shard_hist,
                       &h->rec_keys, &h->rec_w, &h->rec_s, &h->rec_r, &h->ppos, &h->ppos4, &h->pcode, &h->qbox, &h->rws.agg, &h->rws.spill, &h->rws.scan_tmp,
+                      &h->rws.carry, &h->tab.hdr, &h->dws.sort_cnt, &h->dws.sort_tot,
                       &h->dws.part, &h->dws.summ, &h->dws.dstat, &h->dws.rm_bits, &h->tab.stale};
     for (DevBuf* b : bufs) b->release();
     if (h->pend.ev) (void)hipEventDestroy(h->pend.ev);
+    for (auto e : h->rws.cev) (void)hipEventDestroy(e);
+    if (h->rws.ev_in) (void)hipEventDestroy(h->rws.ev_in);
+    if (h->rws.side) (void)hipStreamDestroy(h->rws.side);
     if (h->pend.pinned) (void)hipHostFree(h->pend.pinned);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -365,6 +369,12 @@ int wq_route_health(wq_router* h, uint32_t* error_bits, uint32_t* overflow) {
 int wq_debug_set_route_config(wq_router* h, int cfg) {
     if (!h || cfg < 0 || cfg >= route_config_count()) return WQ_E_INVALID;
     h->route_cfg = cfg;
+    return WQ_OK;
+}
+
+int wq_debug_set_route_chunks(wq_router* h, int chunks) {
+    if (!h || chunks < 0 || chunks > 64) return WQ_E_INVALID;
+    h->route_chunks = (uint32_t)chunks;
     return WQ_OK;
 }
 

@@ -82,6 +82,7 @@ def load_library(build_if_missing: bool = True):
         "wq_debug_set_hash_bits": ([vp, i32], i32),
         "wq_debug_set_record_slack": ([vp, u32], i32),
         "wq_debug_set_route_config": ([vp, i32], i32),
+        "wq_debug_set_route_chunks": ([vp, i32], i32),
         "wq_debug_route_config_count": ([], i32),
         "wq_debug_set_timeline": ([vp, vp], i32),
         "wq_debug_update_counts": ([vp] + [ctypes.POINTER(ctypes.c_uint64)] * 3, i32),
@@ -518,6 +519,10 @@ class Router:
 
     def set_route_config(self, cfg: int) -> None:
         self._check(self.lib.wq_debug_set_route_config(self.h, cfg))
+
+    def set_route_chunks(self, chunks: int) -> None:
+        """Chunks of the pipelined heavy tick (wq_debug_set_route_chunks; 0 = default)."""
+        self._check(self.lib.wq_debug_set_route_chunks(self.h, chunks))
 
     # ---- instrumentation ----
     def profile_enable(self, on: bool = True) -> None:
