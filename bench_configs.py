@@ -390,19 +390,22 @@ def _c3_cube(a, w, rank, world_size, local_rank, dev, stream, sl, owner_form: bo
     cap = 64 * M + 1024
     peers = torch.empty(cap, dtype=torch.int32, device=dev)
     msgs = torch.empty(cap, dtype=torch.int32, device=dev)
-    state = {"P": 0}
+    cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
 
     def tick():
-        rc, P = r.sharded_route_device(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M,
-                                       offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap)
-        assert rc == 0, (rc, P)
-        state["P"] = P
+        # wq_sharded_route_tick_async: no end-of-tick read (the next tick's budgets come from the
+        # tick before); P and the status bits land in cnt, every tick's bits in the sticky health
+        # words that timed_ticks checks afterwards
+        r.sharded_route_async(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M,
+                              offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap, cnt.data_ptr())
 
-    for _ in range(max(a.warmup, 1)):
+    for _ in range(max(a.warmup, 2)):
         tick()
     t_ms = timed_ticks(tick, a.steps, stream, dev, world_size, [r])
+    c = _counters(cnt)[0]
+    assert c["error"] == 0 and c["overflow"] == 0, c
     exact, budgeted = r.shard_tick_stats()
-    t_max_ms, pairs_all = reduce_over_ranks(t_ms, state["P"], dev, world_size)
+    t_max_ms, pairs_all = reduce_over_ranks(t_ms, int(c["n_pairs"]), dev, world_size)
     sent, _ = r.shard_last_bytes()  # the last timed tick's bytes to the other GPUs (xGMI)
     sent_max, _ = reduce_over_ranks(float(sent), 0, dev, world_size)
     out = {"t_max_ms": t_max_ms, "pairs_all": int(pairs_all), "build_s": build_s,
@@ -862,24 +865,25 @@ def _run_c5_sharded(a, rank, world_size, local_rank, dev):
     peers = torch.empty(cap, dtype=torch.int32, device=dev)
     msgs = torch.empty(cap, dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
-    state = {"i": 0, "P": 0}
+    state = {"i": 0}
+    cnt = torch.zeros((a.warmup + a.steps, 24), dtype=torch.uint8, device=dev)
 
     def one():
         i = state["i"]
         r.apply_ops_device(own_ops[i].data_ptr(), int(own_ops[i].shape[0]) // 40)
         r.set_peer_positions_device(pos_d[i].data_ptr(), N)
         p = pos_d[i][lo:hi]
-        rc, P = r.sharded_route_device(p.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M,
-                                       offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap)
-        assert rc == 0, (rc, P)
-        state["P"] += P
+        # asynchronous sharded tick: P and the status bits of tick i land in cnt[i]
+        r.sharded_route_async(p.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M,
+                              offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap, cnt[i].data_ptr())
         state["i"] = i + 1
 
     for _ in range(a.warmup):
         one()
-    state["P"] = 0
     t_ms = timed_ticks(one, a.steps, stream, dev, world_size, [r])
-    t_max_ms, pairs_all = reduce_over_ranks(t_ms, state["P"], dev, world_size)
+    c = _counters(cnt)[a.warmup:]
+    assert (c["error"] == 0).all() and (c["overflow"] == 0).all(), c
+    t_max_ms, pairs_all = reduce_over_ranks(t_ms, int(c["n_pairs"].sum()), dev, world_size)
     out = _line(a, world_size, pairs_all / (t_max_ms / 1e3), t_max_ms / a.steps, "strong",
                 f"C5 over {world_size} GPUs by cube hash: 1M entities, incremental churn on the owners, "
                 "slots to the owners and cube-list pools back by RCCL (wq_sharded_route_tick_device), exact radius "

@@ -347,6 +347,22 @@ int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_
                                  size_t n_msgs, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs,
                                  size_t capacity, size_t* n_pairs);
 int wq_sharded_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity);
+/* The same tick without its end-of-tick read: it returns as soon as its work is enqueued (the GPU
+ * never idles between back-to-back ticks) and writes its result to d_counters (device memory,
+ * nullable) and the sticky wq_route_health words, as wq_route_tick_device does: n_pairs = P,
+ * overflow = P > capacity (outputs truncated), error = the device bits of every shard's counters
+ * and statuses (2, 4, 8 as for a single-GPU tick), 32 when some shard's local step failed, 64 when a
+ * budget was too small — the tick's outputs are then NOT valid and the caller routes it again; every
+ * shard sees the same bits. The budgets of a tick come from the tick two calls back: each call first
+ * folds in the read-back of every earlier asynchronous tick but the latest (all shards fold the same
+ * ticks, so both ends of every pair agree). A tick that must run exact (the first, or after a bit
+ * 64) runs synchronously, as wq_sharded_route_tick_device does. Collective: all G shards make the
+ * same sequence of sharded calls. wq_sharded_copy_out does not apply to an asynchronous tick. The
+ * slot form only (not wq_debug_set_shard_form's expanded form). */
+int wq_sharded_route_tick_async(wq_router* h, const double* d_pos, const int64_t* d_keys,
+                                const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
+                                size_t n_msgs, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs,
+                                size_t capacity, wq_route_counters* d_counters);
 /* What crosses between GPUs in a sharded tick: each message as one 20-byte slot to its owner (two
  * for a key without a packed form), and back a 12-byte row reference per slot plus, per (owner,
  * ingesting shard), ONE copy of every cube list those messages hit — not the expanded (message,

@@ -835,3 +835,80 @@ def test_hub_radius_irregular_keys_vs_whole_table_oracle(form):
     for r in routers:
         r.close()
     hub.close()
+
+
+def _tick_async(r, w, lo, hi, dev, cap=None):
+    """wq_sharded_route_tick_async on messages [lo, hi): (counters, offsets, peers, msgs) once the
+    stream is done (the call itself does not wait)."""
+    import torch
+    M = hi - lo
+    pos = torch.from_numpy(np.ascontiguousarray(w.pos[lo:hi])).to(dev)
+    wo = torch.from_numpy(np.ascontiguousarray(w.world[lo:hi]).view(np.int32)).to(dev)
+    se = torch.from_numpy(np.ascontiguousarray(w.sender[lo:hi]).view(np.int32)).to(dev)
+    rp = torch.from_numpy(np.ascontiguousarray(w.repl[lo:hi])).to(dev)
+    offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    cap = 64 * M + 64 if cap is None else cap
+    peers = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+    msgs = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+    cnt = torch.full((24,), 0xEE, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    r.sharded_route_async(pos.data_ptr(), wo.data_ptr(), se.data_ptr(), rp.data_ptr(), M, offs.data_ptr(),
+                          peers.data_ptr(), msgs.data_ptr(), cap, cnt.data_ptr())
+    torch.cuda.synchronize(dev)  # the handle's stream is done when the device is
+    c = cnt.cpu().numpy().view(abi.COUNTERS_DTYPE)[0]
+    P = int(c["n_pairs"])
+    return c, offs.cpu().numpy().view(np.uint32), peers.cpu().numpy().view(np.uint32)[:P], \
+        msgs.cpu().numpy().view(np.uint32)[:P]
+
+
+def test_hub_async_ticks_vs_whole_table_oracle():
+    """wq_sharded_route_tick_async (no end-of-tick read; budgets from the tick two calls back): exact
+    and budgeted ticks give the oracle's CSR with P in the device counters; a tick that outgrows its
+    budgets reports bit 64 on every shard (outputs not valid) and later ticks recover — through an
+    asynchronous tick on budgets folded in from before it, and through a synchronous tick that redoes
+    itself exactly."""
+    import torch
+    from worldql_server_amd.router import Hub, Router
+    w, _ = _workload(seed=31)
+    M = len(w.world)
+    G = 3
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    results = [None] * G
+
+    def body(rank):
+        r = routers[rank]
+        r.attach_hub(hub, rank)
+        r.sharded_apply_ops(w.ops)
+        lo, hi = _slice(M, G, rank)
+        half = lo + (hi - lo) // 2
+        got = [("a", lo, half, _tick_async(r, w, lo, half, dev)),
+               ("a", lo, half, _tick_async(r, w, lo, half, dev)),
+               ("a", lo, hi, _tick_async(r, w, lo, hi, dev)),     # twice the messages: over budget
+               ("a", lo, half, _tick_async(r, w, lo, half, dev))]
+        h1 = r.route_health()
+        got.append(("s", lo, hi, _tick(r, w, lo, hi, dev)))      # synchronous: redone exactly
+        got.append(("a", lo, lo + 7, _tick_async(r, w, lo, lo + 7, dev)))
+        got.append(("a", lo, hi, _tick_async(r, w, lo, hi, dev)))
+        results[rank] = (got, h1, r.route_health(), r.shard_tick_stats())
+
+    _run_shards(G, body)
+    for rank in range(G):
+        got, h1, h2, stats = results[rank]
+        for k, (kind, a, b, g) in enumerate(got):
+            want = _expected([w.ops], w, a, b)
+            if kind == "s":
+                _check(g, want, b - a)
+                continue
+            c, offs, peers, msgs = g
+            if k == 2:  # outgrew its budgets: flagged, not valid
+                assert int(c["error"]) & 64, (rank, c)
+                continue
+            assert int(c["error"]) == 0 and int(c["overflow"]) == 0, (rank, k, c)
+            assert int(c["n_pairs"]) == len(want[1])
+            _check((0, offs, peers, msgs), want, b - a)
+        assert h1[0] & 64 and not (h2[0] & 64), (h1, h2)
+    for r in routers:
+        r.close()
+    hub.close()

@@ -89,6 +89,8 @@ def main():
     ap.add_argument("--G", type=int, default=8)
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--async", dest="use_async", action="store_true",
+                    help="replay with wq_sharded_route_tick_async (no end-of-tick read)")
     ap.add_argument("--ticks", type=int, default=20)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -123,6 +125,13 @@ def main():
                                                 offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap)
         assert rc == 0, (g, rc, P)
         return P
+
+    cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+
+    def tick_async(g):
+        m, t, offs, peers, msgs, cap = bufs[g]
+        routers[g].sharded_route_async(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), m,
+                                       offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap, cnt.data_ptr())
 
     errs, Ps = [], [0] * G
 
@@ -165,16 +174,28 @@ def main():
     for _ in range(3):
         assert tick(a.rank) == P_live
     torch.cuda.synchronize(dev)
+    if a.use_async:
+        for _ in range(3):
+            tick_async(a.rank)
+        torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(a.ticks):
-        P = tick(a.rank)  # every sharded tick ends with its one host read: wall time is the tick
+        if a.use_async:
+            tick_async(a.rank)  # no end-of-tick read: ticks queue back to back
+        else:
+            P = tick(a.rank)  # every sharded tick ends with its one host read: wall time is the tick
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / a.ticks
+    if a.use_async:
+        from bench_configs import _counters
+        c = _counters(cnt)[0]
+        assert c["error"] == 0 and c["overflow"] == 0, c
+        P = int(c["n_pairs"])
     assert P == P_live
     exact, budgeted = r.shard_tick_stats()
     res = {"workload": f"C3 (scale {a.scale}): {M} messages, G = {G} shards; shard {a.rank} alone, its exchanges "
                        "replaying the bytes it received in a live G-shard tick (no link time)",
-           "G": G, "rank": a.rank, "messages_this_shard": bufs[a.rank][0], "pairs_this_shard": int(P),
+           "G": G, "rank": a.rank, "async": bool(a.use_async), "messages_this_shard": bufs[a.rank][0], "pairs_this_shard": int(P),
            "tick_ms_alone": dt * 1e3, "ticks": a.ticks, "received_bytes_per_tick": int(sum(rec_bytes)),
            "table_build_s": round(build_s, 2), "slot_ticks_exact_budgeted": [int(exact), int(budgeted)]}
     print(json.dumps(res), flush=True)

@@ -227,6 +227,14 @@ struct ShardCtx {
     const double* last_pos = nullptr;       // radius filter on: its positions and replication codes
     const uint8_t* last_repl = nullptr;     // (the emit re-filters list and pool rows)
     bool last_radius = false;
+    // wq_sharded_route_tick_async: pinned snapshots of the small vectors of ticks not read back yet,
+    // oldest first (a ring); every call drains them in the same order on every shard, so the budgets
+    // derived from them stay identical on both ends of every pair
+    static constexpr uint32_t kRing = 4;
+    void* asnap[kRing] = {};
+    hipEvent_t aev[kRing] = {};
+    uint32_t ahead = 0, acount = 0;
+    uint64_t n_async = 0;
 };
 
 namespace {
@@ -868,6 +876,9 @@ int attach(wq_router* h, uint32_t G, uint32_t rank) {
               hipStreamCreateWithFlags(&sc.side, hipStreamNonBlocking) == hipSuccess;
     for (hipEvent_t* e : {&sc.ev_fork, &sc.ev_join, &sc.ev_ready, &sc.ev_done})
         ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+    for (uint32_t k = 0; k < ShardCtx::kRing; ++k)
+        ok = ok && hipHostMalloc(&sc.asnap[k], kSmallBytes, hipHostMallocDefault) == hipSuccess &&
+             hipEventCreateWithFlags(&sc.aev[k], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         shard_release(h);
         return set_error(h, WQ_E_OOM, "shard exchange vectors / stream / events");
@@ -981,6 +992,10 @@ void shard_release(wq_router* h) {
                       &sc->otiles,   &sc->blk};
     for (DevBuf* b : bufs) b->release();
     if (sc->hsmall) (void)hipHostFree(sc->hsmall);
+    for (uint32_t k = 0; k < ShardCtx::kRing; ++k) {
+        if (sc->asnap[k]) (void)hipHostFree(sc->asnap[k]);
+        if (sc->aev[k]) (void)hipEventDestroy(sc->aev[k]);
+    }
     if (sc->side) (void)hipStreamDestroy(sc->side);
     for (hipEvent_t e : {sc->ev_fork, sc->ev_join, sc->ev_ready, sc->ev_done})
         if (e) (void)hipEventDestroy(e);
@@ -1239,10 +1254,97 @@ static int ensure_health(wq_router* h) {
     return WQ_OK;
 }
 
+// The global picture of a finished slot tick from its small vectors (the same on every shard: codes
+// and device bits from every shard's A and C), and the next tick's budgets from its true sizes when
+// it was clean; a tick whose sizes outgrew a budget leaves the budgets off (the next tick is exact).
+struct TickPicture {
+    uint32_t code = 0, bits = 0, code_from = 0, bits_from = 0;
+    bool over = false;
+};
+static TickPicture fold_tick(ShardCtx& sc, const char* hs) {
+    const uint32_t G = sc.G, me = sc.rank;
+    const uint32_t* ha = reinterpret_cast<const uint32_t*>(hs + kSmallA);
+    const uint32_t* hc = reinterpret_cast<const uint32_t*>(hs + kSmallC);
+    TickPicture t;
+    for (uint32_t d = 0; G > 1 && d < G; ++d) {
+        for (uint32_t st : {ha[2 * G + 2 * d + 1], hc[2 * G + 2 * d + 1]}) {
+            if ((st & kStCodeMask) && !t.code) t.code = st & kStCodeMask, t.code_from = d;
+            if (((st >> 8) & 0xFFFFu) && !t.bits) t.bits = (st >> 8) & 0xFFFFu, t.bits_from = d;
+            t.over |= (st & kStBudget) != 0;
+        }
+    }
+    if (G > 1 && !t.code && !t.over) {  // next tick's budgets from this tick's true sizes
+        for (uint32_t d = 0; d < G; ++d) {
+            sc.b1_out[d] = d == me ? 0u : slot_budget(ha[2 * d]);
+            sc.b1_in[d] = d == me ? 0u : slot_budget(ha[2 * G + 2 * d]);
+            sc.b2_out[d] = d == me ? 0 : pool_budget(hc[2 * d]);
+            sc.b2_in[d] = d == me ? 0 : pool_budget(hc[2 * G + 2 * d]);
+        }
+        sc.budgets = true;
+    }
+    if (t.over) sc.budgets = false;
+    return t;
+}
+
+// Folds in the snapshots of asynchronous ticks until at most `keep` are in flight (oldest first,
+// waiting for each; every shard makes the same calls, so every shard folds the same ticks).
+static int async_drain(wq_router* h, uint32_t keep) {
+    ShardCtx& sc = *h->shard;
+    while (sc.acount > keep) {
+        const uint32_t k = sc.ahead;
+        WQ_HIP(h, hipEventSynchronize(sc.aev[k]));
+        (void)fold_tick(sc, static_cast<const char*>(sc.asnap[k]));
+        sc.ahead = (k + 1) % ShardCtx::kRing;
+        sc.acount--;
+    }
+    return WQ_OK;
+}
+
+// wq_route_health / counters error bits of an asynchronous sharded tick (include/wq_router.h)
+constexpr uint32_t kErrShardStep = 32u, kErrRedo = 64u;
+
+struct AsyncResultParams {
+    const uint32_t* a_recv;  // 2G words: {slots, status} from every shard
+    const uint32_t* c_recv;  // 2G words: {pool words, status} from every shard
+    uint32_t G;
+    const wq_route_counters* cnt;  // the tick's counter blocks (kCntScan, kCntSelf, kCntOwner)
+    uint32_t has_msgs;
+    uint64_t capacity;
+    wq_route_counters* out;  // the caller's (nullable)
+    uint32_t* health;        // the handle's sticky words
+};
+
+// (asynchronous tick) what the synchronous tick reads back, folded on the device into the caller's
+// counters and the sticky health words: P, a shard's failed step (32), the device bits of every
+// shard's statuses and counters, a budget that was too small (64: the outputs are not valid; every
+// shard sees it and the next call runs exact).
+__global__ void k_async_result(AsyncResultParams p) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint32_t err = 0;
+    for (uint32_t d = 0; p.G > 1 && d < p.G; ++d) {
+        for (uint32_t st : {p.a_recv[2 * d + 1], p.c_recv[2 * d + 1]}) {
+            if (st & kStCodeMask) err |= kErrShardStep;
+            err |= (st >> 8) & 0xFFFFu;
+            if (st & kStBudget) err |= kErrRedo;
+        }
+    }
+    err |= p.cnt[kCntScan].error | p.cnt[kCntSelf].error | p.cnt[kCntOwner].error;
+    const uint64_t P = p.has_msgs ? p.cnt[kCntScan].n_pairs : 0;
+    const uint32_t ovf = P > p.capacity ? 1u : 0u;
+    if (p.out) {
+        p.out->n_pairs = P;
+        p.out->n_candidates = p.has_msgs ? p.cnt[kCntScan].n_candidates : 0;
+        p.out->overflow = ovf;
+        p.out->error = err;
+    }
+    if (err) atomicOr(p.health, err);
+    if (ovf) atomicOr(p.health + 1, 1u);
+}
+
 static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
                      const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t* d_offsets,
                      uint32_t* d_peers, uint32_t* d_msgs, size_t capacity, size_t* n_pairs, bool exact, int inject,
-                     bool* redo) {
+                     bool* redo, bool async = false, wq_route_counters* d_result = nullptr) {
     hipStream_t s = h->stream;
     ShardCtx& sc = *h->shard;
     const uint32_t G = sc.G, me = sc.rank;
@@ -1621,43 +1723,47 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
         if ((rc = slots_copy_out(h, d_offsets, d_peers, d_msgs, capacity))) return rc;
     }
 
+    // ---- asynchronous end (wq_sharded_route_tick_async, a budgeted tick without a local failure):
+    // no host read; the small vectors go to a pinned snapshot the next calls fold in (budgets), P and
+    // the statuses to the caller's counters and the health words ----
+    if (async && !exact && !late) {
+        const uint32_t k = (sc.ahead + sc.acount) % ShardCtx::kRing;  // async_drain left a free slot
+        WQ_HIP(h, hipMemcpyAsync(sc.asnap[k], small, small_used, hipMemcpyDeviceToHost, s));
+        WQ_HIP(h, hipEventRecord(sc.aev[k], s));
+        sc.acount++;
+        sc.n_async++;
+        AsyncResultParams ar{};
+        ar.a_recv = a_recv;
+        ar.c_recv = c_recv;
+        ar.G = G;
+        ar.cnt = cnts;
+        ar.has_msgs = M ? 1u : 0u;
+        ar.capacity = capacity;
+        ar.out = d_result;
+        ar.health = route_health(h);
+        hipLaunchKernelGGL(k_async_result, dim3(1), dim3(64), 0, s, ar);
+        WQ_HIP(h, hipGetLastError());
+        sc.last_ready = false;  // no copy-out of an unread tick (its P is on the device)
+        *n_pairs = 0;
+        return WQ_OK;
+    }
+
     // ---- the one host read: P, the statuses, the true sizes ----
     WQ_HIP(h, hipMemcpyAsync(sc.hsmall, small, small_used, hipMemcpyDeviceToHost, s));
     WQ_HIP(h, hipStreamSynchronize(s));
     const char* hs = static_cast<const char*>(sc.hsmall);
-    const uint32_t* ha = reinterpret_cast<const uint32_t*>(hs + kSmallA);
-    const uint32_t* hc = reinterpret_cast<const uint32_t*>(hs + kSmallC);
     const wq_route_counters* hcnt = reinterpret_cast<const wq_route_counters*>(hs + kSmallCnt);
-    // the global picture (the same on every shard): codes and device bits from every shard's A and C
-    uint32_t code = 0, bits = 0, code_from = 0, bits_from = 0;
-    bool over = false;
-    for (uint32_t d = 0; G > 1 && d < G; ++d) {
-        for (uint32_t st : {ha[2 * G + 2 * d + 1], hc[2 * G + 2 * d + 1]}) {
-            if ((st & kStCodeMask) && !code) code = st & kStCodeMask, code_from = d;
-            if (((st >> 8) & 0xFFFFu) && !bits) bits = (st >> 8) & 0xFFFFu, bits_from = d;
-            over |= (st & kStBudget) != 0;
-        }
-    }
-    if (G > 1 && !code && !over) {  // next tick's budgets from this tick's true sizes
-        for (uint32_t d = 0; d < G; ++d) {
-            sc.b1_out[d] = d == me ? 0u : slot_budget(ha[2 * d]);
-            sc.b1_in[d] = d == me ? 0u : slot_budget(ha[2 * G + 2 * d]);
-            sc.b2_out[d] = d == me ? 0 : pool_budget(hc[2 * d]);
-            sc.b2_in[d] = d == me ? 0 : pool_budget(hc[2 * G + 2 * d]);
-        }
-        sc.budgets = true;
-    }
+    const TickPicture tp = fold_tick(sc, hs);
     if (late) {
         h->err = late_msg;
         return late;
     }
-    if (code) return status_error(h, code, code_from);
-    if (over) {  // every shard saw it: all of them redo the tick exactly
-        sc.budgets = false;
+    if (tp.code) return status_error(h, tp.code, tp.code_from);
+    if (tp.over) {  // every shard saw it: all of them redo the tick exactly
         *redo = true;
         return WQ_OK;
     }
-    if (bits) return status_error(h, (uint64_t)bits << 32, bits_from);
+    if (tp.bits) return status_error(h, (uint64_t)tp.bits << 32, tp.bits_from);
     const uint32_t err = hcnt[kCntScan].error | hcnt[kCntSelf].error | hcnt[kCntOwner].error;
     const uint64_t P = M ? hcnt[kCntScan].n_pairs : 0;
     sc.last_P = P;
@@ -1670,16 +1776,29 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
 
 static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
                               const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t* d_offsets,
-                              uint32_t* d_peers, uint32_t* d_msgs, size_t capacity, size_t* n_pairs) {
+                              uint32_t* d_peers, uint32_t* d_msgs, size_t capacity, size_t* n_pairs, bool async = false,
+                              wq_route_counters* d_result = nullptr) {
     ShardCtx& sc = *h->shard;
+    // earlier asynchronous ticks first: a synchronous tick folds them all in; an asynchronous one
+    // keeps the latest in flight (its budgets come from the tick before), unless it must run exact
+    if (int rc = async_drain(h, async && sc.budgets ? 1u : 0u)) return rc;
     const int inject = h->shard_inject;
     h->shard_inject = 0;
     bool redo = false;
     int rc = slot_tick(h, d_pos, d_keys, d_world, d_sender, d_repl, M, d_offsets, d_peers, d_msgs, capacity, n_pairs,
-                       sc.G > 1 && !sc.budgets, inject, &redo);
+                       sc.G > 1 && !sc.budgets, inject, &redo, async, d_result);
     if (rc == WQ_OK && redo)
         rc = slot_tick(h, d_pos, d_keys, d_world, d_sender, d_repl, M, d_offsets, d_peers, d_msgs, capacity, n_pairs,
                        true, 0, &redo);
+    // an asynchronous call that ran synchronously (exact, or a local failure) leaves its result in the
+    // caller's counters all the same
+    if (async && d_result && (rc == WQ_OK || rc == WQ_E_CAPACITY) && sc.last_ready) {
+        wq_route_counters c{};
+        c.n_pairs = *n_pairs;
+        c.overflow = *n_pairs > capacity ? 1u : 0u;
+        WQ_HIP(h, hipMemcpyAsync(d_result, &c, sizeof(c), hipMemcpyHostToDevice, h->stream));
+        WQ_HIP(h, hipStreamSynchronize(h->stream));  // c lives on this stack frame
+    }
     return rc;
 }
 
@@ -1806,6 +1925,22 @@ int wq_sharded_route_tick_device(wq_router* h, const double* d_pos, const int64_
     sc.last_P = P;
     sc.last_ready = true;
     return copy_out(h, d_offsets, d_peers, d_msgs, capacity);
+}
+
+int wq_sharded_route_tick_async(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                                const uint32_t* d_sender, const uint8_t* d_repl, size_t n_msgs, uint32_t* d_offsets,
+                                uint32_t* d_peers, uint32_t* d_msgs, size_t capacity, wq_route_counters* d_counters) {
+    if (!h || !d_offsets || (n_msgs && (!d_world || !d_sender || !d_repl || (!d_pos && !d_keys))) ||
+        (capacity && !d_peers))
+        return WQ_E_INVALID;
+    if (n_msgs >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
+    if (!h->shard || h->shard_expanded)
+        return set_error(h, WQ_E_INVALID, "wq_sharded_route_tick_async: no exchange attached, or the expanded form");
+    WQ_HIP(h, hipSetDevice(h->device));
+    if (capacity > 0xFFFFFFFFull) capacity = 0xFFFFFFFFull;
+    size_t P = 0;
+    return sharded_tick_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs, capacity,
+                              &P, true, d_counters);
 }
 
 int wq_sharded_route_owner_device(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,

@@ -105,6 +105,7 @@ def load_library(build_if_missing: bool = True):
         "wq_shard_info": ([vp, ctypes.POINTER(u32), ctypes.POINTER(u32)], i32),
         "wq_sharded_apply_ops": ([vp, vp, sz], i32),
         "wq_sharded_route_tick_device": ([vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, ctypes.POINTER(sz)], i32),
+        "wq_sharded_route_tick_async": ([vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, vp], i32),
         "wq_sharded_copy_out": ([vp, vp, vp, vp, sz], i32),
         "wq_sharded_route_owner_device": ([vp, vp, vp, vp, vp, vp, sz, ctypes.POINTER(abi.OwnerView)], i32),
         "wq_shard_last_bytes": ([vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], i32),
@@ -404,6 +405,15 @@ class Router:
         if rc not in (0, abi.WQ_E_CAPACITY):
             self._check(rc)
         return rc, n.value
+
+    def sharded_route_async(self, pos_ptr, world_ptr, sender_ptr, repl_ptr, n_msgs, offsets_ptr, peers_ptr,
+                            msgs_ptr, capacity, counters_ptr=None, keys_ptr=None) -> None:
+        """wq_sharded_route_tick_async: the collective tick without its end-of-tick read; P and the
+        status bits (64: a budget was too small, route the tick again) land in counters_ptr."""
+        self._check(self.lib.wq_sharded_route_tick_async(self.h, pos_ptr or None, keys_ptr or None, world_ptr or None,
+                                                         sender_ptr or None, repl_ptr or None, n_msgs, offsets_ptr,
+                                                         peers_ptr or None, msgs_ptr or None, capacity,
+                                                         counters_ptr or None))
 
     def sharded_route_owner_device(self, pos_ptr, world_ptr, sender_ptr, repl_ptr, n_msgs, keys_ptr=None):
         """The owner-side form of the collective sharded tick: the pairs stay on the shard that routed
