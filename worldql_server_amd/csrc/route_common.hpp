@@ -98,6 +98,9 @@ struct RouteIn {
     int64_t si;
     const uint32_t* slots = nullptr;  // count_kernel<..., SLOTS = true>: M compact slots instead of the above
     uint32_t own_G = 1, own_me = 0;   // count_kernel<..., OWN = true>: count only shard own_me's cubes of own_G
+    // count_kernel: when set, the number of messages (slots) is min(M, *m_dev) — a count known on the
+    // device only (the sharded tick's own slots)
+    const uint32_t* m_dev = nullptr;
 };
 
 // info.x of a row the sharded tick's owner shipped back: word offset into the received cube-list

@@ -30,6 +30,8 @@ struct CountParams {
     wq_route_counters* cnt_next;
     uint32_t* health;  // sticky {error, overflow} words (flag_route)
     uint32_t n_tiles = 0;  // count_kernel: tiles of kBlock * IPT messages (grid stride when > gridDim.x)
+    // count_kernel: when set, message (slot) m's e and locator go to index perm[m] (kNone: nowhere)
+    const uint32_t* perm = nullptr;
 };
 
 // e / locator once count, membership and list position are known (local_message.rs:60-86)
@@ -300,6 +302,10 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
 
 template <bool RAW_KEYS, int IPT, int MINW, int DBG = 0, bool FULL = false, bool SLOTS = false, bool OWN = false>
 __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
+    if (p.in.m_dev) {
+        const uint32_t mv = *p.in.m_dev;
+        if (mv < p.in.M) p.in.M = mv;
+    }
     __shared__ uint64_t wave_F[kWaves];
     __shared__ uint64_t wave_E[kWaves];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -312,6 +318,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
     const uint32_t nt = p.n_tiles ? p.n_tiles : gridDim.x;
     for (uint32_t blk = blockIdx.x; blk < nt; blk += gridDim.x) {
         const uint32_t m0 = blk * (kBlock * IPT);
+        if (m0 >= p.in.M && blk > 0) break;  // past a device-side count (m_dev): nothing left here
         uint64_t F_local = 0;
         uint32_t E_local = 0;
         uint32_t e_out[IPT];
@@ -321,8 +328,11 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
         for (int i = 0; i < IPT; ++i) {
             const uint32_t m = m0 + i * kBlock + tid;
             if (m < p.in.M) {
-                p.e[m] = e_out[i];
-                p.info[m] = inf_out[i];
+                const uint32_t dst = p.perm ? p.perm[m] : m;
+                if (dst != kNone) {
+                    p.e[dst] = e_out[i];
+                    p.info[dst] = inf_out[i];
+                }
             }
         }
         const uint64_t Fw = wave_sum_u64(F_local);

@@ -34,6 +34,12 @@ struct ShardIn {
     int64_t si;
     bool pos_rec;  // records carry the positions (radius filter on)
     uint32_t me = kNone;  // budgeted slots (slot_*_kernel): this shard's own messages take no slot
+    // ... unless own_slots is set: then they are slots too, in own_slots (never exchanged; its slot
+    // -> message map in own_perm), and the histogram's column `me` counts them
+    uint32_t* own_slots = nullptr;
+    uint32_t* own_perm = nullptr;
+    bool own_too = false;
+    uint32_t* zero_e = nullptr;  // slot_count_kernel: e[m] = 0 for every message (rows no step writes)
 };
 
 template <bool RAW>
@@ -330,7 +336,8 @@ __global__ void __launch_bounds__(kBlock) slot_count_kernel(ShardIn in, uint32_t
             const uint32_t w = in.world[m];
             own[i] = shard_of(w, x, y, z, in.G);
             wt[i] = msg_weight<RAW, true>(in, w, x, y, z);
-            valid[i] = own[i] != in.me;
+            valid[i] = in.own_too || own[i] != in.me;
+            if (in.zero_e) in.zero_e[m] = 0u;
         }
     }
 #pragma unroll
@@ -352,7 +359,8 @@ __global__ void __launch_bounds__(kBlock) slot_count_kernel(ShardIn in, uint32_t
 // (b2) one block per owner d (the columns are independent): the exclusive scan of its column of
 // block counts (in place); the owner's total and the budget bit to a[2d], a[2d + 1].
 __global__ void __launch_bounds__(kScanThreads1)
-    slot_scan_kernel(uint32_t* __restrict__ v, uint32_t nblk, uint32_t G, SlotLayout L, uint32_t* __restrict__ a) {
+    slot_scan_kernel(uint32_t* __restrict__ v, uint32_t nblk, uint32_t G, SlotLayout L, uint32_t* __restrict__ a,
+                     uint32_t me) {
     __shared__ uint32_t wsum[kScanThreads1 / 64];
     __shared__ uint32_t carry_s;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -380,7 +388,8 @@ __global__ void __launch_bounds__(kScanThreads1)
         }
         if (threadIdx.x == 0) {
             a[2 * d] = carry_s;
-            a[2 * d + 1] = carry_s > L.budget[d] ? kStBudget : 0u;
+            // the own column (own slots on): no budget, its buffer holds every message's slots
+            a[2 * d + 1] = d != me && carry_s > L.budget[d] ? kStBudget : 0u;
         }
         __syncthreads();
     }
@@ -419,7 +428,7 @@ __global__ void __launch_bounds__(kBlock)
             rpl[i] = in.repl[m];
             own[i] = shard_of(wrd[i], kx[i], ky[i], kz[i], in.G);
             reg[i] = pack_key(wrd[i], kx[i], ky[i], kz[i], in.sf, &pk[i], &ext[i]);
-            go[i] = own[i] != in.me;
+            go[i] = own[i] != in.me || in.own_too;
         }
     }
 #pragma unroll
@@ -452,9 +461,19 @@ __global__ void __launch_bounds__(kBlock)
         if (!go[i]) continue;
         const uint32_t d = own[i];
         const uint32_t j = wc[i * kWaves + wave][d] + rank[i];  // within the owner's segment
-        if (j + (reg[i] ? 1u : 2u) > L.budget[d]) continue;    // over budget: the tick is redone exactly
-        const uint32_t slot = L.base[d] + j;
-        uint32_t* o = out + (uint64_t)kSlotWords * slot;
+        uint32_t slot;
+        uint32_t* pm;
+        uint32_t* o;
+        if (d == in.me) {  // own slots on: this shard's own message, into its own (unbudgeted) buffer
+            slot = j;
+            pm = in.own_perm;
+            o = in.own_slots + (uint64_t)kSlotWords * slot;
+        } else {
+            if (j + (reg[i] ? 1u : 2u) > L.budget[d]) continue;  // over budget: the tick is redone exactly
+            slot = L.base[d] + j;
+            pm = perm;
+            o = out + (uint64_t)kSlotWords * slot;
+        }
         const uint32_t rp = rpl[i];
         if (reg[i]) {
             o[0] = (uint32_t)pk[i];
@@ -462,7 +481,7 @@ __global__ void __launch_bounds__(kBlock)
             o[2] = ext[i];
             o[3] = snd[i];
             o[4] = rp | (kSlotReg << 8);
-            perm[slot] = m;
+            pm[slot] = m;
         } else {
             o[0] = (uint32_t)(uint64_t)kx[i];
             o[1] = (uint32_t)((uint64_t)kx[i] >> 32);
@@ -474,8 +493,8 @@ __global__ void __launch_bounds__(kBlock)
             o[7] = (uint32_t)(uint64_t)kz[i];
             o[8] = (uint32_t)((uint64_t)kz[i] >> 32);
             o[9] = kSlotTail << 8;
-            perm[slot] = m;
-            perm[slot + 1] = kNone;
+            pm[slot] = m;
+            pm[slot + 1] = kNone;
         }
     }
 }
@@ -633,7 +652,7 @@ int launch_shard_slots(wq_router* h, const double* d_pos, const int64_t* d_keys,
 int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
                         const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, uint32_t me,
                         const SlotLayout& L, uint32_t* d_slots, uint32_t* d_perm, uint32_t* d_a, int phases,
-                        bool hist_ready) {
+                        bool hist_ready, bool own_too, uint32_t* own_slots, uint32_t* own_perm, uint32_t* zero_e) {
     hipStream_t s = h->stream;
     ShardIn in;
     in.pos = d_pos;
@@ -648,6 +667,10 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
     in.si = (int64_t)h->cube_size;
     in.pos_rec = false;
     in.me = me;
+    in.own_too = own_too;
+    in.own_slots = own_slots;
+    in.own_perm = own_perm;
+    in.zero_e = zero_e;
     if (M && (phases & 1)) {
         WQ_ALLOC(h, h->shard_hist, (uint64_t)in.nblk * G * 4);
         uint32_t* hist = h->shard_hist.as<uint32_t>();
@@ -658,7 +681,7 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
         else
             hipLaunchKernelGGL((slot_count_kernel<false>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist);
         WQ_HIP(h, hipGetLastError());
-        hipLaunchKernelGGL(slot_scan_kernel, dim3(G), dim3(kScanThreads1), 0, s, hist, in.nblk, G, L, d_a);
+        hipLaunchKernelGGL(slot_scan_kernel, dim3(G), dim3(kScanThreads1), 0, s, hist, in.nblk, G, L, d_a, me);
         WQ_HIP(h, hipGetLastError());
     } else if (phases & 1) {
         WQ_HIP(h, hipMemsetAsync(d_a, 0, 8 * G, s));

@@ -25,7 +25,9 @@
 // consistent sizes (so no peer is left waiting) and reports the error at the end.
 #include <dlfcn.h>
 
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -49,7 +51,8 @@ int launch_shard_messages(wq_router* h, const double* d_pos, const int64_t* d_ke
 int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
                         const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, uint32_t me,
                         const SlotLayout& L, uint32_t* d_slots, uint32_t* d_perm, uint32_t* d_a, int phases,
-                        bool hist_ready = false);
+                        bool hist_ready = false, bool own_too = false, uint32_t* own_slots = nullptr,
+                        uint32_t* own_perm = nullptr, uint32_t* zero_e = nullptr);
 uint32_t budget_slot_tile();
 int launch_route_records(wq_router* h, const wq_msg_rec* d_recs, size_t M, uint32_t* d_offsets, uint32_t* d_peers,
                          uint32_t* d_msgs, size_t capacity);
@@ -203,6 +206,9 @@ struct ShardCtx {
     // workspace of the slot tick (compact slots out, row references + cube-list pools back)
     DevBuf slots, perm, rslots, ocnt, hslot, plen, poff, claim, lead, ref_send, ref_recv, pool_send, pool_recv,
         desc_fill, e_msg, info_msg, mtiles, otiles, blk;
+    // own slots (the default with G > 1, no radius): this shard's own messages as slots of a segment
+    // that is never exchanged, its slot -> message map, and the scratch tile sums of their count
+    DevBuf own_slots, own_perm, own_tiles;
     uint64_t claim_cap = 0;  // claim table entries (power of two); 0 = not allocated
     uint64_t ticks = 0;      // slot ticks run: the claim table's tag
     // exchange budgets of the slot tick, identical on both ends of every pair: slots me -> d and
@@ -230,9 +236,11 @@ struct ShardCtx {
     // wq_sharded_route_tick_async: pinned snapshots of the small vectors of ticks not read back yet,
     // oldest first (a ring); every call drains them in the same order on every shard, so the budgets
     // derived from them stay identical on both ends of every pair
+    // (mapped pinned memory the tick's last kernel writes itself, then a sequence word: no copy
+    // launch and no event, each of which costs the stream a ~7 us bubble)
     static constexpr uint32_t kRing = 4;
     void* asnap[kRing] = {};
-    hipEvent_t aev[kRing] = {};
+    uint64_t aseq[kRing] = {};  // the sequence number snapshot k completes with
     uint32_t ahead = 0, acount = 0;
     uint64_t n_async = 0;
 };
@@ -876,9 +884,10 @@ int attach(wq_router* h, uint32_t G, uint32_t rank) {
               hipStreamCreateWithFlags(&sc.side, hipStreamNonBlocking) == hipSuccess;
     for (hipEvent_t* e : {&sc.ev_fork, &sc.ev_join, &sc.ev_ready, &sc.ev_done})
         ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
-    for (uint32_t k = 0; k < ShardCtx::kRing; ++k)
-        ok = ok && hipHostMalloc(&sc.asnap[k], kSmallBytes, hipHostMallocDefault) == hipSuccess &&
-             hipEventCreateWithFlags(&sc.aev[k], hipEventDisableTiming) == hipSuccess;
+    for (uint32_t k = 0; k < ShardCtx::kRing; ++k) {
+        ok = ok && hipHostMalloc(&sc.asnap[k], kSmallBytes + 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess;
+        if (ok) memset(sc.asnap[k], 0, kSmallBytes + 64);
+    }
     if (!ok) {
         shard_release(h);
         return set_error(h, WQ_E_OOM, "shard exchange vectors / stream / events");
@@ -989,13 +998,11 @@ void shard_release(wq_router* h) {
                       &sc->small,    &sc->slots,     &sc->perm,      &sc->rslots,    &sc->ocnt,     &sc->hslot,
                       &sc->plen,     &sc->poff,      &sc->claim,     &sc->lead,      &sc->ref_send, &sc->ref_recv,
                       &sc->pool_send, &sc->pool_recv, &sc->desc_fill, &sc->e_msg,    &sc->info_msg, &sc->mtiles,
-                      &sc->otiles,   &sc->blk};
+                      &sc->otiles,   &sc->blk,       &sc->own_slots, &sc->own_perm, &sc->own_tiles};
     for (DevBuf* b : bufs) b->release();
     if (sc->hsmall) (void)hipHostFree(sc->hsmall);
-    for (uint32_t k = 0; k < ShardCtx::kRing; ++k) {
+    for (uint32_t k = 0; k < ShardCtx::kRing; ++k)
         if (sc->asnap[k]) (void)hipHostFree(sc->asnap[k]);
-        if (sc->aev[k]) (void)hipEventDestroy(sc->aev[k]);
-    }
     if (sc->side) (void)hipStreamDestroy(sc->side);
     for (hipEvent_t e : {sc->ev_fork, sc->ev_join, sc->ev_ready, sc->ev_done})
         if (e) (void)hipEventDestroy(e);
@@ -1292,7 +1299,16 @@ static int async_drain(wq_router* h, uint32_t keep) {
     ShardCtx& sc = *h->shard;
     while (sc.acount > keep) {
         const uint32_t k = sc.ahead;
-        WQ_HIP(h, hipEventSynchronize(sc.aev[k]));
+        // k_async_result writes the snapshot, then its sequence word (system-scope release)
+        const volatile uint64_t* seq =
+            reinterpret_cast<const volatile uint64_t*>(static_cast<const char*>(sc.asnap[k]) + kSmallBytes);
+        const auto t0 = std::chrono::steady_clock::now();
+        while (*seq != sc.aseq[k]) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+                return set_error(h, WQ_E_TIMEOUT, "asynchronous sharded tick: its result never arrived");
+            std::this_thread::yield();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
         (void)fold_tick(sc, static_cast<const char*>(sc.asnap[k]));
         sc.ahead = (k + 1) % ShardCtx::kRing;
         sc.acount--;
@@ -1312,14 +1328,23 @@ struct AsyncResultParams {
     uint64_t capacity;
     wq_route_counters* out;  // the caller's (nullable)
     uint32_t* health;        // the handle's sticky words
+    const uint32_t* small;   // the tick's small vectors (words) ...
+    uint32_t small_words;
+    uint32_t* snap;          // ... copied here (mapped pinned memory), then the sequence word
+    uint64_t seq;
 };
 
 // (asynchronous tick) what the synchronous tick reads back, folded on the device into the caller's
 // counters and the sticky health words: P, a shard's failed step (32), the device bits of every
 // shard's statuses and counters, a budget that was too small (64: the outputs are not valid; every
 // shard sees it and the next call runs exact).
-__global__ void k_async_result(AsyncResultParams p) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__global__ __launch_bounds__(256) void k_async_result(AsyncResultParams p) {
+    for (uint32_t i = threadIdx.x; i < p.small_words; i += blockDim.x) p.snap[i] = p.small[i];
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    __threadfence_system();  // the snapshot before its sequence word
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(p.snap + kSmallBytes / 4), p.seq, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t err = 0;
     for (uint32_t d = 0; p.G > 1 && d < p.G; ++d) {
         for (uint32_t st : {p.a_recv[2 * d + 1], p.c_recv[2 * d + 1]}) {
@@ -1397,11 +1422,25 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
                   fail(alloc(sc.mtiles, ((uint64_t)nt * 3 + 4) * 4)))) {
     }
 
-    // ---- own cubes: with G > 1 (no radius) in one pass with the slot grouping's owner histogram on
-    // the tick's stream, else on the side stream beside the exchanges ----
+    // ---- own cubes. G > 1 without the radius filter (own slots): the grouping pass writes this
+    // shard's own messages as slots of a segment that is never exchanged, and the side stream counts
+    // them once grouped (below), beside the exchanges and the owner's work — the grouping's
+    // histogram pass quantises every message, but probes nothing. Otherwise the own-cube count runs
+    // over every message on the side stream (count_kernel<OWN>), or (diagnostics,
+    // WQ_SHARD_OWN_FUSED) in one pass with the histogram on the tick's stream, as in round 4 ----
     bool forked = false, hist_ready = false;
     static const bool two_pass = getenv("WQ_DEBUG_NO_OWN_HIST") != nullptr;  // diagnostics
-    const bool fuse = G > 1 && !radius && budget_slot_tile() == kHistTiles * kBlock && !two_pass;
+    static const bool fused_env = getenv("WQ_SHARD_OWN_FUSED") != nullptr;   // diagnostics
+    const bool own_slots = G > 1 && !radius && !two_pass && !fused_env;
+    const bool fuse = G > 1 && !radius && budget_slot_tile() == kHistTiles * kBlock && !two_pass && fused_env;
+    if (!late && M && own_slots) {
+        const uint64_t nto = (2 * M + kBlock - 1) / kBlock;
+        if (!fail(alloc(sc.own_slots, (2 * M + 2) * kSlotWords * 4)) && !fail(alloc(sc.own_perm, (2 * M + 2) * 4)) &&
+            !fail(alloc(sc.own_tiles, (nto + 1) * 8))) {
+            // (a message no step writes a row for — its slot was over budget, the tick is redone —
+            // routes to nobody: the histogram pass zeroes every e)
+        }
+    }
     if (!late && M && fuse) {
         const uint32_t nblk = (uint32_t)((M + kHistTiles * kBlock - 1) / (kHistTiles * kBlock));
         if (!fail(alloc(h->shard_hist, (uint64_t)nblk * G * 4))) {
@@ -1427,7 +1466,7 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
             WQ_HIP(h, hipGetLastError());
             hist_ready = true;
         }
-    } else if (!late && M) {
+    } else if (!late && M && !own_slots) {
         WQ_HIP(h, hipEventRecord(sc.ev_fork, s));
         WQ_HIP(h, hipStreamWaitEvent(sc.side, sc.ev_fork, 0));
         CountParams cp{};
@@ -1488,7 +1527,8 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
             for (uint32_t d = 0; d < G; ++d) inf.budget[d] = 0xFFFFFFFFu;
             if (!late)
                 fail(launch_budget_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, me, inf, nullptr, nullptr,
-                                         a_send, 1, hist_ready));
+                                         a_send, 1, hist_ready, own_slots, nullptr, nullptr,
+                                         own_slots ? sc.e_msg.as<uint32_t>() : nullptr));
             if (late && (rc = put_status(a_send))) return rc;
             Xfer x{{a_send}, {eight.data()}, {a_recv}, {eight.data()}, 1};
             if ((rc = exchange(h, x))) return rc;
@@ -1508,7 +1548,10 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
             return fatal_receive(h, "hipMalloc of the sharded tick's slots");
         if (!late)
             fail(launch_budget_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, me, L, sc.slots.as<uint32_t>(),
-                                     sc.perm.as<uint32_t>(), a_send, exact ? 2 : 3, hist_ready));
+                                     sc.perm.as<uint32_t>(), a_send, exact ? 2 : 3, hist_ready, own_slots,
+                                     sc.own_slots.as<uint32_t>(), sc.own_perm.as<uint32_t>(),
+                                     own_slots && !exact ? sc.e_msg.as<uint32_t>() : nullptr));
+
         if (late) {  // nothing to send: tail slots everywhere (zero words route to nobody either way)
             WQ_HIP(h, hipMemsetAsync(sc.slots.p, 0, (Sb + 1) * kSlotWords * 4, s));
             WQ_HIP(h, hipMemsetAsync(sc.perm.p, 0xFF, (Sb + 1) * 4, s));
@@ -1554,6 +1597,38 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
             hipLaunchKernelGGL((count_kernel<false, 1, 8, 0, false, true>), dim3((nto + 1) / 2), dim3(kBlock), 0, s, cp);
             if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "count launch (sharded tick)"));
         }
+    }
+    if (G > 1 && !late && M && own_slots) {
+        // after the owner count: beside the claims, references, pool gather and X2 (beside the
+        // owner count, the two probe passes only slowed each other down)
+        // the own slots (their count: the own column of this tick's histogram, a_send[2 me], known
+        // on the device only) counted on the side stream, e / locator straight to message order
+        WQ_HIP(h, hipEventRecord(sc.ev_fork, s));
+        WQ_HIP(h, hipStreamWaitEvent(sc.side, sc.ev_fork, 0));
+        const uint32_t n_max = (uint32_t)(2 * M);
+        const uint32_t nto = (n_max + kBlock - 1) / kBlock;
+        CountParams cp{};
+        cp.in = RouteIn{nullptr, nullptr, nullptr, nullptr, nullptr, n_max, (int64_t)h->cube_size};
+        cp.in.slots = sc.own_slots.as<uint32_t>();
+        cp.in.m_dev = a_send + 2 * me;
+        cp.t = tv;
+        cp.e = sc.e_msg.as<uint32_t>();
+        cp.info = sc.info_msg.as<uint2>();
+        cp.perm = sc.own_perm.as<uint32_t>();
+        cp.tile_total = sc.own_tiles.as<uint32_t>();
+        cp.tile_F = cp.tile_total + nto;
+        cp.cnt = cnts + kCntSelf;
+        cp.cnt_next = cnts + kCntScratch;
+        cp.health = route_health(h);
+        cp.n_tiles = nto;
+        hipLaunchKernelGGL((count_kernel<false, 1, 8, 0, false, true>), dim3(std::min<uint32_t>(nto, 4096u)),
+                           dim3(kBlock), 0, sc.side, cp);
+        WQ_HIP(h, hipGetLastError());
+        WQ_HIP(h, hipEventRecord(sc.ev_join, sc.side));
+        forked = true;
+    }
+    if (G > 1 && Rb && !late) {
+        RouteWs& rw = h->rws;
         uint64_t C = 1024;  // claim table: load <= 1/2
         while (C < 2 * Rb) C <<= 1;
         if (!late && C > sc.claim_cap) {
@@ -1683,7 +1758,7 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
     sc.last_recv = recvd;
 
     // ---- the ingesting side: rows in message order, then the CSR ----
-    if (forked) WQ_HIP(h, hipStreamWaitEvent(s, sc.ev_join, 0));  // own rows written (remote ones as e = 0)
+    if (forked && !own_slots) WQ_HIP(h, hipStreamWaitEvent(s, sc.ev_join, 0));  // own rows written (remote: e = 0)
     if (!late && G > 1 && Sb) {
         ResolveParams rv{};
         rv.perm = sc.perm.as<uint32_t>();
@@ -1706,12 +1781,13 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
             hipLaunchKernelGGL(k_ref_resolve<false>, rg, dim3(kBlock), 0, s, rv);
         }
         WQ_HIP(h, hipGetLastError());
-        // the count pass's per-tile totals held its own rows only
-        if (M) {
-            hipLaunchKernelGGL(row_tile_sums_kernel, dim3(nt), dim3(kBlock), 0, s, sc.e_msg.as<uint32_t>(),
-                               (uint32_t)M, sc.mtiles.as<uint32_t>());
-            WQ_HIP(h, hipGetLastError());
-        }
+    }
+    if (forked && own_slots) WQ_HIP(h, hipStreamWaitEvent(s, sc.ev_join, 0));  // own rows written
+    // the per-tile totals of every row (a count pass's held its own rows only)
+    if (!late && G > 1 && M && (Sb || own_slots)) {
+        hipLaunchKernelGGL(row_tile_sums_kernel, dim3(nt), dim3(kBlock), 0, s, sc.e_msg.as<uint32_t>(), (uint32_t)M,
+                           sc.mtiles.as<uint32_t>());
+        WQ_HIP(h, hipGetLastError());
     }
     if (!late) {
         sc.last_M = M;
@@ -1728,10 +1804,9 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
     // the statuses to the caller's counters and the health words ----
     if (async && !exact && !late) {
         const uint32_t k = (sc.ahead + sc.acount) % ShardCtx::kRing;  // async_drain left a free slot
-        WQ_HIP(h, hipMemcpyAsync(sc.asnap[k], small, small_used, hipMemcpyDeviceToHost, s));
-        WQ_HIP(h, hipEventRecord(sc.aev[k], s));
         sc.acount++;
         sc.n_async++;
+        sc.aseq[k] = sc.n_async;
         AsyncResultParams ar{};
         ar.a_recv = a_recv;
         ar.c_recv = c_recv;
@@ -1741,7 +1816,11 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
         ar.capacity = capacity;
         ar.out = d_result;
         ar.health = route_health(h);
-        hipLaunchKernelGGL(k_async_result, dim3(1), dim3(64), 0, s, ar);
+        ar.small = reinterpret_cast<const uint32_t*>(small);
+        ar.small_words = (uint32_t)(small_used / 4);
+        ar.snap = static_cast<uint32_t*>(sc.asnap[k]);
+        ar.seq = sc.aseq[k];
+        hipLaunchKernelGGL(k_async_result, dim3(1), dim3(256), 0, s, ar);
         WQ_HIP(h, hipGetLastError());
         sc.last_ready = false;  // no copy-out of an unread tick (its P is on the device)
         *n_pairs = 0;
