@@ -360,7 +360,7 @@ __global__ void __launch_bounds__(kBlock) slot_count_kernel(ShardIn in, uint32_t
 // block counts (in place); the owner's total and the budget bit to a[2d], a[2d + 1].
 __global__ void __launch_bounds__(kScanThreads1)
     slot_scan_kernel(uint32_t* __restrict__ v, uint32_t nblk, uint32_t G, SlotLayout L, uint32_t* __restrict__ a,
-                     uint32_t me) {
+                     uint32_t me, uint32_t* __restrict__ out, uint32_t* __restrict__ perm) {
     __shared__ uint32_t wsum[kScanThreads1 / 64];
     __shared__ uint32_t carry_s;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -390,6 +390,23 @@ __global__ void __launch_bounds__(kScanThreads1)
             a[2 * d] = carry_s;
             // the own column (own slots on): no budget, its buffer holds every message's slots
             a[2 * d + 1] = d != me && carry_s > L.budget[d] ? kStBudget : 0u;
+        }
+        // out set (a budgeted tick): the rest of the segment padded here, as slot_pad_kernel does
+        // after the scatter — the scatter writes slots [0, n) only, and past a budget it writes no
+        // head whose tail does not fit, so padding first gives the same segment
+        if (out && d != me) {
+            const uint32_t B = L.budget[d], n = carry_s;
+            const uint32_t from = n <= B ? n : (B ? B - 1 : 0);
+            for (uint32_t j = from + threadIdx.x; j < B; j += blockDim.x) {
+                const uint32_t slot = L.base[d] + j;
+                uint32_t* o = out + (uint64_t)kSlotWords * slot;
+                o[0] = 0;
+                o[1] = 0;
+                o[2] = 0;
+                o[3] = 0;
+                o[4] = kSlotTail << 8;
+                perm[slot] = kNone;
+            }
         }
         __syncthreads();
     }
@@ -681,7 +698,10 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
         else
             hipLaunchKernelGGL((slot_count_kernel<false>), dim3(in.nblk), dim3(kBlock), 0, s, in, hist);
         WQ_HIP(h, hipGetLastError());
-        hipLaunchKernelGGL(slot_scan_kernel, dim3(G), dim3(kScanThreads1), 0, s, hist, in.nblk, G, L, d_a, me);
+        // a budgeted tick (count, scan and scatter in one call) pads its segments in the scan
+        const bool pad_in_scan = (phases & 3) == 3 && d_slots;
+        hipLaunchKernelGGL(slot_scan_kernel, dim3(G), dim3(kScanThreads1), 0, s, hist, in.nblk, G, L, d_a, me,
+                           pad_in_scan ? d_slots : nullptr, pad_in_scan ? d_perm : nullptr);
         WQ_HIP(h, hipGetLastError());
     } else if (phases & 1) {
         WQ_HIP(h, hipMemsetAsync(d_a, 0, 8 * G, s));
@@ -699,7 +719,7 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
     }
     uint32_t bmax = 0;
     for (uint32_t d = 0; d < G; ++d) bmax = std::max(bmax, L.budget[d]);
-    if (bmax) {
+    if (bmax && !(M && (phases & 3) == 3)) {  // (phases 3 with messages: padded by the scan)
         const unsigned gx = std::min<unsigned>(64u, (bmax + kBlock - 1) / kBlock);
         hipLaunchKernelGGL(slot_pad_kernel, dim3(gx, G), dim3(kBlock), 0, s, L, G, d_a, d_slots, d_perm);
         WQ_HIP(h, hipGetLastError());

@@ -243,6 +243,7 @@ struct ShardCtx {
     uint64_t aseq[kRing] = {};  // the sequence number snapshot k completes with
     uint32_t ahead = 0, acount = 0;
     uint64_t n_async = 0;
+    bool small_zeroed = false;  // the last tick's k_async_result left the small vectors zero
 };
 
 namespace {
@@ -882,8 +883,12 @@ int attach(wq_router* h, uint32_t G, uint32_t rank) {
     bool ok = sc.small.ensure(kSmallBytes) == hipSuccess &&
               hipHostMalloc(&sc.hsmall, kSmallBytes, hipHostMallocDefault) == hipSuccess &&
               hipStreamCreateWithFlags(&sc.side, hipStreamNonBlocking) == hipSuccess;
-    for (hipEvent_t* e : {&sc.ev_fork, &sc.ev_join, &sc.ev_ready, &sc.ev_done})
+    // the hub's events order peer copies (system scope); the side stream's fork / join only work on
+    // this device: a device-scope release is enough there
+    for (hipEvent_t* e : {&sc.ev_ready, &sc.ev_done})
         ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+    for (hipEvent_t* e : {&sc.ev_fork, &sc.ev_join})
+        ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventReleaseToDevice) == hipSuccess;
     for (uint32_t k = 0; k < ShardCtx::kRing; ++k) {
         ok = ok && hipHostMalloc(&sc.asnap[k], kSmallBytes + 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess;
         if (ok) memset(sc.asnap[k], 0, kSmallBytes + 64);
@@ -1332,6 +1337,7 @@ struct AsyncResultParams {
     uint32_t small_words;
     uint32_t* snap;          // ... copied here (mapped pinned memory), then the sequence word
     uint64_t seq;
+    uint32_t* zero;          // the small vectors, zeroed last for the next tick
 };
 
 // (asynchronous tick) what the synchronous tick reads back, folded on the device into the caller's
@@ -1341,30 +1347,35 @@ struct AsyncResultParams {
 __global__ __launch_bounds__(256) void k_async_result(AsyncResultParams p) {
     for (uint32_t i = threadIdx.x; i < p.small_words; i += blockDim.x) p.snap[i] = p.small[i];
     __syncthreads();
-    if (threadIdx.x != 0) return;
-    __threadfence_system();  // the snapshot before its sequence word
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(p.snap + kSmallBytes / 4), p.seq, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-    uint32_t err = 0;
-    for (uint32_t d = 0; p.G > 1 && d < p.G; ++d) {
-        for (uint32_t st : {p.a_recv[2 * d + 1], p.c_recv[2 * d + 1]}) {
-            if (st & kStCodeMask) err |= kErrShardStep;
-            err |= (st >> 8) & 0xFFFFu;
-            if (st & kStBudget) err |= kErrRedo;
+    if (threadIdx.x == 0) {
+        __threadfence_system();  // the snapshot before its sequence word
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(p.snap + kSmallBytes / 4), p.seq, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        uint32_t err = 0;
+        for (uint32_t d = 0; p.G > 1 && d < p.G; ++d) {
+            for (uint32_t st : {p.a_recv[2 * d + 1], p.c_recv[2 * d + 1]}) {
+                if (st & kStCodeMask) err |= kErrShardStep;
+                err |= (st >> 8) & 0xFFFFu;
+                if (st & kStBudget) err |= kErrRedo;
+            }
         }
+        err |= p.cnt[kCntScan].error | p.cnt[kCntSelf].error | p.cnt[kCntOwner].error;
+        const uint64_t P = p.has_msgs ? p.cnt[kCntScan].n_pairs : 0;
+        const uint32_t ovf = P > p.capacity ? 1u : 0u;
+        if (p.out) {
+            p.out->n_pairs = P;
+            p.out->n_candidates = p.has_msgs ? p.cnt[kCntScan].n_candidates : 0;
+            p.out->overflow = ovf;
+            p.out->error = err;
+        }
+        if (err) atomicOr(p.health, err);
+        if (ovf) atomicOr(p.health + 1, 1u);
     }
-    err |= p.cnt[kCntScan].error | p.cnt[kCntSelf].error | p.cnt[kCntOwner].error;
-    const uint64_t P = p.has_msgs ? p.cnt[kCntScan].n_pairs : 0;
-    const uint32_t ovf = P > p.capacity ? 1u : 0u;
-    if (p.out) {
-        p.out->n_pairs = P;
-        p.out->n_candidates = p.has_msgs ? p.cnt[kCntScan].n_candidates : 0;
-        p.out->overflow = ovf;
-        p.out->error = err;
-    }
-    if (err) atomicOr(p.health, err);
-    if (ovf) atomicOr(p.health + 1, 1u);
+    __syncthreads();
+    // the small vectors zeroed for the next tick (here, rather than a memset launch at its start)
+    for (uint32_t i = threadIdx.x; i < p.small_words; i += blockDim.x) p.zero[i] = 0u;
 }
+
 
 static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
                      const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t* d_offsets,
@@ -1396,7 +1407,9 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
     wq_route_counters* cnts = reinterpret_cast<wq_route_counters*>(small + kSmallCnt);
     const size_t small_used = kSmallCnt + 4 * sizeof(wq_route_counters);
     static_assert(kSmallC + 16 * WQ_MAX_SHARDS <= kSmallCnt, "the C vectors lie inside the zeroed span");
-    WQ_HIP(h, hipMemsetAsync(small, 0, small_used, s));  // A, C (both directions) and the counters
+    // A, C (both directions) and the counters (an asynchronous tick's last kernel zeroes them itself)
+    if (!sc.small_zeroed) WQ_HIP(h, hipMemsetAsync(small, 0, small_used, s));
+    sc.small_zeroed = false;
     if (int rc = ensure_health(h)) return rc;
     if (exact) sc.n_exact++;
     else sc.n_budget++;
@@ -1820,8 +1833,10 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
         ar.small_words = (uint32_t)(small_used / 4);
         ar.snap = static_cast<uint32_t*>(sc.asnap[k]);
         ar.seq = sc.aseq[k];
+        ar.zero = reinterpret_cast<uint32_t*>(small);
         hipLaunchKernelGGL(k_async_result, dim3(1), dim3(256), 0, s, ar);
         WQ_HIP(h, hipGetLastError());
+        sc.small_zeroed = true;
         sc.last_ready = false;  // no copy-out of an unread tick (its P is on the device)
         *n_pairs = 0;
         return WQ_OK;
