@@ -1346,9 +1346,9 @@ struct AsyncResultParams {
 // shard sees it and the next call runs exact).
 __global__ __launch_bounds__(256) void k_async_result(AsyncResultParams p) {
     for (uint32_t i = threadIdx.x; i < p.small_words; i += blockDim.x) p.snap[i] = p.small[i];
+    __threadfence_system();  // every thread's part of the snapshot visible to the host ...
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence_system();  // the snapshot before its sequence word
+    if (threadIdx.x == 0) {  // ... before the sequence word
         __hip_atomic_store(reinterpret_cast<uint64_t*>(p.snap + kSmallBytes / 4), p.seq, __ATOMIC_RELEASE,
                            __HIP_MEMORY_SCOPE_SYSTEM);
         uint32_t err = 0;
