@@ -960,6 +960,7 @@ int slots_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_
 // Unshard the latest tick into the caller's buffers (message order).
 int copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity) {
     ShardCtx& sc = *h->shard;
+    sc.small_zeroed = false;  // the scan rewrites the counters in the small vectors
     const uint64_t M = sc.last_M, P = sc.last_P;
     hipStream_t s = h->stream;
     if (sc.last_slots) {
@@ -1162,6 +1163,7 @@ static int shard_exchange_route(wq_router* h, const double* d_pos, const int64_t
     const size_t M = n_msgs;
     sc.last_ready = false;
     sc.last_slots = false;
+    sc.small_zeroed = false;  // this form writes the small vectors its own way
     int& late = *late_out;  // a local failure, reported once the tick's exchanges are complete
     std::string& late_msg = *late_msg_out;
     auto fail = [&](int rc) {
