@@ -91,6 +91,8 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--async", dest="use_async", action="store_true",
                     help="replay with wq_sharded_route_tick_async (no end-of-tick read)")
+    ap.add_argument("--form", choices=("slots", "owner"), default="slots",
+                    help="owner: wq_sharded_route_owner_device (40-B records out, the pairs stay on the owner)")
     ap.add_argument("--ticks", type=int, default=20)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -121,6 +123,10 @@ def main():
 
     def tick(g):
         m, t, offs, peers, msgs, cap = bufs[g]
+        if a.form == "owner":  # SURVEY.md §8(e) step 5, first option: this shard's pairs stay here
+            v = routers[g].sharded_route_owner_device(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(),
+                                                      t[3].data_ptr(), m)
+            return int(v.n_pairs)
         rc, P = routers[g].sharded_route_device(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), m,
                                                 offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap)
         assert rc == 0, (g, rc, P)
@@ -195,7 +201,7 @@ def main():
     exact, budgeted = r.shard_tick_stats()
     res = {"workload": f"C3 (scale {a.scale}): {M} messages, G = {G} shards; shard {a.rank} alone, its exchanges "
                        "replaying the bytes it received in a live G-shard tick (no link time)",
-           "G": G, "rank": a.rank, "async": bool(a.use_async), "messages_this_shard": bufs[a.rank][0], "pairs_this_shard": int(P),
+           "G": G, "rank": a.rank, "form": a.form, "async": bool(a.use_async), "messages_this_shard": bufs[a.rank][0], "pairs_this_shard": int(P),
            "tick_ms_alone": dt * 1e3, "ticks": a.ticks, "received_bytes_per_tick": int(sum(rec_bytes)),
            "table_build_s": round(build_s, 2), "slot_ticks_exact_budgeted": [int(exact), int(budgeted)]}
     print(json.dumps(res), flush=True)
