@@ -405,6 +405,35 @@ int wq_sharded_route_owner_device(wq_router* h, const double* d_pos, const int64
                                   const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
                                   size_t n_msgs, wq_owner_view* out);
 
+/* The owner form on budgeted 20-byte slots (first option; the per-slot
+ * lookup is area_map.rs:52-60 / local_message.rs:52-86): every message goes to the shard owning its
+ * cube as one slot (two for a key without a packed form), this shard's own messages through the
+ * self segment. The slot exchange is the tick's only collective step. Each owner routes the slots it
+ * received and keeps the pairs. The exchange sizes are budgets from the previous tick (the first
+ * tick, or one after a short budget anywhere, runs exact), so only the end of the tick reads back.
+ * Collective: every shard calls it. Received segment of source s: slots [seg[s], seg[s+1]), in
+ * the order of s's sent segment for this shard, [send_seg[me], send_seg[me+1]) on s. So slot
+ * seg[s] + k carries the message send_perm[send_seg[me] + k] of shard s (UINT32_MAX: padding, or
+ * the second slot of a wide key). Padding and second slots route to nobody. Pairs: peers[i] gets
+ * the message of received slot msgs[i], in CSR order over the received slots. Device pointers
+ * into the handle's workspace stay valid until the next sharded call. No radius filter here
+ * (wq_sharded_route_owner_device has it). */
+#define WQ_SLOT_WORDS 5
+typedef struct wq_owner_slot_view {
+    const uint32_t* slots;      /* n_slots x WQ_SLOT_WORDS words, as received */
+    const uint32_t* offsets;    /* [n_slots + 1] */
+    const uint32_t* peers;      /* [n_pairs] */
+    const uint32_t* msgs;       /* [n_pairs]: the received slot of each pair */
+    const uint32_t* send_perm;  /* this shard's sent slots -> its message index */
+    uint64_t n_slots;
+    uint64_t n_pairs;
+    uint32_t seg[WQ_MAX_SHARDS + 1];       /* received segments, per source shard */
+    uint32_t send_seg[WQ_MAX_SHARDS + 1];  /* sent segments, per owner shard */
+} wq_owner_slot_view;
+int wq_sharded_route_owner_slots(wq_router* h, const double* d_pos, const int64_t* d_keys,
+                                 const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
+                                 size_t n_msgs, wq_owner_slot_view* out);
+
 /* ---- F2: per-peer send lists (PeerMap::broadcast_to, worldql_server/src/transport/peer_map.rs:151-163)
  * The transpose of a tick's message-major CSR for a transport that batches per peer: for every
  * peer p < n_peers whose bit is set in d_connected (bit p % 32 of word p / 32; NULL = every peer

@@ -248,6 +248,197 @@ def test_hub_owner_form_vs_whole_table_oracle(G):
     hub.close()
 
 
+def _owner_slot_tick(r, pos, world, sender, repl, dev, keys=None):
+    """One wq_sharded_route_owner_slots tick of the given host arrays; the view copied to the host."""
+    import torch
+    t = [torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+         for x in (pos, world.view(np.int32), sender.view(np.int32), repl)]
+    kt = None if keys is None else torch.from_numpy(np.ascontiguousarray(keys)).to(dev)
+    torch.cuda.synchronize(dev)
+    v = r.sharded_route_owner_slots(None if kt is not None else t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(),
+                                    t[3].data_ptr(), len(world), keys_ptr=None if kt is None else kt.data_ptr())
+    R, P = int(v.n_slots), int(v.n_pairs)
+    G = r.shard_info()[0]
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    send_seg = list(v.send_seg[:G + 1])
+    offs = np.empty(R + 1, np.uint32)
+    peers = np.empty(max(P, 1), np.uint32)
+    msgs = np.empty(max(P, 1), np.uint32)
+    perm = np.empty(max(send_seg[-1], 1), np.uint32)
+    torch.cuda.synchronize(dev)
+    assert hip.hipMemcpy(offs.ctypes.data, v.offsets, (R + 1) * 4, 2) == 0
+    if P:
+        assert hip.hipMemcpy(peers.ctypes.data, v.peers, P * 4, 2) == 0
+        assert hip.hipMemcpy(msgs.ctypes.data, v.msgs, P * 4, 2) == 0
+    if send_seg[-1]:
+        assert hip.hipMemcpy(perm.ctypes.data, v.send_perm, send_seg[-1] * 4, 2) == 0
+    return dict(offs=offs, peers=peers[:P], msgs=msgs[:P], perm=perm[:send_seg[-1]], seg=list(v.seg[:G + 1]),
+                send_seg=send_seg)
+
+
+def _check_owner_slots(views, want):
+    """views[o]: owner o's tick; want[s]: (offsets, peers) the whole-table oracle gives for source
+    s's messages. Every message of every source must be routed by exactly one owner, with the
+    oracle's recipients; padding and second slots route to nobody."""
+    G = len(views)
+    got = {}
+    for o, v in enumerate(views):
+        offs, peers, msgs = v["offs"], v["peers"], v["msgs"]
+        assert offs[0] == 0 and offs[-1] == len(peers) and v["seg"][-1] == len(offs) - 1
+        assert (msgs == np.repeat(np.arange(len(offs) - 1, dtype=np.uint32), np.diff(offs.astype(np.int64)))).all()
+        for s in range(G):
+            base = views[s]["send_seg"][o]
+            assert v["seg"][s + 1] - v["seg"][s] == views[s]["send_seg"][o + 1] - base  # the budgets agree
+            for k in range(v["seg"][s + 1] - v["seg"][s]):
+                i = v["seg"][s] + k
+                m = int(views[s]["perm"][base + k])
+                if m == 0xFFFFFFFF:
+                    assert offs[i + 1] == offs[i], (o, s, k)
+                    continue
+                assert (s, m) not in got
+                got[(s, m)] = peers[offs[i]:offs[i + 1]]
+    for s in range(G):
+        w_offs, w_peers = want[s]
+        for m in range(len(w_offs) - 1):
+            assert (got.pop((s, m)) == w_peers[w_offs[m]:w_offs[m + 1]]).all(), (s, m)
+    assert not got
+
+
+@pytest.mark.parametrize("G", [1, 2, 3, 8])
+def test_hub_owner_slots_vs_whole_table_oracle(G):
+    """wq_sharded_route_owner_slots, the owner form on budgeted slots: an exact first tick, a budgeted
+    one after churn, one with four times the messages (budgets short: every shard redoes it exactly), a budgeted one again, a slot tick in between (its budgets leave out the self segment,
+    so the next owner tick runs exact) — every message routed once, against the whole-table oracle."""
+    import torch
+    from worldql_server_amd.router import Hub, Router
+    w, churn = _workload(seed=17)
+    M = len(w.world)
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    results, errors = [None] * G, []
+    barrier = threading.Barrier(G)
+
+    def body(rank):
+        try:
+            r = routers[rank]
+            r.attach_hub(hub, rank)
+            lo, hi = _slice(M, G, rank)
+            sl = (w.pos[lo:hi], w.world[lo:hi], w.sender[lo:hi], w.repl[lo:hi])
+            dbl = tuple(np.concatenate([x] * 4) for x in sl)
+            r.sharded_apply_ops(w.ops)
+            t1 = _owner_slot_tick(r, *sl, dev)
+            r.sharded_apply_ops(churn)
+            t2 = _owner_slot_tick(r, *sl, dev)
+            st2 = r.shard_tick_stats()
+            t3 = _owner_slot_tick(r, *dbl, dev)
+            st3 = r.shard_tick_stats()
+            t4 = _owner_slot_tick(r, *sl, dev)
+            slot = _tick(r, w, lo, hi, dev)
+            t5 = _owner_slot_tick(r, *sl, dev)
+            st5 = r.shard_tick_stats()
+            barrier.wait()
+            results[rank] = (t1, t2, t3, t4, slot, t5, st2, st3, st5)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+            barrier.abort()
+
+    th = [threading.Thread(target=body, args=(k,)) for k in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    assert not errors, errors
+    want1 = [_expected([w.ops], w, *_slice(M, G, s)) for s in range(G)]
+    want2 = [_expected([w.ops, churn], w, *_slice(M, G, s)) for s in range(G)]
+    want_dbl = []
+    for s in range(G):
+        lo, hi = _slice(M, G, s)
+        o = orc.COracle(w.cube_size)
+        o.apply_ops(w.ops)
+        o.apply_ops(churn)
+        dbl = [np.concatenate([x[lo:hi]] * 4) for x in (w.pos, w.world, w.sender, w.repl)]
+        want_dbl.append(o.route(*dbl)[:2])
+    _check_owner_slots([res[0] for res in results], want1)
+    for k, want in ((1, want2), (2, want_dbl), (3, want2), (5, want2)):
+        _check_owner_slots([res[k] for res in results], want)
+    for rank in range(G):
+        lo, hi = _slice(M, G, rank)
+        _check(results[rank][4], want2[rank], hi - lo)
+        st2, st3, st5 = results[rank][6:]
+        if G > 1:
+            assert st2[1] >= 1            # the second owner tick ran on budgets
+            assert st3[0] == st2[0] + 1   # four times the messages: short budgets, redone exactly
+        assert st5[0] > st3[0]            # after the slot tick: exact again
+    for r in routers:
+        r.close()
+    hub.close()
+
+
+def test_hub_owner_slots_irregular_keys_and_failure():
+    """Keys without a packed form (two slots: the second routes to nobody) by position and by raw
+    key, then local failures on one shard: before the exchange (step 1) every shard returns the
+    error, since it travels in the A vectors; after it (step 3: the owner's own routing) only that
+    shard does, the others' pairs are complete. The tick after each is right."""
+    import torch
+    from worldql_server_amd.router import Hub, Router, WQError
+    w, keys, key_ops = _irregular_workload()
+    M, G = len(w.world), 3
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    results, errors = [None] * G, []
+
+    def body(rank):
+        try:
+            r = routers[rank]
+            r.attach_hub(hub, rank)
+            lo, hi = _slice(M, G, rank)
+            sl = (w.pos[lo:hi], w.world[lo:hi], w.sender[lo:hi], w.repl[lo:hi])
+            r.sharded_apply_ops(w.ops)
+            r.sharded_apply_ops(key_ops)
+            by_pos = _owner_slot_tick(r, *sl, dev)
+            by_key = _owner_slot_tick(r, *sl, dev, keys=keys[lo:hi])
+            codes, after = [], []
+            for step in (1, 3):
+                if rank == 1:
+                    r.inject_shard_failure(step)
+                try:
+                    _owner_slot_tick(r, *sl, dev)
+                    codes.append(None)
+                except WQError as e:
+                    codes.append(e.code)
+                after.append(_owner_slot_tick(r, *sl, dev))
+            results[rank] = (by_pos, by_key, codes, after)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=body, args=(k,)) for k in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    assert not errors, errors
+    o = orc.COracle(16)
+    o.apply_ops(w.ops)
+    o.apply_ops(key_ops)
+    want_pos, want_key = [], []
+    for s in range(G):
+        lo, hi = _slice(M, G, s)
+        want_pos.append(o.route(w.pos[lo:hi], w.world[lo:hi], w.sender[lo:hi], w.repl[lo:hi])[:2])
+        want_key.append(o.route(None, w.world[lo:hi], w.sender[lo:hi], w.repl[lo:hi], keys=keys[lo:hi])[:2])
+    _check_owner_slots([res[0] for res in results], want_pos)
+    _check_owner_slots([res[1] for res in results], want_key)
+    assert [res[2][0] for res in results] == [abi.WQ_E_INVALID] * G
+    assert [res[2][1] for res in results] == [None, abi.WQ_E_INVALID, None]
+    for k in range(2):
+        _check_owner_slots([res[3][k] for res in results], want_pos)
+    for r in routers:
+        r.close()
+    hub.close()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -91,8 +91,9 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--async", dest="use_async", action="store_true",
                     help="replay with wq_sharded_route_tick_async (no end-of-tick read)")
-    ap.add_argument("--form", choices=("slots", "owner"), default="slots",
-                    help="owner: wq_sharded_route_owner_device (40-B records out, the pairs stay on the owner)")
+    ap.add_argument("--form", choices=("slots", "owner", "owner_slots"), default="slots",
+                    help="owner: wq_sharded_route_owner_device (40-B records out, the pairs stay on the owner); "
+                         "owner_slots: wq_sharded_route_owner_slots (budgeted 20-B slots, one exchange)")
     ap.add_argument("--ticks", type=int, default=20)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -126,6 +127,10 @@ def main():
         if a.form == "owner":  # SURVEY.md §8(e) step 5, first option: this shard's pairs stay here
             v = routers[g].sharded_route_owner_device(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(),
                                                       t[3].data_ptr(), m)
+            return int(v.n_pairs)
+        if a.form == "owner_slots":
+            v = routers[g].sharded_route_owner_slots(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(),
+                                                     t[3].data_ptr(), m)
             return int(v.n_pairs)
         rc, P = routers[g].sharded_route_device(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), m,
                                                 offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap)

@@ -77,7 +77,7 @@ __device__ __forceinline__ void check_stale(const TableView& t, wq_route_counter
 
 // Compact message slots of the sharded tick (wq_shard.hip shard_scatter20_kernel): five words each,
 // the kind in bits 8-15 of word 4 (its low byte is the replication code).
-constexpr int kSlotWords = 5;
+constexpr int kSlotWords = WQ_SLOT_WORDS;  // include/wq_router.h (the owner form exposes slots)
 constexpr uint32_t kSlotReg = 0, kSlotHead = 1, kSlotTail = 2;
 
 // Budgeted slot segments of the sharded tick (wq_shard.hip launch_budget_slots): owner d's slots at

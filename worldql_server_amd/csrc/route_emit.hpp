@@ -26,6 +26,9 @@ struct EmitParams {
     // emit_map_kernel in the sharded tick: rows whose info.x carries kLocPool read the received
     // cube-list pool at that word offset (wq_sharded.hip); nullptr everywhere else
     const uint32_t* pool = nullptr;
+    // emit_map_kernel: OnlySelf rows read the sender at sender[m * sender_stride] (the owner form
+    // of the sharded tick routes received slots: their sender is word 3 of 5)
+    uint32_t sender_stride = 1;
 };
 
 // LDS of one emit row (256 messages): an image of a window of the row's output, aligned to
@@ -510,7 +513,7 @@ __global__ __launch_bounds__(kBlock) void emit_map_kernel(EmitParams p) {
             base = p.pool + (inf.x & kLocMask);
             skip = inf.y;
         } else if (inf.x & kLocSelf) {
-            base = p.sender + m;
+            base = p.sender + (uint64_t)m * p.sender_stride;
         } else if (inf.x & kLocGlobal) {
             base = p.t.list + (inf.x & ~kLocGlobal) + 1;
             skip = inf.y;

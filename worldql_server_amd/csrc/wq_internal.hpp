@@ -216,6 +216,9 @@ inline TableView table_view(const wq_router* h) {
 inline uint32_t* route_health(wq_router* h) { return h->rws.buf.as<uint32_t>(); }
 // wq_route.hip
 int route_config_count();
+// 256-message tiles per block of a count or emit pass over `tiles` tiles: one for a short tick, two
+// otherwise (the grid strides over the rest) — launch_route's shapes, shared with the sharded passes
+uint32_t route_tiles_per_block(uint32_t tiles);
 // The tick's counter slots (this call's, the next call's); *cur == nullptr when M == 0 (offsets[0]
 // and both slots zeroed, nothing left to launch).
 int route_counters(wq_router* h, size_t M, uint32_t* d_offsets, wq_route_counters** cur, wq_route_counters** nxt);

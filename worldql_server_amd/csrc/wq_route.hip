@@ -99,6 +99,7 @@ constexpr uint32_t kShortTickTiles = 12288;  // 256-message tiles up to which a 
 }  // namespace
 
 int route_config_count() { return kNumCfgs; }
+uint32_t route_tiles_per_block(uint32_t tiles) { return tiles <= kShortTickTiles ? 1u : 2u; }
 
 int route_counters(wq_router* h, size_t M, uint32_t* d_offsets, wq_route_counters** cur_out,
                    wq_route_counters** nxt_out) {

@@ -40,6 +40,10 @@ struct ShardIn {
     uint32_t* own_perm = nullptr;
     bool own_too = false;
     uint32_t* zero_e = nullptr;  // slot_count_kernel: e[m] = 0 for every message (rows no step writes)
+    // slot_scatter_kernel (the owner form's budgeted tick): the budget bit of ANY of this shard's
+    // segments goes to every segment's status word, so each owner learns of every short budget
+    // from X1 alone
+    uint32_t* a_or = nullptr;
 };
 
 template <bool RAW>
@@ -423,6 +427,12 @@ __global__ void __launch_bounds__(kBlock)
     for (uint32_t k = threadIdx.x; k < kShardIPT * kWaves * WQ_MAX_SHARDS; k += kBlock) (&wc[0][0])[k] = 0;
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1;
+    if (in.a_or && blockIdx.x == 0 && threadIdx.x == 0) {  // the scan (previous launch) wrote them
+        uint32_t any = 0;
+        for (uint32_t d = 0; d < in.G; ++d) any |= in.a_or[2 * d + 1] & kStBudget;
+        if (any)
+            for (uint32_t d = 0; d < in.G; ++d) in.a_or[2 * d + 1] |= any;
+    }
     const uint32_t m0 = blockIdx.x * kShardTile + threadIdx.x;
     int64_t kx[kShardIPT], ky[kShardIPT], kz[kShardIPT];
     uint64_t pk[kShardIPT];
@@ -666,10 +676,13 @@ int launch_shard_slots(wq_router* h, const double* d_pos, const int64_t* d_keys,
 // slots in L's segments of d_slots, perm[slot] = message (kNone for tails and padding), the true
 // count and budget bit per owner at d_a[2d], d_a[2d + 1] (zeroed for this shard itself).
 // phases: 1 = the counts only (histogram + scan), 2 = the scatter and padding after them, 3 = both.
+// me = G (no shard) with own_too: every message is a slot of its owner's budgeted segment, this
+// shard's own ones included (the owner form); row_any: see ShardIn::a_or.
 int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
                         const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, uint32_t me,
                         const SlotLayout& L, uint32_t* d_slots, uint32_t* d_perm, uint32_t* d_a, int phases,
-                        bool hist_ready, bool own_too, uint32_t* own_slots, uint32_t* own_perm, uint32_t* zero_e) {
+                        bool hist_ready, bool own_too, uint32_t* own_slots, uint32_t* own_perm, uint32_t* zero_e,
+                        bool row_any) {
     hipStream_t s = h->stream;
     ShardIn in;
     in.pos = d_pos;
@@ -688,6 +701,7 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
     in.own_slots = own_slots;
     in.own_perm = own_perm;
     in.zero_e = zero_e;
+    in.a_or = row_any && (phases & 3) == 3 ? d_a : nullptr;
     if (M && (phases & 1)) {
         WQ_ALLOC(h, h->shard_hist, (uint64_t)in.nblk * G * 4);
         uint32_t* hist = h->shard_hist.as<uint32_t>();

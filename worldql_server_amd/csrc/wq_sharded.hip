@@ -52,7 +52,7 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
                         const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, uint32_t me,
                         const SlotLayout& L, uint32_t* d_slots, uint32_t* d_perm, uint32_t* d_a, int phases,
                         bool hist_ready = false, bool own_too = false, uint32_t* own_slots = nullptr,
-                        uint32_t* own_perm = nullptr, uint32_t* zero_e = nullptr);
+                        uint32_t* own_perm = nullptr, uint32_t* zero_e = nullptr, bool row_any = false);
 uint32_t budget_slot_tile();
 int launch_route_records(wq_router* h, const wq_msg_rec* d_recs, size_t M, uint32_t* d_offsets, uint32_t* d_peers,
                          uint32_t* d_msgs, size_t capacity);
@@ -173,6 +173,13 @@ static_assert(kSmallA + 4 * WQ_MAX_SHARDS * 4 <= kSmallC && kSmallC + 8 * WQ_MAX
                   kSmallCnt + 4 * sizeof(wq_route_counters) <= kSmallBytes,
               "small exchange vector layout");
 constexpr uint32_t kStCodeMask = 0xFFu;
+// Blocks of a sharded count or emit pass over n tiles, shaped as launch_route's (WQ_DEBUG_SHARD_TPB:
+// tiles per block, diagnostics)
+inline uint32_t pass_blocks(uint32_t n) {
+    static const uint32_t env = getenv("WQ_DEBUG_SHARD_TPB") ? (uint32_t)std::max(1, atoi(getenv("WQ_DEBUG_SHARD_TPB"))) : 0u;
+    const uint32_t tpb = env ? env : route_tiles_per_block(n);
+    return (n + tpb - 1) / tpb;
+}
 
 }  // namespace
 
@@ -209,6 +216,10 @@ struct ShardCtx {
     // own slots (the default with G > 1, no radius): this shard's own messages as slots of a segment
     // that is never exchanged, its slot -> message map, and the scratch tile sums of their count
     DevBuf own_slots, own_perm, own_tiles;
+    // the owner form on slots (wq_sharded_route_owner_slots): the message index of each pair's
+    // received slot; which form the budgets above were derived from (0 the slot tick, 1 this one)
+    DevBuf own_msgs;
+    int budget_form = 0;
     uint64_t claim_cap = 0;  // claim table entries (power of two); 0 = not allocated
     uint64_t ticks = 0;      // slot ticks run: the claim table's tag
     // exchange budgets of the slot tick, identical on both ends of every pair: slots me -> d and
@@ -952,7 +963,7 @@ int slots_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_
     if (sc.last_radius)  // the radius filter's emit: masks of inline rows, list and pool rows re-filtered
         hipLaunchKernelGGL((emit_kernel<4096, 2, true>), dim3(nt), dim3(kBlock), 0, s, ep);
     else
-        hipLaunchKernelGGL((emit_map_kernel<16>), dim3((nt + 1) / 2), dim3(kBlock), 0, s, ep);
+        hipLaunchKernelGGL((emit_map_kernel<16>), dim3(pass_blocks(nt)), dim3(kBlock), 0, s, ep);
     WQ_HIP(h, hipGetLastError());
     return WQ_OK;
 }
@@ -1275,11 +1286,28 @@ struct TickPicture {
     uint32_t code = 0, bits = 0, code_from = 0, bits_from = 0;
     bool over = false;
 };
-static TickPicture fold_tick(ShardCtx& sc, const char* hs) {
+static TickPicture fold_tick(ShardCtx& sc, const char* hs, bool self_seg = false) {
     const uint32_t G = sc.G, me = sc.rank;
     const uint32_t* ha = reinterpret_cast<const uint32_t*>(hs + kSmallA);
     const uint32_t* hc = reinterpret_cast<const uint32_t*>(hs + kSmallC);
     TickPicture t;
+    if (self_seg) {  // the owner form on slots: A only, the self segment budgeted like the others
+        for (uint32_t d = 0; d < G; ++d) {
+            const uint32_t st = ha[2 * G + 2 * d + 1];
+            if ((st & kStCodeMask) && !t.code) t.code = st & kStCodeMask, t.code_from = d;
+            if (((st >> 8) & 0xFFFFu) && !t.bits) t.bits = (st >> 8) & 0xFFFFu, t.bits_from = d;
+            t.over |= (st & kStBudget) != 0;
+        }
+        if (!t.code && !t.over) {
+            for (uint32_t d = 0; d < G; ++d) {
+                sc.b1_out[d] = slot_budget(ha[2 * d]);
+                sc.b1_in[d] = slot_budget(ha[2 * G + 2 * d]);
+            }
+            sc.budgets = true;
+        }
+        if (t.over) sc.budgets = false;
+        return t;
+    }
     for (uint32_t d = 0; G > 1 && d < G; ++d) {
         for (uint32_t st : {ha[2 * G + 2 * d + 1], hc[2 * G + 2 * d + 1]}) {
             if ((st & kStCodeMask) && !t.code) t.code = st & kStCodeMask, t.code_from = d;
@@ -1497,7 +1525,7 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
         cp.cnt_next = cnts + kCntScratch;
         cp.health = route_health(h);
         cp.n_tiles = nt;
-        const dim3 grid((nt + 1) / 2);  // two tiles per block (grid stride), as launch_route
+        const dim3 grid(pass_blocks(nt));  // as launch_route
         if (radius && G == 1)
             hipLaunchKernelGGL(count_radius_kernel<false>, dim3(nt), dim3(kBlock), 0, sc.side, cp);
         else if (radius)
@@ -1609,7 +1637,7 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
             cp.cnt_next = cnts + kCntScratch;
             cp.health = route_health(h);
             cp.n_tiles = nto;
-            hipLaunchKernelGGL((count_kernel<false, 1, 8, 0, false, true>), dim3((nto + 1) / 2), dim3(kBlock), 0, s, cp);
+            hipLaunchKernelGGL((count_kernel<false, 1, 8, 0, false, true>), dim3(pass_blocks(nto)), dim3(kBlock), 0, s, cp);
             if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "count launch (sharded tick)"));
         }
     }
@@ -1870,6 +1898,232 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
     return WQ_OK;
 }
 
+// ---- the owner form on budgeted slots (wq_sharded_route_owner_slots) ----
+// Every message becomes a 20-byte slot of its owner's budgeted segment — this shard's own messages
+// included (the self segment is a device copy) — and X1 {A, the slots} is the tick's only exchange:
+// each owner routes what it received where it is (count_kernel<SLOTS>, the tile scan and
+// emit_map_kernel over the received slots) and the pairs stay there (first
+// option; area_map.rs:52-60 per slot). No claims, references, pools or second exchange. The budgets
+// work as in the slot tick (the previous tick's true sizes + headroom, the first tick exact); a short
+// budget anywhere reaches every shard through X1 (ShardIn::a_or) and all of them redo the tick
+// exactly. One host read at the end: P, the statuses, the true sizes.
+static int owner_emit(wq_router* h, uint64_t Rb, const TableView& tv) {
+    ShardCtx& sc = *h->shard;
+    RouteWs& rw = h->rws;
+    hipStream_t s = h->stream;
+    const uint32_t nto = (uint32_t)(Rb / kBlock);
+    uint32_t* tiles = sc.otiles.as<uint32_t>();
+    TileScanParams tp;
+    tp.tile_total = tiles;
+    tp.tile_F = tiles + nto;
+    tp.tile_prefix = tiles + 2 * (uint64_t)nto;
+    tp.n_tiles = nto;
+    tp.offsets = sc.own_off.as<uint32_t>();
+    tp.M = (uint32_t)Rb;
+    tp.capacity = sc.own_cap;
+    tp.cnt = reinterpret_cast<wq_route_counters*>(sc.small.as<char>() + kSmallCnt) + kCntScan;
+    tp.health = nullptr;  // a short pair buffer is grown and emitted again, not an overflow
+    tp.stale = tv.stale;
+    if (int rc = launch_tile_scan(h, tp)) return rc;
+    EmitParams ep;
+    ep.sender = sc.rslots.as<uint32_t>() + 3;  // OnlySelf rows: the slot's sender word
+    ep.sender_stride = kSlotWords;
+    ep.pos = nullptr;
+    ep.repl = nullptr;
+    ep.M = (uint32_t)Rb;
+    ep.t = tv;
+    ep.e = rw.e.as<uint32_t>();
+    ep.tile_prefix = tp.tile_prefix;
+    ep.count_tile = kBlock;
+    ep.offsets = tp.offsets;
+    ep.info = rw.info.as<uint2>();
+    ep.peers = sc.own_peers.as<uint32_t>();
+    ep.msgs = sc.own_msgs.as<uint32_t>();
+    ep.capacity = sc.own_cap;
+    ep.n_blocks = nto;
+    hipLaunchKernelGGL((emit_map_kernel<16>), dim3(pass_blocks(nto)), dim3(kBlock), 0, s, ep);
+    WQ_HIP(h, hipGetLastError());
+    return WQ_OK;
+}
+
+static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                           const uint32_t* d_sender, const uint8_t* d_repl, size_t M, bool exact, int inject,
+                           bool* redo, wq_owner_slot_view* out) {
+    hipStream_t s = h->stream;
+    ShardCtx& sc = *h->shard;
+    const uint32_t G = sc.G, me = sc.rank;
+    *redo = false;
+    sc.last_ready = false;
+    sc.last_slots = false;
+    int late = WQ_OK;
+    std::string late_msg;
+    auto fail = [&](int rc) {
+        if (rc && !late) {
+            late = rc;
+            late_msg = h->err;
+        }
+        return rc;
+    };
+    auto alloc = [&](DevBuf& b, size_t bytes) -> int {
+        return b.ensure(bytes) == hipSuccess ? WQ_OK : set_error(h, WQ_E_OOM, "hipMalloc (sharded tick workspace)");
+    };
+    char* small = sc.small.as<char>();
+    uint32_t* a_send = reinterpret_cast<uint32_t*>(small + kSmallA);
+    uint32_t* a_recv = a_send + 2 * G;
+    wq_route_counters* cnts = reinterpret_cast<wq_route_counters*>(small + kSmallCnt);
+    const size_t small_used = kSmallCnt + 4 * sizeof(wq_route_counters);
+    if (!sc.small_zeroed) WQ_HIP(h, hipMemsetAsync(small, 0, small_used, s));
+    sc.small_zeroed = false;
+    if (int rc = ensure_health(h)) return rc;
+    if (exact) sc.n_exact++;
+    else sc.n_budget++;
+    std::vector<uint32_t> st_host(2 * G, 0);  // alive until the end-of-tick read
+    auto put_status = [&](uint32_t* dst) -> int {
+        for (uint32_t d = 0; d < G; ++d) st_host[2 * d + 1] = status_of(late);
+        WQ_HIP(h, hipMemcpyAsync(dst, st_host.data(), 8 * G, hipMemcpyHostToDevice, s));
+        return WQ_OK;
+    };
+    if (inject == 1) fail(set_error(h, WQ_E_INVALID, "injected failure at step 1 (test hook)"));
+    if (h->radius > 0.0 && !late)
+        fail(set_error(h, WQ_E_INVALID, "the owner form on slots has no radius filter (wq_sharded_route_owner_device has)"));
+    if (!late) fail(table_resolve(h, false));
+    const TableView tv = table_view(h);
+
+    // ---- X1: A + the slots (every owner's segment budgeted, this shard's own included) ----
+    std::vector<size_t> eight(G, 8);
+    SlotLayout L{};
+    SegBounds sb{}, rb{};
+    int rc;
+    if (exact) {  // the true counts first (A alone, read back): budgets = the counts, whole blocks
+        SlotLayout inf{};
+        for (uint32_t d = 0; d < G; ++d) inf.budget[d] = 0xFFFFFFFFu;
+        if (!late)
+            fail(launch_budget_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, G, inf, nullptr, nullptr,
+                                     a_send, 1, false, true));
+        if (late && (rc = put_status(a_send))) return rc;
+        Xfer x{{a_send}, {eight.data()}, {a_recv}, {eight.data()}, 1};
+        if ((rc = exchange(h, x))) return rc;
+        uint32_t* hv = static_cast<uint32_t*>(sc.hsmall);
+        WQ_HIP(h, hipMemcpyAsync(hv, a_send, 16 * G, hipMemcpyDeviceToHost, s));
+        WQ_HIP(h, hipStreamSynchronize(s));
+        for (uint32_t d = 0; d < G; ++d) {
+            sc.b1_out[d] = whole_blocks(hv[2 * d]);
+            sc.b1_in[d] = whole_blocks(hv[2 * G + 2 * d]);
+        }
+    }
+    uint64_t so = 0, ro = 0;
+    for (uint32_t d = 0; d < G; ++d) {
+        L.base[d] = (uint32_t)so;
+        L.budget[d] = sc.b1_out[d];
+        sb.b[d] = (uint32_t)so;
+        rb.b[d] = (uint32_t)ro;
+        so += sc.b1_out[d];
+        ro += sc.b1_in[d];
+    }
+    if (so >= (1ull << 31) || ro >= (1ull << 31)) return fatal_receive(h, "sharded tick: more than 2^31 slots");
+    L.base[G] = sb.b[G] = (uint32_t)so;
+    rb.b[G] = (uint32_t)ro;
+    const uint64_t Sb = so, Rb = ro;
+    if (alloc(sc.slots, (Sb + 2) * kSlotWords * 4) || alloc(sc.perm, (Sb + 2) * 4) ||
+        alloc(sc.rslots, (Rb + 2) * kSlotWords * 4))
+        return fatal_receive(h, "hipMalloc of the sharded tick's slots");
+    if (!late)
+        fail(launch_budget_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, G, L, sc.slots.as<uint32_t>(),
+                                 sc.perm.as<uint32_t>(), a_send, exact ? 2 : 3, false, true, nullptr, nullptr, nullptr,
+                                 !exact));
+    if (late) {  // nothing to send: tail slots everywhere
+        WQ_HIP(h, hipMemsetAsync(sc.slots.p, 0, (Sb + 1) * kSlotWords * 4, s));
+        WQ_HIP(h, hipMemsetAsync(sc.perm.p, 0xFF, (Sb + 1) * 4, s));
+        if (!exact && (rc = put_status(a_send))) return rc;
+    }
+    std::vector<size_t> sbytes(G), rbytes(G);
+    uint64_t sent = 0, recvd = 0;
+    for (uint32_t d = 0; d < G; ++d) {
+        sbytes[d] = (size_t)sc.b1_out[d] * kSlotWords * 4;
+        rbytes[d] = (size_t)sc.b1_in[d] * kSlotWords * 4;
+        if (d != me) {
+            sent += 8 + sbytes[d];
+            recvd += 8 + rbytes[d];
+        }
+    }
+    if (exact) {
+        Xfer x{{sc.slots.p}, {sbytes.data()}, {sc.rslots.p}, {rbytes.data()}, 1};
+        if ((rc = exchange(h, x))) return rc;
+    } else {
+        Xfer x{{a_send, sc.slots.p}, {eight.data(), sbytes.data()}, {a_recv, sc.rslots.p},
+               {eight.data(), rbytes.data()}, 2};
+        if ((rc = exchange(h, x))) return rc;
+    }
+    sc.last_sent = sent;
+    sc.last_recv = recvd;
+
+    // ---- the owner: count the received slots, the tile scan, the emit; the pairs stay here ----
+    if (inject == 3) fail(set_error(h, WQ_E_INVALID, "injected failure at step 3 (test hook)"));
+    RouteWs& rw = h->rws;
+    const uint32_t nto = (uint32_t)(Rb / kBlock);  // whole blocks
+    if (!sc.own_cap) sc.own_cap = std::min<uint64_t>(8 * Rb + 4096, 0xFFFFFFFFull);
+    if (!late && (fail(alloc(rw.e, (Rb + 1) * 4)) || fail(alloc(rw.info, (Rb + 1) * 8)) ||
+                  fail(alloc(sc.otiles, ((uint64_t)nto * 3 + 4) * 4)) || fail(alloc(sc.own_off, (Rb + 1) * 4)) ||
+                  fail(alloc(sc.own_peers, sc.own_cap * 4)) || fail(alloc(sc.own_msgs, sc.own_cap * 4)))) {
+    }
+    if (!late && Rb) {
+        CountParams cp{};
+        cp.in = RouteIn{nullptr, nullptr, nullptr, nullptr, nullptr, (uint32_t)Rb, (int64_t)h->cube_size};
+        cp.in.slots = sc.rslots.as<uint32_t>();
+        cp.t = tv;
+        cp.e = rw.e.as<uint32_t>();
+        cp.info = rw.info.as<uint2>();
+        cp.tile_total = sc.otiles.as<uint32_t>();
+        cp.tile_F = cp.tile_total + nto;
+        cp.cnt = cnts + kCntOwner;
+        cp.cnt_next = cnts + kCntScratch;
+        cp.health = route_health(h);
+        cp.n_tiles = nto;
+        hipLaunchKernelGGL((count_kernel<false, 1, 8, 0, false, true>), dim3(pass_blocks(nto)), dim3(kBlock), 0, s, cp);
+        if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "count launch (owner form)"));
+        if (!late) fail(owner_emit(h, Rb, tv));
+    }
+
+    // ---- the one host read ----
+    WQ_HIP(h, hipMemcpyAsync(sc.hsmall, small, small_used, hipMemcpyDeviceToHost, s));
+    WQ_HIP(h, hipStreamSynchronize(s));
+    const char* hs = static_cast<const char*>(sc.hsmall);
+    const wq_route_counters* hcnt = reinterpret_cast<const wq_route_counters*>(hs + kSmallCnt);
+    const TickPicture tp = fold_tick(sc, hs, true);
+    if (late) {
+        h->err = late_msg;
+        return late;
+    }
+    if (tp.code) return status_error(h, tp.code, tp.code_from);
+    if (tp.over) {  // every shard saw it: all of them redo the tick exactly
+        *redo = true;
+        return WQ_OK;
+    }
+    if (tp.bits) return status_error(h, (uint64_t)tp.bits << 32, tp.bits_from);
+    const uint32_t err = Rb ? (hcnt[kCntScan].error | hcnt[kCntOwner].error) : 0u;
+    if (err) return status_error(h, (uint64_t)err << 32, me);
+    const uint64_t P = Rb ? hcnt[kCntScan].n_pairs : 0;
+    if (P > sc.own_cap) {  // the pair buffers were short: grow them and emit again (the rows are kept)
+        sc.own_cap = std::min<uint64_t>(P + P / 4 + 4096, 0xFFFFFFFFull);
+        if (alloc(sc.own_peers, sc.own_cap * 4) || alloc(sc.own_msgs, sc.own_cap * 4)) return WQ_E_OOM;
+        if ((rc = owner_emit(h, Rb, tv))) return rc;
+        WQ_HIP(h, hipStreamSynchronize(s));
+    }
+    if (!Rb) WQ_HIP(h, hipMemsetAsync(sc.own_off.p, 0, 4, s));
+    out->slots = sc.rslots.as<uint32_t>();
+    out->offsets = sc.own_off.as<uint32_t>();
+    out->peers = sc.own_peers.as<uint32_t>();
+    out->msgs = sc.own_msgs.as<uint32_t>();
+    out->send_perm = sc.perm.as<uint32_t>();
+    out->n_slots = Rb;
+    out->n_pairs = P;
+    for (uint32_t d = 0; d <= G; ++d) {
+        out->seg[d] = rb.b[d];
+        out->send_seg[d] = sb.b[d];
+    }
+    return WQ_OK;
+}
+
 static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
                               const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t* d_offsets,
                               uint32_t* d_peers, uint32_t* d_msgs, size_t capacity, size_t* n_pairs, bool async = false,
@@ -1878,6 +2132,10 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
     // earlier asynchronous ticks first: a synchronous tick folds them all in; an asynchronous one
     // keeps the latest in flight (its budgets come from the tick before), unless it must run exact
     if (int rc = async_drain(h, async && sc.budgets ? 1u : 0u)) return rc;
+    if (sc.budget_form != 0) {  // the owner form's budgets include the self segment: run exact
+        sc.budgets = false;
+        sc.budget_form = 0;
+    }
     const int inject = h->shard_inject;
     h->shard_inject = 0;
     bool redo = false;
@@ -2081,6 +2339,29 @@ int wq_sharded_route_owner_device(wq_router* h, const double* d_pos, const int64
     out->n_pairs = R ? c.n_pairs : 0;
     for (uint32_t d = 0; d <= sc.G; ++d) out->seg[d] = seg.b[d];
     return WQ_OK;
+}
+
+int wq_sharded_route_owner_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                                 const uint32_t* d_sender, const uint8_t* d_repl, size_t n_msgs,
+                                 wq_owner_slot_view* out) {
+    if (!h || !out || (n_msgs && (!d_world || !d_sender || !d_repl || (!d_pos && !d_keys)))) return WQ_E_INVALID;
+    if (n_msgs >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
+    WQ_HIP(h, hipSetDevice(h->device));
+    if (!h->shard) return set_error(h, WQ_E_INVALID, "no exchange attached (wq_shard_attach_*)");
+    memset(out, 0, sizeof(*out));
+    ShardCtx& sc = *h->shard;
+    if (int rc = async_drain(h, 0)) return rc;  // the slot tick's asynchronous ticks, folded first
+    if (sc.budget_form != 1) {  // budgets of the slot tick leave out the self segment: run exact
+        sc.budgets = false;
+        sc.budget_form = 1;
+    }
+    const int inject = h->shard_inject;
+    h->shard_inject = 0;
+    bool redo = false;
+    int rc = owner_slot_tick(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, !sc.budgets, inject, &redo, out);
+    if (rc == WQ_OK && redo)
+        rc = owner_slot_tick(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, true, 0, &redo, out);
+    return rc;
 }
 
 int wq_sharded_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity) {

@@ -108,6 +108,7 @@ def load_library(build_if_missing: bool = True):
         "wq_sharded_route_tick_async": ([vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, vp], i32),
         "wq_sharded_copy_out": ([vp, vp, vp, vp, sz], i32),
         "wq_sharded_route_owner_device": ([vp, vp, vp, vp, vp, vp, sz, ctypes.POINTER(abi.OwnerView)], i32),
+        "wq_sharded_route_owner_slots": ([vp, vp, vp, vp, vp, vp, sz, ctypes.POINTER(abi.OwnerSlotView)], i32),
         "wq_shard_last_bytes": ([vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], i32),
         "wq_debug_set_shard_form": ([vp, i32], i32),
         "wq_debug_inject_shard_failure": ([vp, i32], i32),
@@ -422,6 +423,16 @@ class Router:
         self._check(self.lib.wq_sharded_route_owner_device(self.h, pos_ptr or None, keys_ptr or None, world_ptr or None,
                                                            sender_ptr or None, repl_ptr or None, n_msgs,
                                                            ctypes.byref(v)))
+        return v
+
+    def sharded_route_owner_slots(self, pos_ptr, world_ptr, sender_ptr, repl_ptr, n_msgs, keys_ptr=None):
+        """wq_sharded_route_owner_slots: the owner form on budgeted 20-byte slots (one exchange per
+        tick; the pairs stay on the owner). Returns an abi.OwnerSlotView of device pointers valid
+        until the next sharded call."""
+        v = abi.OwnerSlotView()
+        self._check(self.lib.wq_sharded_route_owner_slots(self.h, pos_ptr or None, keys_ptr or None, world_ptr or None,
+                                                          sender_ptr or None, repl_ptr or None, n_msgs,
+                                                          ctypes.byref(v)))
         return v
 
     def sharded_copy_out(self, offsets_ptr, peers_ptr, msgs_ptr, capacity) -> None:
