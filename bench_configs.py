@@ -412,19 +412,27 @@ def _c3_cube(a, w, rank, world_size, local_rank, dev, stream, sl, owner_form: bo
            "subscriptions_this_shard": int(st["n_entries"]), "xgmi_bytes_per_gpu": int(sent_max),
            "exact_ticks": exact, "budgeted_ticks": budgeted}
     if owner_form:
-        # SURVEY.md §8(e) step 5's other option: the pairs left on the owner (no return exchange)
+        # SURVEY.md §8(e) step 5's other option: the pairs left on the owner — wq_sharded_route_owner_slots,
+        # budgeted 20-byte slots out and nothing back (one exchange per tick, one host read at its end)
         own = {"P": 0}
 
         def tick_owner():
-            v = r.sharded_route_owner_device(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M)
+            v = r.sharded_route_owner_slots(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M)
             own["P"] = int(v.n_pairs)
-        for _ in range(max(a.warmup, 1)):
+        for _ in range(max(a.warmup, 2)):
             tick_owner()
+        e0, b0 = r.shard_tick_stats()
         t_ms = timed_ticks(tick_owner, a.steps, stream, dev, world_size, [r])
+        e1, b1 = r.shard_tick_stats()
         t2, pairs_own = reduce_over_ranks(t_ms, own["P"], dev, world_size)
         assert pairs_own == pairs_all, (pairs_own, pairs_all)  # every pair routed exactly once
+        sent_o, _ = r.shard_last_bytes()
+        sent_o_max, _ = reduce_over_ranks(float(sent_o), 0, dev, world_size)
         out["pairs_on_owner"] = {"value": pairs_own * a.steps / (t2 / 1e3), "unit": "pairs/s",
-                                 "ms_per_step": t2 / a.steps, "note": "same tick, pairs left on the owning GPU"}
+                                 "ms_per_step": t2 / a.steps, "xgmi_bytes_per_gpu": int(sent_o_max),
+                                 "exact_ticks_timed": e1 - e0, "budgeted_ticks_timed": b1 - b0,
+                                 "note": "wq_sharded_route_owner_slots: the same tick's pairs left on the owning "
+                                         "GPU (20-byte slots out, no return exchange)"}
     r.close()
     del peers, msgs
     return out

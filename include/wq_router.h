@@ -414,16 +414,15 @@ int wq_sharded_route_owner_device(wq_router* h, const double* d_pos, const int64
  * Collective: every shard calls it. Received segment of source s: slots [seg[s], seg[s+1]), in
  * the order of s's sent segment for this shard, [send_seg[me], send_seg[me+1]) on s. So slot
  * seg[s] + k carries the message send_perm[send_seg[me] + k] of shard s (UINT32_MAX: padding, or
- * the second slot of a wide key). Padding and second slots route to nobody. Pairs: peers[i] gets
- * the message of received slot msgs[i], in CSR order over the received slots. Device pointers
- * into the handle's workspace stay valid until the next sharded call. No radius filter here
- * (wq_sharded_route_owner_device has it). */
+ * the second slot of a wide key). Padding and second slots route to nobody. The pairs are a CSR
+ * over the received slots: slot i's recipients are peers[offsets[i] .. offsets[i+1]). Device
+ * pointers into the handle's workspace stay valid until the next sharded call. No radius filter
+ * here (wq_sharded_route_owner_device has it). */
 #define WQ_SLOT_WORDS 5
 typedef struct wq_owner_slot_view {
     const uint32_t* slots;      /* n_slots x WQ_SLOT_WORDS words, as received */
     const uint32_t* offsets;    /* [n_slots + 1] */
     const uint32_t* peers;      /* [n_pairs] */
-    const uint32_t* msgs;       /* [n_pairs]: the received slot of each pair */
     const uint32_t* send_perm;  /* this shard's sent slots -> its message index */
     uint64_t n_slots;
     uint64_t n_pairs;

@@ -92,7 +92,7 @@ SLOT_WORDS = 5  # WQ_SLOT_WORDS
 
 class OwnerSlotView(ctypes.Structure):  # struct wq_owner_slot_view
     _fields_ = [("slots", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("peers", ctypes.c_void_p),
-                ("msgs", ctypes.c_void_p), ("send_perm", ctypes.c_void_p), ("n_slots", ctypes.c_uint64),
+                ("send_perm", ctypes.c_void_p), ("n_slots", ctypes.c_uint64),
                 ("n_pairs", ctypes.c_uint64), ("seg", ctypes.c_uint32 * (MAX_SHARDS + 1)),
                 ("send_seg", ctypes.c_uint32 * (MAX_SHARDS + 1))]
 

@@ -216,9 +216,7 @@ struct ShardCtx {
     // own slots (the default with G > 1, no radius): this shard's own messages as slots of a segment
     // that is never exchanged, its slot -> message map, and the scratch tile sums of their count
     DevBuf own_slots, own_perm, own_tiles;
-    // the owner form on slots (wq_sharded_route_owner_slots): the message index of each pair's
-    // received slot; which form the budgets above were derived from (0 the slot tick, 1 this one)
-    DevBuf own_msgs;
+    // which form the budgets above were derived from (0 the slot tick, 1 wq_sharded_route_owner_slots)
     int budget_form = 0;
     uint64_t claim_cap = 0;  // claim table entries (power of two); 0 = not allocated
     uint64_t ticks = 0;      // slot ticks run: the claim table's tag
@@ -1938,7 +1936,7 @@ static int owner_emit(wq_router* h, uint64_t Rb, const TableView& tv) {
     ep.offsets = tp.offsets;
     ep.info = rw.info.as<uint2>();
     ep.peers = sc.own_peers.as<uint32_t>();
-    ep.msgs = sc.own_msgs.as<uint32_t>();
+    ep.msgs = nullptr;  // the CSR over the received slots says whose each pair is
     ep.capacity = sc.own_cap;
     ep.n_blocks = nto;
     hipLaunchKernelGGL((emit_map_kernel<16>), dim3(pass_blocks(nto)), dim3(kBlock), 0, s, ep);
@@ -2064,7 +2062,7 @@ static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_k
     if (!sc.own_cap) sc.own_cap = std::min<uint64_t>(8 * Rb + 4096, 0xFFFFFFFFull);
     if (!late && (fail(alloc(rw.e, (Rb + 1) * 4)) || fail(alloc(rw.info, (Rb + 1) * 8)) ||
                   fail(alloc(sc.otiles, ((uint64_t)nto * 3 + 4) * 4)) || fail(alloc(sc.own_off, (Rb + 1) * 4)) ||
-                  fail(alloc(sc.own_peers, sc.own_cap * 4)) || fail(alloc(sc.own_msgs, sc.own_cap * 4)))) {
+                  fail(alloc(sc.own_peers, sc.own_cap * 4)))) {
     }
     if (!late && Rb) {
         CountParams cp{};
@@ -2105,7 +2103,7 @@ static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_k
     const uint64_t P = Rb ? hcnt[kCntScan].n_pairs : 0;
     if (P > sc.own_cap) {  // the pair buffers were short: grow them and emit again (the rows are kept)
         sc.own_cap = std::min<uint64_t>(P + P / 4 + 4096, 0xFFFFFFFFull);
-        if (alloc(sc.own_peers, sc.own_cap * 4) || alloc(sc.own_msgs, sc.own_cap * 4)) return WQ_E_OOM;
+        if (alloc(sc.own_peers, sc.own_cap * 4)) return WQ_E_OOM;
         if ((rc = owner_emit(h, Rb, tv))) return rc;
         WQ_HIP(h, hipStreamSynchronize(s));
     }
@@ -2113,7 +2111,6 @@ static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_k
     out->slots = sc.rslots.as<uint32_t>();
     out->offsets = sc.own_off.as<uint32_t>();
     out->peers = sc.own_peers.as<uint32_t>();
-    out->msgs = sc.own_msgs.as<uint32_t>();
     out->send_perm = sc.perm.as<uint32_t>();
     out->n_slots = Rb;
     out->n_pairs = P;
