@@ -412,27 +412,29 @@ def _c3_cube(a, w, rank, world_size, local_rank, dev, stream, sl, owner_form: bo
            "subscriptions_this_shard": int(st["n_entries"]), "xgmi_bytes_per_gpu": int(sent_max),
            "exact_ticks": exact, "budgeted_ticks": budgeted}
     if owner_form:
-        # SURVEY.md §8(e) step 5's other option: the pairs left on the owner — wq_sharded_route_owner_slots,
-        # budgeted 20-byte slots out and nothing back (one exchange per tick, one host read at its end)
-        own = {"P": 0}
+        # SURVEY.md §8(e) step 5's other option: the pairs left on the owner — wq_sharded_route_owner_slots_async,
+        # budgeted 20-byte slots out and nothing back (one exchange per tick, no end-of-tick read)
+        cnt_o = torch.zeros(24, dtype=torch.uint8, device=dev)
 
         def tick_owner():
-            v = r.sharded_route_owner_slots(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M)
-            own["P"] = int(v.n_pairs)
-        for _ in range(max(a.warmup, 2)):
+            r.sharded_route_owner_slots_async(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M,
+                                              cnt_o.data_ptr())
+        for _ in range(max(a.warmup, 3)):
             tick_owner()
         e0, b0 = r.shard_tick_stats()
         t_ms = timed_ticks(tick_owner, a.steps, stream, dev, world_size, [r])
         e1, b1 = r.shard_tick_stats()
-        t2, pairs_own = reduce_over_ranks(t_ms, own["P"], dev, world_size)
+        co = _counters(cnt_o)[0]
+        assert co["error"] == 0 and co["overflow"] == 0, co
+        t2, pairs_own = reduce_over_ranks(t_ms, int(co["n_pairs"]), dev, world_size)
         assert pairs_own == pairs_all, (pairs_own, pairs_all)  # every pair routed exactly once
         sent_o, _ = r.shard_last_bytes()
         sent_o_max, _ = reduce_over_ranks(float(sent_o), 0, dev, world_size)
         out["pairs_on_owner"] = {"value": pairs_own * a.steps / (t2 / 1e3), "unit": "pairs/s",
                                  "ms_per_step": t2 / a.steps, "xgmi_bytes_per_gpu": int(sent_o_max),
                                  "exact_ticks_timed": e1 - e0, "budgeted_ticks_timed": b1 - b0,
-                                 "note": "wq_sharded_route_owner_slots: the same tick's pairs left on the owning "
-                                         "GPU (20-byte slots out, no return exchange)"}
+                                 "note": "wq_sharded_route_owner_slots_async: the same tick's pairs left on the "
+                                         "owning GPU (20-byte slots out, no return exchange, no end-of-tick read)"}
     r.close()
     del peers, msgs
     return out

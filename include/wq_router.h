@@ -432,6 +432,16 @@ typedef struct wq_owner_slot_view {
 int wq_sharded_route_owner_slots(wq_router* h, const double* d_pos, const int64_t* d_keys,
                                  const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
                                  size_t n_msgs, wq_owner_slot_view* out);
+/* The same without the end-of-tick read (as wq_sharded_route_tick_async): a budgeted tick returns
+ * once enqueued, with out->n_pairs = UINT64_MAX; P and the status bits land in d_counters (device;
+ * nullable) and the sticky health words (error bit 64: a budget was too small, the tick's outputs
+ * are not valid and the next call runs exact; overflow: the handle's pair buffer was short, the
+ * outputs are truncated and the buffer grows for the tick after next). A tick that must run exact
+ * (the first, one after a short budget, one after the slot tick) runs synchronously and fills
+ * n_pairs. The view's arrays are rewritten by the next tick on the handle's stream. */
+int wq_sharded_route_owner_slots_async(wq_router* h, const double* d_pos, const int64_t* d_keys,
+                                       const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
+                                       size_t n_msgs, wq_route_counters* d_counters, wq_owner_slot_view* out);
 
 /* ---- F2: per-peer send lists (PeerMap::broadcast_to, worldql_server/src/transport/peer_map.rs:151-163)
  * The transpose of a tick's message-major CSR for a transport that batches per peer: for every

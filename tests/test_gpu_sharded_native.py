@@ -374,6 +374,108 @@ def test_hub_owner_slots_vs_whole_table_oracle(G):
     hub.close()
 
 
+def _view_to_host(r, v, G):
+    """An owner-slot view (its tick finished) copied to the host, as _owner_slot_tick returns it."""
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    R = int(v.n_slots)
+    send_seg = list(v.send_seg[:G + 1])
+    offs = np.empty(R + 1, np.uint32)
+    perm = np.empty(max(send_seg[-1], 1), np.uint32)
+    assert hip.hipMemcpy(offs.ctypes.data, v.offsets, (R + 1) * 4, 2) == 0
+    P = int(offs[-1])
+    peers = np.empty(max(P, 1), np.uint32)
+    if P:
+        assert hip.hipMemcpy(peers.ctypes.data, v.peers, P * 4, 2) == 0
+    if send_seg[-1]:
+        assert hip.hipMemcpy(perm.ctypes.data, v.send_perm, send_seg[-1] * 4, 2) == 0
+    return dict(offs=offs, peers=peers[:P], perm=perm[:send_seg[-1]], seg=list(v.seg[:G + 1]), send_seg=send_seg)
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_hub_owner_slots_async_vs_whole_table_oracle(G):
+    """wq_sharded_route_owner_slots_async: the first call runs exact (synchronously, n_pairs filled),
+    the next ones return at once with P in the caller's counters; the last tick's view against the
+    whole-table oracle; four times the messages on budgets: error bit 64 on every shard (outputs not
+    valid); a synchronous call after it folds that tick in, redoes itself exactly and is right."""
+    import torch
+    from worldql_server_amd.router import Hub, Router
+    w, churn = _workload(seed=23)
+    M = len(w.world)
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    results, errors = [None] * G, []
+    counters_dtype = abi.COUNTERS_DTYPE
+
+    def body(rank):
+        try:
+            r = routers[rank]
+            r.attach_hub(hub, rank)
+            lo, hi = _slice(M, G, rank)
+            r.sharded_apply_ops(w.ops)
+            r.sharded_apply_ops(churn)
+            arr = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in
+                   (w.pos[lo:hi], w.world[lo:hi].view(np.int32), w.sender[lo:hi].view(np.int32), w.repl[lo:hi])]
+            quad = [torch.cat([x] * 4) for x in arr]
+            cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize(dev)
+
+            def tick(a):
+                return r.sharded_route_owner_slots_async(a[0].data_ptr(), a[1].data_ptr(), a[2].data_ptr(),
+                                                         a[3].data_ptr(), len(a[1]), cnt.data_ptr())
+            first = tick(arr)
+            n_first = int(first.n_pairs)
+            for _ in range(3):
+                v = tick(arr)
+            torch.cuda.synchronize(dev)
+            c_last = cnt.cpu().numpy().view(counters_dtype)[0].copy()
+            view_last = _view_to_host(r, v, G)
+            r.route_health()  # clear
+            vq = tick(quad)   # budgets short everywhere
+            torch.cuda.synchronize(dev)
+            c_quad = cnt.cpu().numpy().view(counters_dtype)[0].copy()
+            sync_quad = int(vq.n_pairs) != 2 ** 64 - 1
+            health = r.route_health()
+            # synchronous: folds the flagged tick in and redoes itself exactly
+            after = r.sharded_route_owner_slots(quad[0].data_ptr(), quad[1].data_ptr(), quad[2].data_ptr(),
+                                                quad[3].data_ptr(), len(quad[1]))
+            torch.cuda.synchronize(dev)
+            results[rank] = (n_first, c_last, view_last, c_quad, sync_quad, health, int(after.n_pairs),
+                             _view_to_host(r, after, G), r.shard_tick_stats())
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=body, args=(k,)) for k in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    assert not errors, errors
+    want = [_expected([w.ops, churn], w, *_slice(M, G, s)) for s in range(G)]
+    _check_owner_slots([res[2] for res in results], want)
+    want_quad = []
+    for s in range(G):
+        lo, hi = _slice(M, G, s)
+        o = orc.COracle(w.cube_size)
+        o.apply_ops(w.ops)
+        o.apply_ops(churn)
+        want_quad.append(o.route(*[np.concatenate([x[lo:hi]] * 4) for x in (w.pos, w.world, w.sender, w.repl)])[:2])
+    _check_owner_slots([res[7] for res in results], want_quad)
+    for rank in range(G):
+        n_first, c_last, view_last, c_quad, sync_quad, health, n_after, _, stats = results[rank]
+        assert n_first != 2 ** 64 - 1                      # the first tick ran exact
+        assert c_last["error"] == 0 and c_last["overflow"] == 0
+        assert int(c_last["n_pairs"]) == int(view_last["offs"][-1])
+        assert not sync_quad and (int(c_quad["error"]) & 64)  # the short budgets, seen on every shard
+        assert health[0] & 64
+        assert n_after == int(results[rank][7]["offs"][-1])
+        assert stats[1] >= 3                               # asynchronous ticks ran on budgets
+    for r in routers:
+        r.close()
+    hub.close()
+
+
 def test_hub_owner_slots_irregular_keys_and_failure():
     """Keys without a packed form (two slots: the second routes to nobody) by position and by raw
     key, then local failures on one shard: before the exchange (step 1) every shard returns the

@@ -141,6 +141,10 @@ def main():
 
     def tick_async(g):
         m, t, offs, peers, msgs, cap = bufs[g]
+        if a.form == "owner_slots":
+            routers[g].sharded_route_owner_slots_async(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(),
+                                                       t[3].data_ptr(), m, cnt.data_ptr())
+            return
         routers[g].sharded_route_async(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), m,
                                        offs.data_ptr(), peers.data_ptr(), msgs.data_ptr(), cap, cnt.data_ptr())
 

@@ -1342,7 +1342,12 @@ static int async_drain(wq_router* h, uint32_t keep) {
             std::this_thread::yield();
         }
         std::atomic_thread_fence(std::memory_order_acquire);
-        (void)fold_tick(sc, static_cast<const char*>(sc.asnap[k]));
+        const char* snap = static_cast<const char*>(sc.asnap[k]);
+        (void)fold_tick(sc, snap, sc.budget_form == 1);  // the ring only ever holds one form's ticks
+        if (sc.budget_form == 1) {  // the owner form: a pair buffer that was short grows for the next tick
+            const uint64_t P = reinterpret_cast<const wq_route_counters*>(snap + kSmallCnt)[kCntScan].n_pairs;
+            if (P > sc.own_cap) sc.own_cap = std::min<uint64_t>(P + P / 4 + 4096, 0xFFFFFFFFull);
+        }
         sc.ahead = (k + 1) % ShardCtx::kRing;
         sc.acount--;
     }
@@ -1946,7 +1951,8 @@ static int owner_emit(wq_router* h, uint64_t Rb, const TableView& tv) {
 
 static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
                            const uint32_t* d_sender, const uint8_t* d_repl, size_t M, bool exact, int inject,
-                           bool* redo, wq_owner_slot_view* out) {
+                           bool* redo, wq_owner_slot_view* out, bool async = false,
+                           wq_route_counters* d_result = nullptr) {
     hipStream_t s = h->stream;
     ShardCtx& sc = *h->shard;
     const uint32_t G = sc.G, me = sc.rank;
@@ -2082,6 +2088,48 @@ static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_k
         if (!late) fail(owner_emit(h, Rb, tv));
     }
 
+    auto fill_view = [&](uint64_t P) {
+        out->slots = sc.rslots.as<uint32_t>();
+        out->offsets = sc.own_off.as<uint32_t>();
+        out->peers = sc.own_peers.as<uint32_t>();
+        out->send_perm = sc.perm.as<uint32_t>();
+        out->n_slots = Rb;
+        out->n_pairs = P;
+        for (uint32_t d = 0; d <= G; ++d) {
+            out->seg[d] = rb.b[d];
+            out->send_seg[d] = sb.b[d];
+        }
+    };
+    // ---- asynchronous end (a budgeted tick without a local failure): as the slot tick's — the
+    // small vectors to a pinned snapshot folded in two calls later, P and the statuses to the
+    // caller's counters and the health words; a pair buffer that was short shows as overflow ----
+    if (async && !exact && !late) {
+        if (!Rb) WQ_HIP(h, hipMemsetAsync(sc.own_off.p, 0, 4, s));
+        const uint32_t k = (sc.ahead + sc.acount) % ShardCtx::kRing;  // async_drain left a free slot
+        sc.acount++;
+        sc.n_async++;
+        sc.aseq[k] = sc.n_async;
+        AsyncResultParams ar{};
+        ar.a_recv = a_recv;
+        ar.c_recv = reinterpret_cast<const uint32_t*>(small + kSmallC) + 2 * G;  // zero: no second exchange
+        ar.G = G;
+        ar.cnt = cnts;
+        ar.has_msgs = Rb ? 1u : 0u;
+        ar.capacity = sc.own_cap;
+        ar.out = d_result;
+        ar.health = route_health(h);
+        ar.small = reinterpret_cast<const uint32_t*>(small);
+        ar.small_words = (uint32_t)(small_used / 4);
+        ar.snap = static_cast<uint32_t*>(sc.asnap[k]);
+        ar.seq = sc.aseq[k];
+        ar.zero = reinterpret_cast<uint32_t*>(small);
+        hipLaunchKernelGGL(k_async_result, dim3(1), dim3(256), 0, s, ar);
+        WQ_HIP(h, hipGetLastError());
+        sc.small_zeroed = true;
+        fill_view(~0ull);  // P: in the caller's counters
+        return WQ_OK;
+    }
+
     // ---- the one host read ----
     WQ_HIP(h, hipMemcpyAsync(sc.hsmall, small, small_used, hipMemcpyDeviceToHost, s));
     WQ_HIP(h, hipStreamSynchronize(s));
@@ -2108,16 +2156,7 @@ static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_k
         WQ_HIP(h, hipStreamSynchronize(s));
     }
     if (!Rb) WQ_HIP(h, hipMemsetAsync(sc.own_off.p, 0, 4, s));
-    out->slots = sc.rslots.as<uint32_t>();
-    out->offsets = sc.own_off.as<uint32_t>();
-    out->peers = sc.own_peers.as<uint32_t>();
-    out->send_perm = sc.perm.as<uint32_t>();
-    out->n_slots = Rb;
-    out->n_pairs = P;
-    for (uint32_t d = 0; d <= G; ++d) {
-        out->seg[d] = rb.b[d];
-        out->send_seg[d] = sb.b[d];
-    }
+    fill_view(P);
     return WQ_OK;
 }
 
@@ -2128,10 +2167,12 @@ static int sharded_tick_slots(wq_router* h, const double* d_pos, const int64_t* 
     ShardCtx& sc = *h->shard;
     // earlier asynchronous ticks first: a synchronous tick folds them all in; an asynchronous one
     // keeps the latest in flight (its budgets come from the tick before), unless it must run exact
-    if (int rc = async_drain(h, async && sc.budgets ? 1u : 0u)) return rc;
     if (sc.budget_form != 0) {  // the owner form's budgets include the self segment: run exact
+        if (int rc = async_drain(h, 0)) return rc;
         sc.budgets = false;
         sc.budget_form = 0;
+    } else if (int rc = async_drain(h, async && sc.budgets ? 1u : 0u)) {
+        return rc;
     }
     const int inject = h->shard_inject;
     h->shard_inject = 0;
@@ -2338,6 +2379,37 @@ int wq_sharded_route_owner_device(wq_router* h, const double* d_pos, const int64
     return WQ_OK;
 }
 
+// Folds in earlier asynchronous ticks (all of them when the budgets' form changes: the ring then
+// holds only one form's ticks), then one tick, redone exactly when a budget was short.
+static int owner_slots_call(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
+                            const uint32_t* d_sender, const uint8_t* d_repl, size_t n_msgs, wq_owner_slot_view* out,
+                            bool async, wq_route_counters* d_result) {
+    ShardCtx& sc = *h->shard;
+    if (sc.budget_form != 1) {  // budgets of the slot tick leave out the self segment: run exact
+        if (int rc = async_drain(h, 0)) return rc;
+        sc.budgets = false;
+        sc.budget_form = 1;
+    } else if (int rc = async_drain(h, async && sc.budgets ? 1u : 0u)) {
+        return rc;
+    }
+    const int inject = h->shard_inject;
+    h->shard_inject = 0;
+    bool redo = false;
+    int rc = owner_slot_tick(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, !sc.budgets, inject, &redo, out,
+                             async, d_result);
+    if (rc == WQ_OK && redo)
+        rc = owner_slot_tick(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, true, 0, &redo, out);
+    // an asynchronous call that ran synchronously (exact, or redone) leaves its result in the
+    // caller's counters all the same
+    if (async && d_result && rc == WQ_OK && out->n_pairs != ~0ull) {
+        wq_route_counters c{};
+        c.n_pairs = out->n_pairs;
+        WQ_HIP(h, hipMemcpyAsync(d_result, &c, sizeof(c), hipMemcpyHostToDevice, h->stream));
+        WQ_HIP(h, hipStreamSynchronize(h->stream));  // c lives on this stack frame
+    }
+    return rc;
+}
+
 int wq_sharded_route_owner_slots(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
                                  const uint32_t* d_sender, const uint8_t* d_repl, size_t n_msgs,
                                  wq_owner_slot_view* out) {
@@ -2346,19 +2418,18 @@ int wq_sharded_route_owner_slots(wq_router* h, const double* d_pos, const int64_
     WQ_HIP(h, hipSetDevice(h->device));
     if (!h->shard) return set_error(h, WQ_E_INVALID, "no exchange attached (wq_shard_attach_*)");
     memset(out, 0, sizeof(*out));
-    ShardCtx& sc = *h->shard;
-    if (int rc = async_drain(h, 0)) return rc;  // the slot tick's asynchronous ticks, folded first
-    if (sc.budget_form != 1) {  // budgets of the slot tick leave out the self segment: run exact
-        sc.budgets = false;
-        sc.budget_form = 1;
-    }
-    const int inject = h->shard_inject;
-    h->shard_inject = 0;
-    bool redo = false;
-    int rc = owner_slot_tick(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, !sc.budgets, inject, &redo, out);
-    if (rc == WQ_OK && redo)
-        rc = owner_slot_tick(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, true, 0, &redo, out);
-    return rc;
+    return owner_slots_call(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, out, false, nullptr);
+}
+
+int wq_sharded_route_owner_slots_async(wq_router* h, const double* d_pos, const int64_t* d_keys,
+                                       const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
+                                       size_t n_msgs, wq_route_counters* d_counters, wq_owner_slot_view* out) {
+    if (!h || !out || (n_msgs && (!d_world || !d_sender || !d_repl || (!d_pos && !d_keys)))) return WQ_E_INVALID;
+    if (n_msgs >= 0xFFFFFC00ull) return set_error(h, WQ_E_INVALID, "n_msgs must be < 2^32 - 1024 per tick");
+    WQ_HIP(h, hipSetDevice(h->device));
+    if (!h->shard) return set_error(h, WQ_E_INVALID, "no exchange attached (wq_shard_attach_*)");
+    memset(out, 0, sizeof(*out));
+    return owner_slots_call(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, out, true, d_counters);
 }
 
 int wq_sharded_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity) {

@@ -109,6 +109,8 @@ def load_library(build_if_missing: bool = True):
         "wq_sharded_copy_out": ([vp, vp, vp, vp, sz], i32),
         "wq_sharded_route_owner_device": ([vp, vp, vp, vp, vp, vp, sz, ctypes.POINTER(abi.OwnerView)], i32),
         "wq_sharded_route_owner_slots": ([vp, vp, vp, vp, vp, vp, sz, ctypes.POINTER(abi.OwnerSlotView)], i32),
+        "wq_sharded_route_owner_slots_async": ([vp, vp, vp, vp, vp, vp, sz, vp, ctypes.POINTER(abi.OwnerSlotView)],
+                                               i32),
         "wq_shard_last_bytes": ([vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], i32),
         "wq_debug_set_shard_form": ([vp, i32], i32),
         "wq_debug_inject_shard_failure": ([vp, i32], i32),
@@ -433,6 +435,16 @@ class Router:
         self._check(self.lib.wq_sharded_route_owner_slots(self.h, pos_ptr or None, keys_ptr or None, world_ptr or None,
                                                           sender_ptr or None, repl_ptr or None, n_msgs,
                                                           ctypes.byref(v)))
+        return v
+
+    def sharded_route_owner_slots_async(self, pos_ptr, world_ptr, sender_ptr, repl_ptr, n_msgs, counters_ptr=None,
+                                        keys_ptr=None):
+        """wq_sharded_route_owner_slots_async: the owner-slot tick without its end-of-tick read; P and the
+        status bits land in counters_ptr (view.n_pairs is 2^64-1 when the tick ran asynchronously)."""
+        v = abi.OwnerSlotView()
+        self._check(self.lib.wq_sharded_route_owner_slots_async(self.h, pos_ptr or None, keys_ptr or None,
+                                                                world_ptr or None, sender_ptr or None, repl_ptr or None,
+                                                                n_msgs, counters_ptr or None, ctypes.byref(v)))
         return v
 
     def sharded_copy_out(self, offsets_ptr, peers_ptr, msgs_ptr, capacity) -> None:
