@@ -166,6 +166,10 @@ struct wq_router {
     wq::RouteWs rws;
     // sharded ticks (wq_shard.hip): owner histograms, unpacked received records
     wq::DevBuf shard_hist, rec_keys, rec_w, rec_s, rec_r;
+    // the one-pass slot grouping (wq_shard.hip slot_group_kernel): tagged look-back granules per
+    // (owner, block), zeroed once per allocation (tag 0 never matches), and the launches so far
+    wq::DevBuf shard_look;
+    uint64_t shard_look_zeroed = 0, shard_look_calls = 0;
     int route_cfg = 0;  // route kernel shapes (wq_route.hip kCfgs)
     uint32_t route_chunks = 0;  // wq_debug_set_route_chunks: chunks of the pipelined heavy tick (0 = default)
     bool heavy_fanout = false;  // wq_set_fanout_hint: default shape -> kCfgHeavy

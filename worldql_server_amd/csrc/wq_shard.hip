@@ -12,6 +12,7 @@
 // Subscription ops go to the owner of their cube (op_owner_kernel); REMOVE_PEER goes to all.
 // The per-message body that runs on the owner is still local_message.rs:52-86.
 #include "route_common.hpp"
+#include "route_tick.hpp"  // granule / poll_granule: the tagged look-back words
 
 namespace wq {
 
@@ -526,6 +527,177 @@ __global__ void __launch_bounds__(kBlock)
     }
 }
 
+// (b1 + b2 + b3 in one pass: a budgeted tick) block b quantises its kShardTile messages and ranks
+// them per owner as slot_scatter_kernel does, publishes its per-owner counts as tagged granules
+// (look[d * nblk + b]) and finds each owner's running base over the lower blocks by decoupled
+// look-back (route_tick.hpp; wave 0, one group of 64 / G' lanes per owner, each lane one lower
+// block per round), then scatters into the budgeted segments. A block waits only on lower-numbered
+// blocks, dispatched before it, and every poll is bounded: one that gives up reports
+// WQ_E_TIMEOUT in every status word instead of hanging. The last block writes the A vector (every
+// owner's true count, its budget bit; with a_or the bit of any segment in all of them);
+// slot_pad_kernel pads the segments after it. Against the three passes it saves the histogram
+// pass's second quantisation of every message and the scan's launch.
+struct GroupArgs {
+    uint64_t* look;  // [G * nblk] granules
+    uint32_t tag;    // this launch's tag, 1 .. 2^30 - 1
+    uint32_t* a;     // the A vector: {count, status} per owner
+};
+
+template <bool RAW>
+__global__ void __launch_bounds__(kBlock)
+    slot_group_kernel(ShardIn in, SlotLayout L, uint32_t* __restrict__ out, uint32_t* __restrict__ perm, GroupArgs g) {
+    __shared__ uint32_t wc[kShardIPT * kWaves][WQ_MAX_SHARDS];
+    __shared__ uint32_t bcnt[WQ_MAX_SHARDS], base[WQ_MAX_SHARDS];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t b = blockIdx.x, NB = in.nblk, G = in.G;
+    for (uint32_t k = threadIdx.x; k < kShardIPT * kWaves * WQ_MAX_SHARDS; k += kBlock) (&wc[0][0])[k] = 0;
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1;
+    const uint32_t m0 = b * kShardTile + threadIdx.x;
+    int64_t kx[kShardIPT], ky[kShardIPT], kz[kShardIPT];
+    uint64_t pk[kShardIPT];
+    uint32_t ext[kShardIPT], own[kShardIPT], rank[kShardIPT];
+    bool reg[kShardIPT], go[kShardIPT];
+    uint32_t wrd[kShardIPT], snd[kShardIPT], rpl[kShardIPT];
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint32_t m = m0 + i * kBlock;
+        go[i] = m < in.M;
+        own[i] = 0xFFFFFFFFu;
+        rank[i] = 0;
+        reg[i] = true;
+        wrd[i] = snd[i] = rpl[i] = 0;
+        if (go[i]) {
+            msg_key<RAW>(in, m, kx[i], ky[i], kz[i]);
+            wrd[i] = in.world[m];
+            snd[i] = in.sender[m];
+            rpl[i] = in.repl[m];
+            own[i] = shard_of(wrd[i], kx[i], ky[i], kz[i], G);
+            reg[i] = pack_key(wrd[i], kx[i], ky[i], kz[i], in.sf, &pk[i], &ext[i]);
+            go[i] = own[i] != in.me || in.own_too;
+            if (in.zero_e) in.zero_e[m] = 0u;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint64_t wide = __ballot(go[i] && !reg[i]);
+        uint64_t todo = __ballot(go[i]);
+        while (todo) {
+            const int leader = __ffsll((unsigned long long)todo) - 1;
+            const uint32_t d = __shfl(own[i], leader, 64);
+            const uint64_t mask = __ballot(go[i] && own[i] == d);
+            if (go[i] && own[i] == d) rank[i] = __popcll(mask & lt) + __popcll(mask & wide & lt);
+            if (lane == leader) wc[i * kWaves + wave][d] = __popcll(mask) + __popcll(mask & wide);
+            todo &= ~mask;
+        }
+    }
+    __syncthreads();
+    // the block's per-owner totals (published at once) and its rows' offsets within the block
+    for (uint32_t d = threadIdx.x; d < G; d += kBlock) {
+        uint32_t run = 0;
+#pragma unroll
+        for (int k = 0; k < kShardIPT * kWaves; ++k) {
+            const uint32_t t = wc[k][d];
+            wc[k][d] = run;
+            run += t;
+        }
+        bcnt[d] = run;
+        __hip_atomic_store(g.look + (uint64_t)d * NB + b, granule(g.tag, b == 0 ? kFlagP : kFlagA, run),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (wave == 0) {
+        // lanes [d * W, d * W + W) look back for owner d, lane k of the group at block b - 1 - (r W + k)
+        uint32_t Gp = 1;
+        while (Gp < G) Gp <<= 1;
+        const uint32_t W = 64u / Gp, d = (uint32_t)lane / W, k = (uint32_t)lane % W;
+        const uint64_t gmask = (W == 64 ? ~0ull : ((1ull << W) - 1ull)) << (d * W);
+        uint64_t acc = 0;
+        bool gave_up = false, done = d >= G || b == 0;
+        for (int64_t hi = (int64_t)b - 1; __ballot(!done); hi -= W) {
+            const int64_t idx = hi - (int64_t)k;
+            uint64_t v = 0;
+            if (!done && idx >= 0) v = poll_granule(g.look + (uint64_t)d * NB + idx, g.tag, &gave_up);
+            const bool isP = !done && idx >= 0 && ((uint32_t)(v >> 32) & 3u) == kFlagP;
+            const uint64_t pm = __ballot(isP) & gmask;
+            const uint32_t first = pm ? (uint32_t)__builtin_ctzll(pm) - d * W : W;  // nearest inclusive prefix
+            uint64_t x = (!done && idx >= 0 && k <= first) ? (uint32_t)v : 0u;
+            for (uint32_t o = W >> 1; o >= 1; o >>= 1) x += __shfl_xor(x, (int)o, 64);  // the group's sum
+            if (!done) acc += x;
+            // the group is done at an inclusive prefix or past block 0
+            if (pm || hi - (int64_t)W < 0) done = true;
+        }
+        if (d < G && k == 0) {
+            base[d] = (uint32_t)acc;
+            if (b > 0)
+                __hip_atomic_store(g.look + (uint64_t)d * NB + b, granule(g.tag, kFlagP, (uint32_t)acc + bcnt[d]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (__any(gave_up) && lane == 0)  // WQ_E_TIMEOUT (status code 7) in every status word
+            for (uint32_t q = 0; q < G; ++q) atomicOr(&g.a[2 * q + 1], 7u);
+    }
+    __syncthreads();
+    if (b == NB - 1) {  // the last block knows every owner's true count
+        for (uint32_t d = threadIdx.x; d < G; d += kBlock) {
+            const uint32_t n = base[d] + bcnt[d];
+            g.a[2 * d] = n;
+            // the own column (own slots on): no budget, its buffer holds every message's slots
+            if (d != in.me && n > L.budget[d]) atomicOr(&g.a[2 * d + 1], kStBudget);
+        }
+        if (in.a_or) {
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                uint32_t any = 0;
+                for (uint32_t d = 0; d < G; ++d) any |= in.a_or[2 * d + 1] & kStBudget;
+                if (any)
+                    for (uint32_t d = 0; d < G; ++d) atomicOr(&in.a_or[2 * d + 1], any);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint32_t m = m0 + i * kBlock;
+        if (!go[i]) continue;
+        const uint32_t d = own[i];
+        const uint32_t j = base[d] + wc[i * kWaves + wave][d] + rank[i];  // within the owner's segment
+        uint32_t slot;
+        uint32_t* pm;
+        uint32_t* o;
+        if (d == in.me) {  // own slots on: this shard's own message, into its own (unbudgeted) buffer
+            slot = j;
+            pm = in.own_perm;
+            o = in.own_slots + (uint64_t)kSlotWords * slot;
+        } else {
+            if (j + (reg[i] ? 1u : 2u) > L.budget[d]) continue;  // over budget: the tick is redone exactly
+            slot = L.base[d] + j;
+            pm = perm;
+            o = out + (uint64_t)kSlotWords * slot;
+        }
+        const uint32_t rp = rpl[i];
+        if (reg[i]) {
+            o[0] = (uint32_t)pk[i];
+            o[1] = (uint32_t)(pk[i] >> 32);
+            o[2] = ext[i];
+            o[3] = snd[i];
+            o[4] = rp | (kSlotReg << 8);
+            pm[slot] = m;
+        } else {
+            o[0] = (uint32_t)(uint64_t)kx[i];
+            o[1] = (uint32_t)((uint64_t)kx[i] >> 32);
+            o[2] = wrd[i];
+            o[3] = snd[i];
+            o[4] = rp | (kSlotHead << 8);
+            o[5] = (uint32_t)(uint64_t)ky[i];
+            o[6] = (uint32_t)((uint64_t)ky[i] >> 32);
+            o[7] = (uint32_t)(uint64_t)kz[i];
+            o[8] = (uint32_t)((uint64_t)kz[i] >> 32);
+            o[9] = kSlotTail << 8;
+            pm[slot] = m;
+            pm[slot + 1] = kNone;
+        }
+    }
+}
+
 // (b4) the unused rest of every segment becomes tail slots (route to nobody; perm kNone), so the
 // owner can count its whole receive budget without knowing the true counts. Over budget, the last
 // slot of the segment is overwritten as well (a head whose tail did not fit); that tick is redone.
@@ -702,6 +874,31 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
     in.own_perm = own_perm;
     in.zero_e = zero_e;
     in.a_or = row_any && (phases & 3) == 3 ? d_a : nullptr;
+    // a budgeted tick (count, scan and scatter in one call): the one-pass grouping, then the padding
+    // (WQ_DEBUG_SLOT_3PASS: the three passes, diagnostics)
+    static const bool three_pass = getenv("WQ_DEBUG_SLOT_3PASS") != nullptr;
+    if (M && (phases & 3) == 3 && d_slots && !hist_ready && !three_pass) {
+        const uint64_t ng = (uint64_t)G * in.nblk;
+        WQ_ALLOC(h, h->shard_look, ng * 8);
+        if (h->shard_look_zeroed < ng) {  // fresh granules: tag 0 never matches a launch's tag
+            WQ_HIP(h, hipMemsetAsync(h->shard_look.p, 0, h->shard_look.bytes, s));
+            h->shard_look_zeroed = h->shard_look.bytes / 8;
+        }
+        GroupArgs ga{h->shard_look.as<uint64_t>(), (uint32_t)(h->shard_look_calls++ % ((1ull << 30) - 1)) + 1u, d_a};
+        if (d_keys)
+            hipLaunchKernelGGL((slot_group_kernel<true>), dim3(in.nblk), dim3(kBlock), 0, s, in, L, d_slots, d_perm, ga);
+        else
+            hipLaunchKernelGGL((slot_group_kernel<false>), dim3(in.nblk), dim3(kBlock), 0, s, in, L, d_slots, d_perm, ga);
+        WQ_HIP(h, hipGetLastError());
+        uint32_t bmax = 0;
+        for (uint32_t d = 0; d < G; ++d) bmax = std::max(bmax, L.budget[d]);
+        if (bmax) {
+            const unsigned gx = std::min<unsigned>(64u, (bmax + kBlock - 1) / kBlock);
+            hipLaunchKernelGGL(slot_pad_kernel, dim3(gx, G), dim3(kBlock), 0, s, L, G, d_a, d_slots, d_perm);
+            WQ_HIP(h, hipGetLastError());
+        }
+        return WQ_OK;
+    }
     if (M && (phases & 1)) {
         WQ_ALLOC(h, h->shard_hist, (uint64_t)in.nblk * G * 4);
         uint32_t* hist = h->shard_hist.as<uint32_t>();

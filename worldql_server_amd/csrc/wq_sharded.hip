@@ -1366,8 +1366,7 @@ struct AsyncResultParams {
     uint64_t capacity;
     wq_route_counters* out;  // the caller's (nullable)
     uint32_t* health;        // the handle's sticky words
-    const uint32_t* small;   // the tick's small vectors (words) ...
-    uint32_t small_words;
+    const uint32_t* small;   // the tick's small vectors (words; the ones in use: small_word) ...
     uint32_t* snap;          // ... copied here (mapped pinned memory), then the sequence word
     uint64_t seq;
     uint32_t* zero;          // the small vectors, zeroed last for the next tick
@@ -1377,8 +1376,19 @@ struct AsyncResultParams {
 // counters and the sticky health words: P, a shard's failed step (32), the device bits of every
 // shard's statuses and counters, a budget that was too small (64: the outputs are not valid; every
 // shard sees it and the next call runs exact).
+// The words of the small vectors a tick uses: A and C (4G words each) and the counter blocks.
+__device__ __forceinline__ uint32_t small_word(uint32_t k, uint32_t G) {
+    const uint32_t ac = 4 * G;
+    return k < ac ? kSmallA / 4 + k : k < 2 * ac ? kSmallC / 4 + (k - ac) : kSmallCnt / 4 + (k - 2 * ac);
+}
+
 __global__ __launch_bounds__(256) void k_async_result(AsyncResultParams p) {
-    for (uint32_t i = threadIdx.x; i < p.small_words; i += blockDim.x) p.snap[i] = p.small[i];
+    // only the words in use cross PCIe (the vectors' 8 KB would be ~20 times as many)
+    const uint32_t nw = 8 * p.G + (uint32_t)(4 * sizeof(wq_route_counters) / 4);
+    for (uint32_t k = threadIdx.x; k < nw; k += blockDim.x) {
+        const uint32_t i = small_word(k, p.G);
+        p.snap[i] = p.small[i];
+    }
     __threadfence_system();  // every thread's part of the snapshot visible to the host ...
     __syncthreads();
     if (threadIdx.x == 0) {  // ... before the sequence word
@@ -1406,7 +1416,7 @@ __global__ __launch_bounds__(256) void k_async_result(AsyncResultParams p) {
     }
     __syncthreads();
     // the small vectors zeroed for the next tick (here, rather than a memset launch at its start)
-    for (uint32_t i = threadIdx.x; i < p.small_words; i += blockDim.x) p.zero[i] = 0u;
+    for (uint32_t k = threadIdx.x; k < nw; k += blockDim.x) p.zero[small_word(k, p.G)] = 0u;
 }
 
 
@@ -1863,7 +1873,6 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
         ar.out = d_result;
         ar.health = route_health(h);
         ar.small = reinterpret_cast<const uint32_t*>(small);
-        ar.small_words = (uint32_t)(small_used / 4);
         ar.snap = static_cast<uint32_t*>(sc.asnap[k]);
         ar.seq = sc.aseq[k];
         ar.zero = reinterpret_cast<uint32_t*>(small);
@@ -2119,7 +2128,6 @@ static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_k
         ar.out = d_result;
         ar.health = route_health(h);
         ar.small = reinterpret_cast<const uint32_t*>(small);
-        ar.small_words = (uint32_t)(small_used / 4);
         ar.snap = static_cast<uint32_t*>(sc.asnap[k]);
         ar.seq = sc.aseq[k];
         ar.zero = reinterpret_cast<uint32_t*>(small);
