@@ -306,7 +306,8 @@ def _check_owner_slots(views, want):
 @pytest.mark.parametrize("G", [1, 2, 3, 8])
 def test_hub_owner_slots_vs_whole_table_oracle(G):
     """wq_sharded_route_owner_slots, the owner form on budgeted slots: an exact first tick, a budgeted
-    one after churn, one with four times the messages (budgets short: every shard redoes it exactly), a budgeted one again, a slot tick in between (its budgets leave out the self segment,
+    one after churn, one with four times the messages (budgets short: every shard redoes it
+    exactly), a budgeted one again, a slot tick in between (its budgets leave out the self segment,
     so the next owner tick runs exact) — every message routed once, against the whole-table oracle."""
     import torch
     from worldql_server_amd.router import Hub, Router
