@@ -594,6 +594,14 @@ def _proc(rank, G, port, mode, out):
         rc, offs, peers, msgs = _tick(r, w, lo, hi, dev)
         want = _expected([w.ops, churn], w, lo, hi)
         ok = bool((offs == want[0]).all() and (peers == want[1]).all())
+        if mode == "callback":  # the owner form too (its self segment goes through the callback)
+            sl = (w.pos[lo:hi], w.world[lo:hi], w.sender[lo:hi], w.repl[lo:hi])
+            _owner_slot_tick(r, *sl, dev)       # exact
+            v = _owner_slot_tick(r, *sl, dev)   # on budgets
+            views = [None] * G
+            dist.all_gather_object(views, v)
+            if rank == 0:
+                _check_owner_slots(views, [_expected([w.ops, churn], w, *_slice(M, G, q)) for q in range(G)])
         out[rank] = ("ok" if ok else "mismatch", int(len(peers)))
         r.close()
     except Exception as e:  # noqa: BLE001
@@ -613,9 +621,9 @@ def _run_procs(G, mode):
 
 @pytest.mark.parametrize("G", [2, 3])
 def test_callback_exchange_gloo_processes(G):
-    """The native slot tick across G processes (one per shard, all on cuda:0) whose exchange is the
-    caller's own gloo all-to-all (wq_shard_attach_exchange) — the multi-process form of the product
-    path, as one process per GPU runs it."""
+    """The native slot tick, then the owner-slot tick, across G processes (one per shard, all on
+    cuda:0) whose exchange is the caller's own gloo all-to-all (wq_shard_attach_exchange) — the
+    multi-process form of the product path, as one process per GPU runs it."""
     res = _run_procs(G, "callback")
     assert [res[k][0] for k in range(G)] == ["ok"] * G, res
     assert sum(res[k][1] for k in range(G)) > 0
