@@ -490,6 +490,11 @@ def _run_c3_multi(a, w, rank, world_size, local_rank, dev, gen_s):
                 e = {"value": x["pairs_all"] * a.steps / (x["t_max_ms"] / 1e3), "unit": "pairs/s",
                      "ms_per_step": x["t_max_ms"] / a.steps, "n_gpus": world_size, "scaling": "strong"}
                 e.update({k: v for k, v in x.items() if k not in ("t_max_ms", "pairs_all", "B_all")})
+                if "pairs_on_owner" in e and "replicate" in res:
+                    # the same tick's §8(d) bytes per GPU over the owner form's time (link time included)
+                    po = e["pairs_on_owner"]
+                    po["roofline_frac_per_gpu"] = (res["replicate"]["B_all"] / world_size /
+                                                   (po["ms_per_step"] / 1e3) / 1e9 / HBM_PEAK_GBS)
                 extra["cube_hash" if f == "cube" else "replicated_table"] = e
             else:
                 extra["cube_hash" if f == "cube" else "replicated_table"] = {"error": "did not finish in time"}
