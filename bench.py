@@ -21,7 +21,9 @@ each subscribed to a 3x3x3 neighbourhood (27M subscriptions), 10M LocalMessages 
           table (every GPU holds the whole ~10 GB table and routes its slice with the single-GPU
           tick, no exchange; DESIGN.md §6 says why); beside it, extra.cube_hash: the cube-hash
           sharded tick over RCCL (20-byte slots to the owners, row references + cube-list pools
-          back; wq_sharded_route_tick_device). --shard cube makes that form the headline.
+          back; wq_sharded_route_tick_device), and under it pairs_on_owner: the owner form
+          (wq_sharded_route_owner_slots_async: slots to the owners, the pairs left there). --shard
+          cube or --shard owner makes that form the headline (extra: the replicated table).
 The table is built once before timing. Every timed loop is checked afterwards through the
 routers' sticky health words (wq_route_health): no tick may have given up or overflowed.
 Other configs: --config c1 | c2 | c4 | c5 (bench_configs.py); --config c2 --shard cube = one world
@@ -61,9 +63,10 @@ def parse():
     ap.add_argument("--scale", type=float, default=1.0, help="shrink C2 (tests only; 1.0 = the headline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline's routing work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--shard", choices=["world", "cube", "replicate"], default="world",
-                    help="multi-GPU partitioning (see module docstring); C3: replicate (the default at N > 1) "
-                         "or cube as the headline form")
+    ap.add_argument("--shard", choices=["world", "cube", "replicate", "owner"], default="world",
+                    help="multi-GPU partitioning (see module docstring); C3: replicate (the default at N > 1), "
+                         "cube (pairs returned to the ingesting GPU) or owner (pairs left on the owning GPU) as "
+                         "the headline form")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "r02_pmc_route.json"),
                     help="rocprofv3 --pmc summary of the C2 tick (roofline.traffic)")
     a = ap.parse_args()

@@ -177,7 +177,7 @@ def run_c3(a, rank, world_size, local_rank, dev):
     t0 = time.perf_counter()
     w = synth_ext.config_c3(scale=a.scale)
     gen_s = time.perf_counter() - t0
-    if world_size > 1 or a.shard in ("cube", "replicate"):
+    if world_size > 1 or a.shard in ("cube", "replicate", "owner"):
         # N > 1: both multi-GPU forms, the replicated table as the headline unless
         # --shard cube; --shard cube / replicate at N = 1: that form alone on one rank
         return _run_c3_multi(a, w, rank, world_size, local_rank, dev, gen_s)
@@ -440,6 +440,49 @@ def _c3_cube(a, w, rank, world_size, local_rank, dev, stream, sl, owner_form: bo
     return out
 
 
+def _c3_owner(a, w, rank, world_size, local_rank, dev, stream, sl):
+    """The cube-hash owner form (wq_sharded_route_owner_slots_async over RCCL, SURVEY.md §8(e) step 5's
+    first option): every rank holds the buckets it owns and ingests M/N messages; a tick sends every
+    message to its owner as a 20-byte slot (budgeted sizes, one exchange, no end-of-tick read) and the
+    owner routes it there, leaving the pairs on that GPU (a CSR over its received slots)."""
+    import torch
+    from worldql_server_amd.router import Router
+    lo, hi, (pos, world, sender, repl) = sl
+    M = hi - lo
+    r = Router(w.cube_size, local_rank)
+    r.set_stream(stream.cuda_stream)
+    attach_rccl(r, rank, world_size)
+    t0 = time.perf_counter()
+    r.sharded_apply_ops(w.ops)
+    build_s = time.perf_counter() - t0
+    st = r.stats()
+    r.set_fanout_hint(40.0)
+    cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+
+    def tick():
+        r.sharded_route_owner_slots_async(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M,
+                                          cnt.data_ptr())
+    for _ in range(max(a.warmup, 3)):
+        tick()
+    e0, b0 = r.shard_tick_stats()
+    t_ms = timed_ticks(tick, a.steps, stream, dev, world_size, [r])
+    e1, b1 = r.shard_tick_stats()
+    c = _counters(cnt)[0]
+    assert c["error"] == 0 and c["overflow"] == 0, c
+    P, F = int(c["n_pairs"]), int(c["n_candidates"])
+    sent, _ = r.shard_last_bytes()
+    r.close()
+    (t_max_ms,) = bench.allreduce([t_ms], "max", dev, world_size)
+    # §8(d) bytes of the routing this GPU did: its ingested messages' 69 B, the candidates it read, and
+    # its pairs written once (a CSR over its received slots: no per-pair message index)
+    pairs_all, B_all = bench.allreduce([P, 69 * M + 4 * F + 4 * P + 4], "sum", dev, world_size)
+    (sent_max,) = bench.allreduce([float(sent)], "max", dev, world_size)
+    return {"t_max_ms": t_max_ms, "pairs_all": int(pairs_all), "B_all": int(B_all), "build_s": build_s,
+            "subscriptions_this_shard": int(st["n_entries"]), "xgmi_bytes_per_gpu": int(sent_max),
+            "exact_ticks_timed": e1 - e0, "budgeted_ticks_timed": b1 - b0}
+
+
 def _run_c3_multi(a, w, rank, world_size, local_rank, dev, gen_s):
     """C3 over N GPUs, strong scaling (the 10M messages of a tick split over the ranks), both
     multi-GPU forms measured in the same run on the same slices:
@@ -451,36 +494,42 @@ def _run_c3_multi(a, w, rank, world_size, local_rank, dev, gen_s):
     Each timed region: barrier + synchronize, K ticks, synchronize + barrier, max over ranks."""
     import threading
     import torch
-    head = "cube" if a.shard == "cube" else "replicate"
+    head = a.shard if a.shard in ("cube", "owner") else "replicate"
     stream = torch.cuda.Stream(device=dev)
     sl = _c3_slice(w, rank, world_size, dev)
     M_all = len(w.world)
     M = sl[1] - sl[0]
     res = {}
     forms = [head] if (world_size == 1 or a.no_extra) else [head, "cube" if head == "replicate" else "replicate"]
+    name = {"cube": "cube_hash", "replicate": "replicated_table", "owner": "owner_slots"}
 
     def line():
         h = res[head]
         t = h["t_max_ms"]
-        B = res["replicate"]["B_all"] if "replicate" in res else algorithmic_bytes(M_all, h["pairs_all"], h["pairs_all"])
-        par = (f"replicated table x{world_size} (every GPU holds all {len(w.ops)} subscriptions and routes its "
-               f"{M} of the {M_all} messages; no exchange)" if head == "replicate" else
-               f"cube-hash x{world_size} (wq_sharded_route_tick_device over RCCL: 20-byte slots out, row "
-               "references + per-destination cube-list pools back, budgeted exchanges)")
+        B = (h["B_all"] if head == "owner" else res["replicate"]["B_all"] if "replicate" in res else
+             algorithmic_bytes(M_all, h["pairs_all"], h["pairs_all"]))
+        par = {"replicate": f"replicated table x{world_size} (every GPU holds all {len(w.ops)} subscriptions and routes "
+                            f"its {M} of the {M_all} messages; no exchange)",
+               "cube": f"cube-hash x{world_size} (wq_sharded_route_tick_device over RCCL: 20-byte slots out, row "
+                       "references + per-destination cube-list pools back, budgeted exchanges)",
+               "owner": f"cube-hash owner form x{world_size} (wq_sharded_route_owner_slots_async over RCCL: every "
+                        "message to its owner as a 20-byte slot, one budgeted exchange, the pairs left on the "
+                        "owning GPU)"}[head]
         cfg = {"messages_per_tick": M_all, "messages_per_gpu": M, "peers": w.n_peers,
                "pairs_per_tick": h["pairs_all"], "parallelism": par, "table_build_s": round(h["build_s"], 3),
                "generate_s": round(gen_s, 1)}
-        if head == "cube":
-            cfg.update({k: h[k] for k in ("subscriptions_this_shard", "xgmi_bytes_per_gpu", "exact_ticks",
-                                          "budgeted_ticks")})
+        if head in ("cube", "owner"):
+            cfg.update({k: h[k] for k in h if k.startswith(("subscriptions", "xgmi", "exact", "budgeted"))})
         out = _line(a, world_size, h["pairs_all"] * a.steps / (t / 1e3), t / a.steps, "strong",
                     f"C3 over {world_size} GPU(s): 1M peers x 3x3x3, 10M LocalMessages/tick in total, "
                     "256 Zipf(1) Gaussian hotspots + 10% uniform, cube_size 16, ExceptSelf"
                     + ("" if a.scale == 1.0 else f" (scaled {a.scale})"), cfg,
                     roofline(B // world_size, t / a.steps / 1e3,
                              "whole tick per GPU; bytes = the tick's SURVEY §8(d) bytes / N" +
-                             (" (count / tile_scan / emit on each GPU's slice)" if head == "replicate" else
-                              " (own-cube count + slots + exchanges + owner count + pools + emit)")),
+                             {"replicate": " (count / tile_scan / emit on each GPU's slice)",
+                              "cube": " (own-cube count + slots + exchanges + owner count + pools + emit)",
+                              "owner": " (pairs written once, no per-pair message index: grouping + exchange + "
+                                       "owner count / tile_scan / emit)"}[head]),
                     "synthetic (splitmix64, SURVEY.md §8(d) C3 generator)")
         out["xgmi_model"] = _xgmi_model()
         extra = {}
@@ -495,9 +544,9 @@ def _run_c3_multi(a, w, rank, world_size, local_rank, dev, gen_s):
                     po = e["pairs_on_owner"]
                     po["roofline_frac_per_gpu"] = (res["replicate"]["B_all"] / world_size /
                                                    (po["ms_per_step"] / 1e3) / 1e9 / HBM_PEAK_GBS)
-                extra["cube_hash" if f == "cube" else "replicated_table"] = e
+                extra[name[f]] = e
             else:
-                extra["cube_hash" if f == "cube" else "replicated_table"] = {"error": "did not finish in time"}
+                extra[name[f]] = {"error": "did not finish in time"}
         if extra:
             out["extra"] = extra
         return out
@@ -518,6 +567,8 @@ def _run_c3_multi(a, w, rank, world_size, local_rank, dev, gen_s):
         try:
             if f == "replicate":
                 res[f] = _c3_replicated(a, w, rank, world_size, local_rank, dev, stream, sl)
+            elif f == "owner":
+                res[f] = _c3_owner(a, w, rank, world_size, local_rank, dev, stream, sl)
             else:
                 res[f] = _c3_cube(a, w, rank, world_size, local_rank, dev, stream, sl, owner_form=not a.no_extra)
         except Exception as e:  # noqa: BLE001
@@ -529,13 +580,14 @@ def _run_c3_multi(a, w, rank, world_size, local_rank, dev, gen_s):
             print(f"rank {rank}: {f} form failed: {e!r}", file=sys.stderr, flush=True)
             if rank == 0:
                 out = line()
-                out.setdefault("extra", {})["cube_hash" if f == "cube" else "replicated_table"] = {"error": repr(e)}
+                out.setdefault("extra", {})[name[f]] = {"error": repr(e)}
                 print(json.dumps(out), flush=True)
             os._exit(3)  # the headline line stands; the failed form makes the run's status non-zero
         if dog:
             dog.cancel()
-    if "replicate" in res and "cube" in res:
-        assert res["replicate"]["pairs_all"] == res["cube"]["pairs_all"]  # the same pairs either way
+    for f in ("cube", "owner"):
+        if "replicate" in res and f in res:
+            assert res["replicate"]["pairs_all"] == res[f]["pairs_all"]  # the same pairs either way
     return line()
 
 
