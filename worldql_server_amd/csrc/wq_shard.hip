@@ -40,6 +40,9 @@ struct ShardIn {
     uint32_t* own_slots = nullptr;
     uint32_t* own_perm = nullptr;
     bool own_too = false;
+    // own_slots with a budget: the owner form writes its self segment straight into its receive
+    // buffer (no self copy in the exchange), budgeted like every other segment
+    uint32_t own_budget = 0xFFFFFFFFu;
     uint32_t* zero_e = nullptr;  // slot_count_kernel: e[m] = 0 for every message (rows no step writes)
     // slot_scatter_kernel (the owner form's budgeted tick): the budget bit of ANY of this shard's
     // segments goes to every segment's status word, so each owner learns of every short budget
@@ -365,7 +368,7 @@ __global__ void __launch_bounds__(kBlock) slot_count_kernel(ShardIn in, uint32_t
 // block counts (in place); the owner's total and the budget bit to a[2d], a[2d + 1].
 __global__ void __launch_bounds__(kScanThreads1)
     slot_scan_kernel(uint32_t* __restrict__ v, uint32_t nblk, uint32_t G, SlotLayout L, uint32_t* __restrict__ a,
-                     uint32_t me, uint32_t* __restrict__ out, uint32_t* __restrict__ perm) {
+                     uint32_t me, uint32_t* __restrict__ out, uint32_t* __restrict__ perm, uint32_t own_budget) {
     __shared__ uint32_t wsum[kScanThreads1 / 64];
     __shared__ uint32_t carry_s;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -393,8 +396,8 @@ __global__ void __launch_bounds__(kScanThreads1)
         }
         if (threadIdx.x == 0) {
             a[2 * d] = carry_s;
-            // the own column (own slots on): no budget, its buffer holds every message's slots
-            a[2 * d + 1] = d != me && carry_s > L.budget[d] ? kStBudget : 0u;
+            // the own column (own slots on): no budget unless own_budget says so
+            a[2 * d + 1] = carry_s > (d != me ? L.budget[d] : own_budget) ? kStBudget : 0u;
         }
         // out set (a budgeted tick): the rest of the segment padded here, as slot_pad_kernel does
         // after the scatter — the scatter writes slots [0, n) only, and past a budget it writes no
@@ -492,7 +495,8 @@ __global__ void __launch_bounds__(kBlock)
         uint32_t slot;
         uint32_t* pm;
         uint32_t* o;
-        if (d == in.me) {  // own slots on: this shard's own message, into its own (unbudgeted) buffer
+        if (d == in.me) {  // own slots on: this shard's own message, into its own buffer
+            if (j + (reg[i] ? 1u : 2u) > in.own_budget) continue;  // (the owner form's self segment)
             slot = j;
             pm = in.own_perm;
             o = in.own_slots + (uint64_t)kSlotWords * slot;
@@ -541,6 +545,10 @@ struct GroupArgs {
     uint64_t* look;  // [G * nblk] granules
     uint32_t tag;    // this launch's tag, 1 .. 2^30 - 1
     uint32_t* a;     // the A vector: {count, status} per owner
+    // the owner form's in-place self segment: its {count, status} straight into the received A
+    // vector as well (the exchange then skips the self copy), nullable
+    uint32_t* a_self = nullptr;
+    uint32_t self = 0;
 };
 
 template <bool RAW>
@@ -633,24 +641,30 @@ __global__ void __launch_bounds__(kBlock)
                 __hip_atomic_store(g.look + (uint64_t)d * NB + b, granule(g.tag, kFlagP, (uint32_t)acc + bcnt[d]),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (__any(gave_up) && lane == 0)  // WQ_E_TIMEOUT (status code 7) in every status word
+        if (__any(gave_up) && lane == 0) {  // WQ_E_TIMEOUT (status code 7) in every status word
             for (uint32_t q = 0; q < G; ++q) atomicOr(&g.a[2 * q + 1], 7u);
+            if (g.a_self) atomicOr(&g.a_self[1], 7u);
+        }
     }
     __syncthreads();
     if (b == NB - 1) {  // the last block knows every owner's true count
         for (uint32_t d = threadIdx.x; d < G; d += kBlock) {
             const uint32_t n = base[d] + bcnt[d];
             g.a[2 * d] = n;
-            // the own column (own slots on): no budget, its buffer holds every message's slots
-            if (d != in.me && n > L.budget[d]) atomicOr(&g.a[2 * d + 1], kStBudget);
+            // the own column (own slots on): no budget unless own_budget says so
+            if (n > (d != in.me ? L.budget[d] : in.own_budget)) atomicOr(&g.a[2 * d + 1], kStBudget);
         }
-        if (in.a_or) {
-            __syncthreads();
-            if (threadIdx.x == 0) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (in.a_or) {
                 uint32_t any = 0;
                 for (uint32_t d = 0; d < G; ++d) any |= in.a_or[2 * d + 1] & kStBudget;
                 if (any)
                     for (uint32_t d = 0; d < G; ++d) atomicOr(&in.a_or[2 * d + 1], any);
+            }
+            if (g.a_self) {
+                g.a_self[0] = g.a[2 * g.self];
+                atomicOr(&g.a_self[1], g.a[2 * g.self + 1]);
             }
         }
     }
@@ -663,7 +677,8 @@ __global__ void __launch_bounds__(kBlock)
         uint32_t slot;
         uint32_t* pm;
         uint32_t* o;
-        if (d == in.me) {  // own slots on: this shard's own message, into its own (unbudgeted) buffer
+        if (d == in.me) {  // own slots on: this shard's own message, into its own buffer
+            if (j + (reg[i] ? 1u : 2u) > in.own_budget) continue;  // (the owner form's self segment)
             slot = j;
             pm = in.own_perm;
             o = in.own_slots + (uint64_t)kSlotWords * slot;
@@ -703,15 +718,22 @@ __global__ void __launch_bounds__(kBlock)
 // slot of the segment is overwritten as well (a head whose tail did not fit); that tick is redone.
 __global__ void __launch_bounds__(kBlock)
     slot_pad_kernel(SlotLayout L, uint32_t G, const uint32_t* __restrict__ a, uint32_t* __restrict__ out,
-                    uint32_t* __restrict__ perm) {
+                    uint32_t* __restrict__ perm, uint32_t own_d, uint32_t* __restrict__ own_out,
+                    uint32_t* __restrict__ own_perm, uint32_t own_budget) {
     const uint32_t d = blockIdx.y;
     if (d >= G) return;
-    const uint32_t B = L.budget[d], n = a[2 * d];
+    // own_d: the owner form's self segment, written in place into the receive buffer
+    const bool ownd = d == own_d;
+    if (ownd) {
+        out = own_out;
+        perm = own_perm;
+    }
+    const uint32_t B = ownd ? own_budget : L.budget[d], n = a[2 * d];
     // n == B: every slot fit, nothing of the segment is overwritten; n > B: the last slot may be a
     // head whose tail did not fit, so it becomes a tail too (the tick is redone)
     const uint32_t from = n <= B ? n : (B ? B - 1 : 0);
     for (uint32_t j = from + blockIdx.x * kBlock + threadIdx.x; j < B; j += gridDim.x * kBlock) {
-        const uint32_t slot = L.base[d] + j;
+        const uint32_t slot = (ownd ? 0u : L.base[d]) + j;
         uint32_t* o = out + (uint64_t)kSlotWords * slot;
         o[0] = 0;
         o[1] = 0;
@@ -854,7 +876,7 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
                         const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, uint32_t me,
                         const SlotLayout& L, uint32_t* d_slots, uint32_t* d_perm, uint32_t* d_a, int phases,
                         bool hist_ready, bool own_too, uint32_t* own_slots, uint32_t* own_perm, uint32_t* zero_e,
-                        bool row_any) {
+                        bool row_any, uint32_t own_budget, uint32_t* a_self) {
     hipStream_t s = h->stream;
     ShardIn in;
     in.pos = d_pos;
@@ -873,7 +895,11 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
     in.own_slots = own_slots;
     in.own_perm = own_perm;
     in.zero_e = zero_e;
+    in.own_budget = own_budget;
     in.a_or = row_any && (phases & 3) == 3 ? d_a : nullptr;
+    // the owner form's self segment in place: slot_pad_kernel pads it (the scan pads only the others)
+    const bool own_in_place = own_slots && own_budget != 0xFFFFFFFFu;
+    const uint32_t own_d = own_in_place ? me : G;
     // a budgeted tick (count, scan and scatter in one call): the one-pass grouping, then the padding
     // (WQ_DEBUG_SLOT_3PASS: the three passes, diagnostics)
     static const bool three_pass = getenv("WQ_DEBUG_SLOT_3PASS") != nullptr;
@@ -884,17 +910,19 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
             WQ_HIP(h, hipMemsetAsync(h->shard_look.p, 0, h->shard_look.bytes, s));
             h->shard_look_zeroed = h->shard_look.bytes / 8;
         }
-        GroupArgs ga{h->shard_look.as<uint64_t>(), (uint32_t)(h->shard_look_calls++ % ((1ull << 30) - 1)) + 1u, d_a};
+        GroupArgs ga{h->shard_look.as<uint64_t>(), (uint32_t)(h->shard_look_calls++ % ((1ull << 30) - 1)) + 1u, d_a,
+                     a_self, me};
         if (d_keys)
             hipLaunchKernelGGL((slot_group_kernel<true>), dim3(in.nblk), dim3(kBlock), 0, s, in, L, d_slots, d_perm, ga);
         else
             hipLaunchKernelGGL((slot_group_kernel<false>), dim3(in.nblk), dim3(kBlock), 0, s, in, L, d_slots, d_perm, ga);
         WQ_HIP(h, hipGetLastError());
-        uint32_t bmax = 0;
+        uint32_t bmax = own_in_place ? own_budget : 0u;
         for (uint32_t d = 0; d < G; ++d) bmax = std::max(bmax, L.budget[d]);
         if (bmax) {
             const unsigned gx = std::min<unsigned>(64u, (bmax + kBlock - 1) / kBlock);
-            hipLaunchKernelGGL(slot_pad_kernel, dim3(gx, G), dim3(kBlock), 0, s, L, G, d_a, d_slots, d_perm);
+            hipLaunchKernelGGL(slot_pad_kernel, dim3(gx, G), dim3(kBlock), 0, s, L, G, d_a, d_slots, d_perm, own_d,
+                               own_slots, own_perm, own_budget);
             WQ_HIP(h, hipGetLastError());
         }
         return WQ_OK;
@@ -912,7 +940,7 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
         // a budgeted tick (count, scan and scatter in one call) pads its segments in the scan
         const bool pad_in_scan = (phases & 3) == 3 && d_slots;
         hipLaunchKernelGGL(slot_scan_kernel, dim3(G), dim3(kScanThreads1), 0, s, hist, in.nblk, G, L, d_a, me,
-                           pad_in_scan ? d_slots : nullptr, pad_in_scan ? d_perm : nullptr);
+                           pad_in_scan ? d_slots : nullptr, pad_in_scan ? d_perm : nullptr, own_budget);
         WQ_HIP(h, hipGetLastError());
     } else if (phases & 1) {
         WQ_HIP(h, hipMemsetAsync(d_a, 0, 8 * G, s));
@@ -930,9 +958,12 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
     }
     uint32_t bmax = 0;
     for (uint32_t d = 0; d < G; ++d) bmax = std::max(bmax, L.budget[d]);
-    if (bmax && !(M && (phases & 3) == 3)) {  // (phases 3 with messages: padded by the scan)
+    if (own_in_place) bmax = std::max(bmax, own_budget);
+    // (phases 3 with messages: padded by the scan, all but an in-place self segment)
+    if (bmax && (!(M && (phases & 3) == 3) || own_in_place)) {
         const unsigned gx = std::min<unsigned>(64u, (bmax + kBlock - 1) / kBlock);
-        hipLaunchKernelGGL(slot_pad_kernel, dim3(gx, G), dim3(kBlock), 0, s, L, G, d_a, d_slots, d_perm);
+        hipLaunchKernelGGL(slot_pad_kernel, dim3(gx, G), dim3(kBlock), 0, s, L, G, d_a, d_slots, d_perm, own_d,
+                           own_slots, own_perm, own_budget);
         WQ_HIP(h, hipGetLastError());
     }
     return WQ_OK;

@@ -52,7 +52,8 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
                         const uint32_t* d_sender, const uint8_t* d_repl, size_t M, uint32_t G, uint32_t me,
                         const SlotLayout& L, uint32_t* d_slots, uint32_t* d_perm, uint32_t* d_a, int phases,
                         bool hist_ready = false, bool own_too = false, uint32_t* own_slots = nullptr,
-                        uint32_t* own_perm = nullptr, uint32_t* zero_e = nullptr, bool row_any = false);
+                        uint32_t* own_perm = nullptr, uint32_t* zero_e = nullptr, bool row_any = false,
+                        uint32_t own_budget = 0xFFFFFFFFu, uint32_t* a_self = nullptr);
 uint32_t budget_slot_tile();
 int launch_route_records(wq_router* h, const wq_msg_rec* d_recs, size_t M, uint32_t* d_offsets, uint32_t* d_peers,
                          uint32_t* d_msgs, size_t capacity);
@@ -196,6 +197,8 @@ struct Xfer {
     void* recv[3];
     const size_t* rbytes[3];
     int n;
+    // buffer k's self segment is already in place in recv[k] (RCCL and hub exchanges only): not copied
+    bool skip_self[3] = {false, false, false};
 };
 
 struct ShardCtx {
@@ -269,6 +272,7 @@ int exchange(wq_router* h, const Xfer& x) {
     hipStream_t s = h->stream;
     if (sc.kind == kXCallback) {
         for (int k = 0; k < x.n; ++k) {
+            if (x.skip_self[k]) return set_error(h, WQ_E_INVALID, "exchange: the caller's callback copies every segment");
             const int rc = sc.fn(sc.fn_ctx, x.send[k], x.sbytes[k], x.recv[k], x.rbytes[k], (void*)s);
             if (rc) return set_error(h, WQ_E_RCCL, "the caller's exchange callback failed");
         }
@@ -279,7 +283,7 @@ int exchange(wq_router* h, const Xfer& x) {
         for (int k = 0; k < x.n; ++k) {  // the self segment: a device copy
             const auto so = prefix(x.sbytes[k], G), ro = prefix(x.rbytes[k], G);
             if (x.sbytes[k][me] != x.rbytes[k][me]) return set_error(h, WQ_E_INVALID, "self segment size mismatch");
-            if (x.sbytes[k][me])
+            if (x.sbytes[k][me] && !x.skip_self[k])
                 WQ_HIP(h, hipMemcpyAsync(static_cast<char*>(x.recv[k]) + ro[me],
                                          static_cast<const char*>(x.send[k]) + so[me], x.sbytes[k][me],
                                          hipMemcpyDeviceToDevice, s));
@@ -339,7 +343,7 @@ int exchange(wq_router* h, const Xfer& x) {
                     rc = set_error(h, WQ_E_INVALID, "hub exchange: send / receive sizes disagree");
                     break;
                 }
-                if (!bytes) continue;
+                if (!bytes || (src == me && x.skip_self[k])) continue;
                 size_t soff = 0, roff = 0;
                 for (uint32_t d = 0; d < me; ++d) soff += p.sbytes[k][d];
                 for (uint32_t q = 0; q < src; ++q) roff += x.rbytes[k][q];
@@ -2040,10 +2044,18 @@ static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_k
     if (alloc(sc.slots, (Sb + 2) * kSlotWords * 4) || alloc(sc.perm, (Sb + 2) * 4) ||
         alloc(sc.rslots, (Rb + 2) * kSlotWords * 4))
         return fatal_receive(h, "hipMalloc of the sharded tick's slots");
+    // the self segment straight into the receive buffer (not through the exchange's self copy), except
+    // with the caller's callback, which copies every segment itself
+    const bool in_place = sc.kind != kXCallback;
+    // ... and its A entry too, on a budgeted tick (the one-pass grouping's last block writes it)
+    const bool a_in_place = in_place && !exact && M && !late && !getenv("WQ_DEBUG_SLOT_3PASS");
+    uint32_t* a_self = a_in_place ? a_recv + 2 * me : nullptr;
     if (!late)
-        fail(launch_budget_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, G, L, sc.slots.as<uint32_t>(),
-                                 sc.perm.as<uint32_t>(), a_send, exact ? 2 : 3, false, true, nullptr, nullptr, nullptr,
-                                 !exact));
+        fail(launch_budget_slots(h, d_pos, d_keys, d_world, d_sender, d_repl, M, G, in_place ? me : G, L,
+                                 sc.slots.as<uint32_t>(), sc.perm.as<uint32_t>(), a_send, exact ? 2 : 3, false, true,
+                                 in_place ? sc.rslots.as<uint32_t>() + (uint64_t)kSlotWords * rb.b[me] : nullptr,
+                                 in_place ? sc.perm.as<uint32_t>() + L.base[me] : nullptr, nullptr, !exact,
+                                 in_place ? L.budget[me] : 0xFFFFFFFFu, a_self));
     if (late) {  // nothing to send: tail slots everywhere
         WQ_HIP(h, hipMemsetAsync(sc.slots.p, 0, (Sb + 1) * kSlotWords * 4, s));
         WQ_HIP(h, hipMemsetAsync(sc.perm.p, 0xFF, (Sb + 1) * 4, s));
@@ -2061,10 +2073,13 @@ static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_k
     }
     if (exact) {
         Xfer x{{sc.slots.p}, {sbytes.data()}, {sc.rslots.p}, {rbytes.data()}, 1};
+        x.skip_self[0] = in_place && !late;
         if ((rc = exchange(h, x))) return rc;
     } else {
         Xfer x{{a_send, sc.slots.p}, {eight.data(), sbytes.data()}, {a_recv, sc.rslots.p},
                {eight.data(), rbytes.data()}, 2};
+        x.skip_self[0] = a_in_place && !late;
+        x.skip_self[1] = in_place && !late;
         if ((rc = exchange(h, x))) return rc;
     }
     sc.last_sent = sent;
