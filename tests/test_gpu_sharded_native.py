@@ -638,7 +638,13 @@ def test_rccl_exchange_one_rank():
     r.attach_rccl(1, 0, rccl_unique_id())
     r.sharded_apply_ops(w.ops)
     r.sharded_apply_ops(churn)
-    _check(_tick(r, w, 0, M, torch.device("cuda:0")), _expected([w.ops, churn], w, 0, M), M)
+    dev = torch.device("cuda:0")
+    want = _expected([w.ops, churn], w, 0, M)
+    _check(_tick(r, w, 0, M, dev), want, M)
+    # the owner form over RCCL: its self segment written in place (no self copy), exact then budgeted
+    sl = (w.pos, w.world, w.sender, w.repl)
+    for _ in range(2):
+        _check_owner_slots([_owner_slot_tick(r, *sl, dev)], [want])
     r.detach_shard()
     r.close()
 
