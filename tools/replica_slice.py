@@ -27,6 +27,10 @@ def main():
     ap.add_argument("--skip-full", action="store_true", help="skip the N = 1 line (profiling one slice size)")
     ap.add_argument("--cfg", type=int, default=0, help="route config (wq_debug_set_route_config; 0 = default)")
     ap.add_argument("--chunks", type=int, default=0, help="pipelined heavy-tick chunks (wq_debug_set_route_chunks)")
+    ap.add_argument("--keys", action="store_true",
+                    help="experiment: route host-quantised raw keys (floor(pos / 16) * 16) instead of the positions")
+    ap.add_argument("--no-msgs", action="store_true", help="experiment: no per-pair message index")
+    ap.add_argument("--slack", type=int, default=0, help="record slots per cube (wq_debug_set_record_slack; 0 = default)")
     a = ap.parse_args()
     import torch
     import bench
@@ -44,6 +48,8 @@ def main():
         r.set_route_config(a.cfg)
     if a.chunks:
         r.set_route_chunks(a.chunks)
+    if a.slack:
+        r.set_record_slack(a.slack)
     t0 = time.perf_counter()
     r.apply_ops(w.ops)
     build_s = time.perf_counter() - t0
@@ -58,25 +64,28 @@ def main():
         repl = torch.from_numpy(w.repl[lo:hi]).to(dev)
         offs = torch.empty(M + 1, dtype=torch.int32, device=dev)
         cnt = torch.zeros(24, dtype=torch.uint8, device=dev)
+        keys = (torch.from_numpy((np.floor(w.pos[lo:hi] / w.cube_size) * w.cube_size).astype(np.int64)).to(dev)
+                if a.keys else None)
         torch.cuda.synchronize(dev)
-        r.route_device(pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
-                       0, 0, 0, cnt.data_ptr())
+        kp = keys.data_ptr() if a.keys else None
+        r.route_device(0 if a.keys else pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M,
+                       offs.data_ptr(), 0, 0, 0, cnt.data_ptr(), keys_ptr=kp)
         torch.cuda.synchronize(dev)
         P = int(_counters(cnt)["n_pairs"][0])
         r.set_fanout_hint(P / max(M, 1))
         cap = P + 1024
         peers = torch.empty(cap, dtype=torch.int32, device=dev)
         msgs = torch.empty(cap, dtype=torch.int32, device=dev)
-        args = (pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M, offs.data_ptr(),
-                peers.data_ptr(), msgs.data_ptr(), cap)
+        args = (0 if a.keys else pos.data_ptr(), world.data_ptr(), sender.data_ptr(), repl.data_ptr(), M,
+                offs.data_ptr(), peers.data_ptr(), 0 if a.no_msgs else msgs.data_ptr(), cap)
         for _ in range(a.warmup):
-            r.route_device(*args, 0)
-        r.route_device(*args, cnt.data_ptr())
+            r.route_device(*args, 0, keys_ptr=kp)
+        r.route_device(*args, cnt.data_ptr(), keys_ptr=kp)
         torch.cuda.synchronize(dev)
         c = _counters(cnt)[0]
         P, F = int(c["n_pairs"]), int(c["n_candidates"])
         assert c["overflow"] == 0 and c["error"] == 0, c
-        t_ms = bench.timed_ticks(lambda: r.route_device(*args, 0), a.steps, stream, dev, 1, [r])
+        t_ms = bench.timed_ticks(lambda: r.route_device(*args, 0, keys_ptr=kp), a.steps, stream, dev, 1, [r])
         tick_s = t_ms / a.steps / 1e3
         B = bench.algorithmic_bytes(M, F, P)
         res["per_n"][str(n)] = {"rank": a.rank, "messages": M, "pairs": P, "tick_us": round(tick_s * 1e6, 1),
