@@ -255,10 +255,10 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
                                 : 1u;
     if (nchunk > 1) {
         if (!rw.side) WQ_HIP(h, hipStreamCreateWithFlags(&rw.side, hipStreamNonBlocking));
-        if (!rw.ev_in) WQ_HIP(h, hipEventCreateWithFlags(&rw.ev_in, hipEventDisableTiming));
+        if (!rw.ev_in) WQ_HIP(h, hipEventCreateWithFlags(&rw.ev_in, hipEventDisableTiming | hipEventReleaseToDevice));
         while (rw.cev.size() < nchunk) {
             hipEvent_t ev;
-            WQ_HIP(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            WQ_HIP(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToDevice));
             rw.cev.push_back(ev);
         }
         WQ_ALLOC(h, rw.carry, 16);
