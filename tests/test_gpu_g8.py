@@ -8,6 +8,8 @@ kernels, exchanges and budgets as on an 8-GPU node, without the link time.
   hub radius tick    C5-shaped (1M moving entities, r = 16): the owners return rows and pools, every
                      ingesting shard filters by radius; two ticks with the move's churn between them
   hub irregular      keys without a packed form (two slots on the wire), by position and by raw key
+  hub owner slots    the owner form (pairs left on the owners) on the C3-shaped tick, mapped back to
+                     every source's messages
   multi handle       wq_router_create_multi_mode with 8 devices, both layouts, the slice form
                      (wq_route_tick_slices_device) on the C3-shaped tick
 """
@@ -129,6 +131,111 @@ def test_hub_g8_c3_slot_tick_route_check():
     for k in range(2):
         assert all(bad == 0 for bad, _ in checks[k]), (k, checks[k])
     assert sum(res[3] for res in results) == o.counts()[0]  # the eight shards partition the table
+    assert P > 2e7
+
+
+def _owner_slot_view(r, pos, world, sender, repl, dev):
+    """One wq_sharded_route_owner_slots tick of host arrays on shard r, its view copied to the host."""
+    import ctypes
+
+    import torch
+    t = [torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+         for x in (pos, world.view(np.int32), sender.view(np.int32), repl)]
+    torch.cuda.synchronize(dev)
+    v = r.sharded_route_owner_slots(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), len(world))
+    R, P, S = int(v.n_slots), int(v.n_pairs), int(v.send_seg[G])
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    offs, peers, perm = np.empty(R + 1, np.uint32), np.empty(max(P, 1), np.uint32), np.empty(max(S, 1), np.uint32)
+    assert hip.hipMemcpy(offs.ctypes.data, v.offsets, (R + 1) * 4, 2) == 0
+    if P:
+        assert hip.hipMemcpy(peers.ctypes.data, v.peers, P * 4, 2) == 0
+    if S:
+        assert hip.hipMemcpy(perm.ctypes.data, v.send_perm, S * 4, 2) == 0
+    return dict(offs=offs, peers=peers[:P], perm=perm[:S], seg=np.array(v.seg[:G + 1], np.int64),
+                send_seg=np.array(v.send_seg[:G + 1], np.int64))
+
+
+def _owner_views_to_csr(views, n_msgs):
+    """The owners' CSRs over their received slots -> each source's CSR in message order (numpy)."""
+    out = []
+    for s in range(G):
+        msg, cnt, start, owner = [], [], [], []
+        for o in range(G):
+            v = views[o]
+            k0, k1 = v["seg"][s], v["seg"][s + 1]
+            sb = views[s]["send_seg"][o]
+            m = views[s]["perm"][sb:sb + (k1 - k0)].astype(np.int64)
+            keep = m != 0xFFFFFFFF
+            slots = np.arange(k0, k1)[keep]
+            msg.append(m[keep])
+            cnt.append((v["offs"][slots + 1] - v["offs"][slots]).astype(np.int64))
+            start.append(v["offs"][slots].astype(np.int64))
+            owner.append(np.full(int(keep.sum()), o))
+        msg, cnt, start, owner = (np.concatenate(x) for x in (msg, cnt, start, owner))
+        assert len(msg) == n_msgs[s] and len(np.unique(msg)) == n_msgs[s]  # every message once
+        order = np.argsort(msg, kind="stable")
+        cnt, start, owner = cnt[order], start[order], owner[order]
+        offs = np.zeros(n_msgs[s] + 1, np.int64)
+        offs[1:] = np.cumsum(cnt)
+        peers = np.empty(int(offs[-1]), np.uint32)
+        for o in range(G):  # each owner's rows, gathered in one vectorised copy
+            sel = owner == o
+            c, st, dst = cnt[sel], start[sel], offs[:-1][sel]
+            if not c.sum():
+                continue
+            within = np.arange(int(c.sum())) - np.repeat(np.cumsum(c) - c, c)
+            peers[np.repeat(dst, c) + within] = views[o]["peers"][np.repeat(st, c) + within]
+        out.append((offs.astype(np.uint32), peers))
+    return out
+
+
+def test_hub_g8_c3_owner_slots_route_check():
+    """The owner form on slots (wq_sharded_route_owner_slots) at G = 8 on the C3-shaped tick: an exact
+    tick, a churn batch, a budgeted tick; the owners' CSRs mapped back to each source's messages
+    through the sources' slot -> message maps, every slice checked by wqo_route_check."""
+    import torch
+    from worldql_server_amd import synth_ext
+    from worldql_server_amd.router import Hub, Router
+    w = synth_ext.config_c3(scale=0.1)
+    churn = _c3_churn(w)
+    M = len(w.world)
+    dev = torch.device("cuda:0")
+    hub = Hub(G)
+    routers = [Router(16, 0) for _ in range(G)]
+    results = [None] * G
+
+    def body(rank):
+        r = routers[rank]
+        r.attach_hub(hub, rank)
+        r.set_fanout_hint(40.0)
+        lo, hi = _slice(M, rank)
+        args = (w.pos[lo:hi], w.world[lo:hi], w.sender[lo:hi], w.repl[lo:hi], dev)
+        r.sharded_apply_ops(w.ops)
+        first = _owner_slot_view(r, *args)
+        r.sharded_apply_ops(churn)
+        second = _owner_slot_view(r, *args)
+        results[rank] = (first, second, r.shard_tick_stats())
+
+    _run_shards(body)
+    for r in routers:
+        r.close()
+    hub.close()
+    n_msgs = [_slice(M, s)[1] - _slice(M, s)[0] for s in range(G)]
+    o = orc.COracle(16)
+    o.apply_ops(w.ops)
+    P = 0
+    for k in range(2):
+        if k == 1:
+            o.apply_ops(churn)
+        csr = _owner_views_to_csr([res[k] for res in results], n_msgs)
+        for s in range(G):
+            lo, hi = _slice(M, s)
+            bad, first_bad = o.route_check(w.pos[lo:hi], w.world[lo:hi], w.sender[lo:hi], w.repl[lo:hi], *csr[s])
+            assert bad == 0, (k, s, bad, first_bad)
+            P += len(csr[s][1]) if k == 1 else 0
+    for res in results:
+        assert res[2] == (1, 1), res[2]  # an exact first tick, a budgeted second
     assert P > 2e7
 
 
