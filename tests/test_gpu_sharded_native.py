@@ -393,7 +393,7 @@ def _view_to_host(r, v, G):
     return dict(offs=offs, peers=peers[:P], perm=perm[:send_seg[-1]], seg=list(v.seg[:G + 1]), send_seg=send_seg)
 
 
-@pytest.mark.parametrize("G", [2, 3])
+@pytest.mark.parametrize("G", [1, 2, 3])
 def test_hub_owner_slots_async_vs_whole_table_oracle(G):
     """wq_sharded_route_owner_slots_async: the first call runs exact (synchronously, n_pairs filled),
     the next ones return at once with P in the caller's counters; the last tick's view against the

@@ -10,6 +10,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include "route_common.hpp"
+#include "route_async.hpp"
 
 namespace wq {
 
@@ -32,6 +33,9 @@ struct TileScanParams {
     // offsets[M], no counters)
     uint64_t* carry = nullptr;
     uint32_t chunk = 0;
+    // an asynchronous sharded tick's end (route_async.hpp), run by the one-block scan after its counters
+    AsyncResultParams ar{};
+    bool async_end = false;
 };
 
 // Inclusive wave64 prefix sum of u32 by DPP row shifts and row broadcasts (no LDS round trips).
@@ -125,6 +129,10 @@ static __global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScan
         flag_route(p.cnt, p.health, P > 0xFFFFFFFFull ? 2u : 0u, P > p.capacity ? 1u : 0u);
         if (p.stale && *p.stale) flag_route(p.cnt, p.health, kErrStale, 0u);
     }
+    if (p.async_end) {  // (never with chunks) the counters above are final: the tick's end, here
+        __syncthreads();
+        async_result_block(p.ar);
+    }
 }
 
 // Many tiles (C3: 39,063): one block cannot keep up (the single-block scan above took ~60-76 us
@@ -159,12 +167,15 @@ constexpr uint32_t kScanOneBlockMax = 8192;  // tiles: up to here the one-block 
 
 // The tick's tile scan (n_tiles >= 1): one block for a few thousand tiles (C2: 3,907),
 // rocPRIM + tile_finish_kernel beyond. P must fit the u32 offsets either way (error bit 2 if not);
-// a tick of > 2^32 pairs wraps the prefix, which the error bit already reports.
-inline int launch_tile_scan(wq_router* h, const TileScanParams& sp) {
+// a tick of > 2^32 pairs wraps the prefix, which the error bit already reports. With sp.async_end,
+// *async_done says whether the scan took the asynchronous tick's end (the one-block scan only).
+inline int launch_tile_scan(wq_router* h, const TileScanParams& sp, bool* async_done = nullptr) {
     hipStream_t s = h->stream;
+    if (async_done) *async_done = false;
     if (sp.n_tiles <= kScanOneBlockMax) {
         hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, sp);
         WQ_HIP(h, hipGetLastError());
+        if (async_done) *async_done = sp.async_end;
         return WQ_OK;
     }
     size_t bytes = 0;

@@ -160,20 +160,7 @@ RcclApi& rccl() {
 
 constexpr int kXNone = 0, kXHub = 1, kXRccl = 2, kXCallback = 3;
 constexpr double kHubTimeoutS = 120.0;
-// The small exchange vectors (ShardCtx::small, allocated at attach). Slot tick: A = {slots, status}
-// u32 x 2 per shard (send at kSmallA, receive right after), C = {pool words, status} u32 x 2 per
-// shard (send at kSmallC, receive right after), and at kSmallCnt four counter blocks: the
-// message-side tile scan (P, error / overflow bits), the own-cube count pass, the owner's count pass
-// over received slots, and a scratch block (the count kernels' "next call" slot). Status words:
-// bits 0-7 the negated WQ_E_* code of a local failure, 8-23 device error bits (8 stale table, 4
-// spin, 2 > 2^32 pairs), 31 (kStBudget) an exchange budget was too small. The expanded-return tick
-// uses {count, status} u32 x 2 at kSmallA and {pairs, status} u64 x 2 at kSmallC.
-constexpr size_t kSmallA = 0, kSmallC = 1024, kSmallCnt = 5120, kSmallBytes = 8192;
-constexpr size_t kCntScan = 0, kCntSelf = 1, kCntOwner = 2, kCntScratch = 3;
-static_assert(kSmallA + 4 * WQ_MAX_SHARDS * 4 <= kSmallC && kSmallC + 8 * WQ_MAX_SHARDS * 8 <= kSmallCnt &&
-                  kSmallCnt + 4 * sizeof(wq_route_counters) <= kSmallBytes,
-              "small exchange vector layout");
-constexpr uint32_t kStCodeMask = 0xFFu;
+// (the small exchange vectors' layout, kSmall* / kCnt* / kStCodeMask: route_async.hpp)
 // Blocks of a sharded count or emit pass over n tiles, shaped as launch_route's (WQ_DEBUG_SHARD_TPB:
 // tiles per block, diagnostics)
 inline uint32_t pass_blocks(uint32_t n) {
@@ -921,7 +908,8 @@ int attach(wq_router* h, uint32_t G, uint32_t rank) {
 // mtiles): the tile scan (offsets[M] = P, the counters at kCntScan: P, the overflow / error bits),
 // then emit_map_kernel — rows of this shard's own cubes read the table, the others the pools
 // received (outputs beyond capacity are not written).
-int slots_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity) {
+int slots_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs, size_t capacity,
+                   const AsyncResultParams* ar = nullptr, bool* ar_done = nullptr) {
     ShardCtx& sc = *h->shard;
     const uint64_t M = sc.last_M;
     hipStream_t s = h->stream;
@@ -945,7 +933,11 @@ int slots_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, uint32_
     tp.cnt = cnt;
     tp.health = h->rws.buf.p ? route_health(h) : nullptr;
     tp.stale = h->tab.stale.as<uint32_t>();  // error bit 8: the table still misses a device batch
-    if (int rc = launch_tile_scan(h, tp)) return rc;
+    if (ar) {  // an asynchronous tick: the scan ends it (if it is the one-block scan)
+        tp.ar = *ar;
+        tp.async_end = true;
+    }
+    if (int rc = launch_tile_scan(h, tp, ar_done)) return rc;
     EmitParams ep;
     ep.sender = sc.last_sender;
     ep.pos = sc.last_radius ? sc.last_pos : nullptr;
@@ -1358,70 +1350,9 @@ static int async_drain(wq_router* h, uint32_t keep) {
     return WQ_OK;
 }
 
-// wq_route_health / counters error bits of an asynchronous sharded tick (include/wq_router.h)
-constexpr uint32_t kErrShardStep = 32u, kErrRedo = 64u;
-
-struct AsyncResultParams {
-    const uint32_t* a_recv;  // 2G words: {slots, status} from every shard
-    const uint32_t* c_recv;  // 2G words: {pool words, status} from every shard
-    uint32_t G;
-    const wq_route_counters* cnt;  // the tick's counter blocks (kCntScan, kCntSelf, kCntOwner)
-    uint32_t has_msgs;
-    uint64_t capacity;
-    wq_route_counters* out;  // the caller's (nullable)
-    uint32_t* health;        // the handle's sticky words
-    const uint32_t* small;   // the tick's small vectors (words; the ones in use: small_word) ...
-    uint32_t* snap;          // ... copied here (mapped pinned memory), then the sequence word
-    uint64_t seq;
-    uint32_t* zero;          // the small vectors, zeroed last for the next tick
-};
-
-// (asynchronous tick) what the synchronous tick reads back, folded on the device into the caller's
-// counters and the sticky health words: P, a shard's failed step (32), the device bits of every
-// shard's statuses and counters, a budget that was too small (64: the outputs are not valid; every
-// shard sees it and the next call runs exact).
-// The words of the small vectors a tick uses: A and C (4G words each) and the counter blocks.
-__device__ __forceinline__ uint32_t small_word(uint32_t k, uint32_t G) {
-    const uint32_t ac = 4 * G;
-    return k < ac ? kSmallA / 4 + k : k < 2 * ac ? kSmallC / 4 + (k - ac) : kSmallCnt / 4 + (k - 2 * ac);
-}
-
-__global__ __launch_bounds__(256) void k_async_result(AsyncResultParams p) {
-    // only the words in use cross PCIe (the vectors' 8 KB would be ~20 times as many)
-    const uint32_t nw = 8 * p.G + (uint32_t)(4 * sizeof(wq_route_counters) / 4);
-    for (uint32_t k = threadIdx.x; k < nw; k += blockDim.x) {
-        const uint32_t i = small_word(k, p.G);
-        p.snap[i] = p.small[i];
-    }
-    __threadfence_system();  // every thread's part of the snapshot visible to the host ...
-    __syncthreads();
-    if (threadIdx.x == 0) {  // ... before the sequence word
-        __hip_atomic_store(reinterpret_cast<uint64_t*>(p.snap + kSmallBytes / 4), p.seq, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-        uint32_t err = 0;
-        for (uint32_t d = 0; p.G > 1 && d < p.G; ++d) {
-            for (uint32_t st : {p.a_recv[2 * d + 1], p.c_recv[2 * d + 1]}) {
-                if (st & kStCodeMask) err |= kErrShardStep;
-                err |= (st >> 8) & 0xFFFFu;
-                if (st & kStBudget) err |= kErrRedo;
-            }
-        }
-        err |= p.cnt[kCntScan].error | p.cnt[kCntSelf].error | p.cnt[kCntOwner].error;
-        const uint64_t P = p.has_msgs ? p.cnt[kCntScan].n_pairs : 0;
-        const uint32_t ovf = P > p.capacity ? 1u : 0u;
-        if (p.out) {
-            p.out->n_pairs = P;
-            p.out->n_candidates = p.has_msgs ? p.cnt[kCntScan].n_candidates : 0;
-            p.out->overflow = ovf;
-            p.out->error = err;
-        }
-        if (err) atomicOr(p.health, err);
-        if (ovf) atomicOr(p.health + 1, 1u);
-    }
-    __syncthreads();
-    // the small vectors zeroed for the next tick (here, rather than a memset launch at its start)
-    for (uint32_t k = threadIdx.x; k < nw; k += blockDim.x) p.zero[small_word(k, p.G)] = 0u;
-}
+// (asynchronous tick) the end-of-tick snapshot kernel, when the tile scan could not take it
+// (route_async.hpp async_result_block: a scan over more tiles than one block takes, or no scan)
+__global__ __launch_bounds__(256) void k_async_result(AsyncResultParams p) { async_result_block(p); }
 
 
 static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, const uint32_t* d_world,
@@ -1856,32 +1787,40 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
         sc.last_repl = d_repl;
         sc.last_radius = radius;
         sc.last_gen = h->table_gen;
-        if ((rc = slots_copy_out(h, d_offsets, d_peers, d_msgs, capacity))) return rc;
     }
-
     // ---- asynchronous end (wq_sharded_route_tick_async, a budgeted tick without a local failure):
     // no host read; the small vectors go to a pinned snapshot the next calls fold in (budgets), P and
-    // the statuses to the caller's counters and the health words ----
-    if (async && !exact && !late) {
-        const uint32_t k = (sc.ahead + sc.acount) % ShardCtx::kRing;  // async_drain left a free slot
-        sc.acount++;
-        sc.n_async++;
-        sc.aseq[k] = sc.n_async;
-        AsyncResultParams ar{};
+    // the statuses to the caller's counters and the health words — at the end of the tile scan when
+    // one block runs it, else by k_async_result ----
+    const bool async_end = async && !exact && !late;
+    AsyncResultParams ar{};
+    const uint32_t ak = (sc.ahead + sc.acount) % ShardCtx::kRing;  // async_drain left a free slot
+    if (async_end) {
         ar.a_recv = a_recv;
         ar.c_recv = c_recv;
         ar.G = G;
+        ar.statuses = G > 1 ? 1u : 0u;
         ar.cnt = cnts;
         ar.has_msgs = M ? 1u : 0u;
         ar.capacity = capacity;
         ar.out = d_result;
         ar.health = route_health(h);
         ar.small = reinterpret_cast<const uint32_t*>(small);
-        ar.snap = static_cast<uint32_t*>(sc.asnap[k]);
-        ar.seq = sc.aseq[k];
+        ar.snap = static_cast<uint32_t*>(sc.asnap[ak]);
+        ar.seq = sc.n_async + 1;
         ar.zero = reinterpret_cast<uint32_t*>(small);
-        hipLaunchKernelGGL(k_async_result, dim3(1), dim3(256), 0, s, ar);
-        WQ_HIP(h, hipGetLastError());
+    }
+    bool ar_done = false;
+    if (!late && (rc = slots_copy_out(h, d_offsets, d_peers, d_msgs, capacity, async_end ? &ar : nullptr, &ar_done)))
+        return rc;
+    if (async_end) {
+        if (!ar_done) {
+            hipLaunchKernelGGL(k_async_result, dim3(1), dim3(256), 0, s, ar);
+            WQ_HIP(h, hipGetLastError());
+        }
+        sc.acount++;
+        sc.n_async++;
+        sc.aseq[ak] = sc.n_async;
         sc.small_zeroed = true;
         sc.last_ready = false;  // no copy-out of an unread tick (its P is on the device)
         *n_pairs = 0;
@@ -1923,7 +1862,8 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
 // work as in the slot tick (the previous tick's true sizes + headroom, the first tick exact); a short
 // budget anywhere reaches every shard through X1 (ShardIn::a_or) and all of them redo the tick
 // exactly. One host read at the end: P, the statuses, the true sizes.
-static int owner_emit(wq_router* h, uint64_t Rb, const TableView& tv) {
+static int owner_emit(wq_router* h, uint64_t Rb, const TableView& tv, const AsyncResultParams* ar = nullptr,
+                      bool* ar_done = nullptr) {
     ShardCtx& sc = *h->shard;
     RouteWs& rw = h->rws;
     hipStream_t s = h->stream;
@@ -1940,7 +1880,11 @@ static int owner_emit(wq_router* h, uint64_t Rb, const TableView& tv) {
     tp.cnt = reinterpret_cast<wq_route_counters*>(sc.small.as<char>() + kSmallCnt) + kCntScan;
     tp.health = nullptr;  // a short pair buffer is grown and emitted again, not an overflow
     tp.stale = tv.stale;
-    if (int rc = launch_tile_scan(h, tp)) return rc;
+    if (ar) {  // an asynchronous tick: the scan ends it (if it is the one-block scan)
+        tp.ar = *ar;
+        tp.async_end = true;
+    }
+    if (int rc = launch_tile_scan(h, tp, ar_done)) return rc;
     EmitParams ep;
     ep.sender = sc.rslots.as<uint32_t>() + 3;  // OnlySelf rows: the slot's sender word
     ep.sender_stride = kSlotWords;
@@ -2094,6 +2038,26 @@ static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_k
                   fail(alloc(sc.otiles, ((uint64_t)nto * 3 + 4) * 4)) || fail(alloc(sc.own_off, (Rb + 1) * 4)) ||
                   fail(alloc(sc.own_peers, sc.own_cap * 4)))) {
     }
+    // the asynchronous end's snapshot (below), taken by the tile scan when one block runs it
+    const bool async_end = async && !exact;
+    AsyncResultParams ar{};
+    const uint32_t ak = (sc.ahead + sc.acount) % ShardCtx::kRing;  // async_drain left a free slot
+    if (async_end) {
+        ar.a_recv = a_recv;
+        ar.c_recv = reinterpret_cast<const uint32_t*>(small + kSmallC) + 2 * G;  // zero: no second exchange
+        ar.G = G;
+        ar.statuses = 1u;  // every segment budgeted, this shard's own included: G = 1 too
+        ar.cnt = cnts;
+        ar.has_msgs = Rb ? 1u : 0u;
+        ar.capacity = sc.own_cap;
+        ar.out = d_result;
+        ar.health = route_health(h);
+        ar.small = reinterpret_cast<const uint32_t*>(small);
+        ar.snap = static_cast<uint32_t*>(sc.asnap[ak]);
+        ar.seq = sc.n_async + 1;
+        ar.zero = reinterpret_cast<uint32_t*>(small);
+    }
+    bool ar_done = false;
     if (!late && Rb) {
         CountParams cp{};
         cp.in = RouteIn{nullptr, nullptr, nullptr, nullptr, nullptr, (uint32_t)Rb, (int64_t)h->cube_size};
@@ -2109,7 +2073,7 @@ static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_k
         cp.n_tiles = nto;
         hipLaunchKernelGGL((count_kernel<false, 1, 8, 0, false, true>), dim3(pass_blocks(nto)), dim3(kBlock), 0, s, cp);
         if (hipGetLastError() != hipSuccess) fail(set_error(h, WQ_E_HIP, "count launch (owner form)"));
-        if (!late) fail(owner_emit(h, Rb, tv));
+        if (!late) fail(owner_emit(h, Rb, tv, async_end && !late ? &ar : nullptr, &ar_done));
     }
 
     auto fill_view = [&](uint64_t P) {
@@ -2127,27 +2091,15 @@ static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_k
     // ---- asynchronous end (a budgeted tick without a local failure): as the slot tick's — the
     // small vectors to a pinned snapshot folded in two calls later, P and the statuses to the
     // caller's counters and the health words; a pair buffer that was short shows as overflow ----
-    if (async && !exact && !late) {
+    if (async_end && !late) {
         if (!Rb) WQ_HIP(h, hipMemsetAsync(sc.own_off.p, 0, 4, s));
-        const uint32_t k = (sc.ahead + sc.acount) % ShardCtx::kRing;  // async_drain left a free slot
+        if (!ar_done) {
+            hipLaunchKernelGGL(k_async_result, dim3(1), dim3(256), 0, s, ar);
+            WQ_HIP(h, hipGetLastError());
+        }
         sc.acount++;
         sc.n_async++;
-        sc.aseq[k] = sc.n_async;
-        AsyncResultParams ar{};
-        ar.a_recv = a_recv;
-        ar.c_recv = reinterpret_cast<const uint32_t*>(small + kSmallC) + 2 * G;  // zero: no second exchange
-        ar.G = G;
-        ar.cnt = cnts;
-        ar.has_msgs = Rb ? 1u : 0u;
-        ar.capacity = sc.own_cap;
-        ar.out = d_result;
-        ar.health = route_health(h);
-        ar.small = reinterpret_cast<const uint32_t*>(small);
-        ar.snap = static_cast<uint32_t*>(sc.asnap[k]);
-        ar.seq = sc.aseq[k];
-        ar.zero = reinterpret_cast<uint32_t*>(small);
-        hipLaunchKernelGGL(k_async_result, dim3(1), dim3(256), 0, s, ar);
-        WQ_HIP(h, hipGetLastError());
+        sc.aseq[ak] = sc.n_async;
         sc.small_zeroed = true;
         fill_view(~0ull);  // P: in the caller's counters
         return WQ_OK;
