@@ -559,47 +559,81 @@ __global__ void __launch_bounds__(kBlock)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t b = blockIdx.x, NB = in.nblk, G = in.G;
     for (uint32_t k = threadIdx.x; k < kShardIPT * kWaves * WQ_MAX_SHARDS; k += kBlock) (&wc[0][0])[k] = 0;
-    __syncthreads();
+    lds_barrier();
     const uint64_t lt = (1ull << lane) - 1;
     const uint32_t m0 = b * kShardTile + threadIdx.x;
-    int64_t kx[kShardIPT], ky[kShardIPT], kz[kShardIPT];
-    uint64_t pk[kShardIPT];
-    uint32_t ext[kShardIPT], own[kShardIPT], rank[kShardIPT];
-    bool reg[kShardIPT], go[kShardIPT];
-    uint32_t wrd[kShardIPT], snd[kShardIPT], rpl[kShardIPT];
+    // per message only what the scatter writes for a regular key (a wide key's coordinates are
+    // quantised again there): few registers live across the look-back, so every block of a tick
+    // is resident at once. inf: bits 0-7 the owner (kNoOwner: no slot), 8-15 replication, 16 regular
+    constexpr uint32_t kNoOwner = 0xFFu;
+    uint32_t pkl[kShardIPT], pkh[kShardIPT], ext[kShardIPT], snd[kShardIPT], inf[kShardIPT], rank[kShardIPT];
+    // every load of the block's messages in flight before any is used (no branch between them: a
+    // lane past M reads message M - 1 and drops it), then the keys, owners and slot words
+    uint64_t raw[kShardIPT][3];
+    uint32_t wrd[kShardIPT], rpl[kShardIPT];
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint32_t m = min(m0 + i * kBlock, in.M - 1);
+        const uint64_t* src = RAW ? reinterpret_cast<const uint64_t*>(in.keys) + 3ull * m
+                                  : reinterpret_cast<const uint64_t*>(in.pos) + 3ull * m;
+        raw[i][0] = src[0];
+        raw[i][1] = src[1];
+        raw[i][2] = src[2];
+        wrd[i] = in.world[m];
+        snd[i] = in.sender[m];
+        rpl[i] = in.repl[m];
+    }
 #pragma unroll
     for (int i = 0; i < kShardIPT; ++i) {
         const uint32_t m = m0 + i * kBlock;
-        go[i] = m < in.M;
-        own[i] = 0xFFFFFFFFu;
+        inf[i] = kNoOwner;
         rank[i] = 0;
-        reg[i] = true;
-        wrd[i] = snd[i] = rpl[i] = 0;
-        if (go[i]) {
-            msg_key<RAW>(in, m, kx[i], ky[i], kz[i]);
-            wrd[i] = in.world[m];
-            snd[i] = in.sender[m];
-            rpl[i] = in.repl[m];
-            own[i] = shard_of(wrd[i], kx[i], ky[i], kz[i], G);
-            reg[i] = pack_key(wrd[i], kx[i], ky[i], kz[i], in.sf, &pk[i], &ext[i]);
-            go[i] = own[i] != in.me || in.own_too;
-            if (in.zero_e) in.zero_e[m] = 0u;
+        pkl[i] = pkh[i] = ext[i] = 0;
+        if (m < in.M) {
+            int64_t kx, ky, kz;
+            if (RAW) {
+                kx = (int64_t)raw[i][0];
+                ky = (int64_t)raw[i][1];
+                kz = (int64_t)raw[i][2];
+            } else {
+                kx = coord_clamp_dev(__longlong_as_double((long long)raw[i][0]), in.sf, in.si);
+                ky = coord_clamp_dev(__longlong_as_double((long long)raw[i][1]), in.sf, in.si);
+                kz = coord_clamp_dev(__longlong_as_double((long long)raw[i][2]), in.sf, in.si);
+            }
+            const uint32_t own = shard_of(wrd[i], kx, ky, kz, G);
+            uint64_t pk = 0;
+            const bool reg = pack_key(wrd[i], kx, ky, kz, in.sf, &pk, &ext[i]);
+            pkl[i] = (uint32_t)pk;
+            pkh[i] = (uint32_t)(pk >> 32);
+            if (own != in.me || in.own_too) inf[i] = own | (rpl[i] << 8) | (reg ? 1u << 16 : 0u);
         }
     }
+    if (in.zero_e) {
+#pragma unroll
+        for (int i = 0; i < kShardIPT; ++i)
+            if (m0 + i * kBlock < in.M) in.zero_e[m0 + i * kBlock] = 0u;
+    }
+    // ranks within the wave: the lanes of one owner found by log2(G') ballots of the owner's bits
+    // (not one ballot round per owner present)
+    uint32_t nbits = 0;
+    while ((1u << nbits) < G) ++nbits;
 #pragma unroll
     for (int i = 0; i < kShardIPT; ++i) {
-        const uint64_t wide = __ballot(go[i] && !reg[i]);
-        uint64_t todo = __ballot(go[i]);
-        while (todo) {
-            const int leader = __ffsll((unsigned long long)todo) - 1;
-            const uint32_t d = __shfl(own[i], leader, 64);
-            const uint64_t mask = __ballot(go[i] && own[i] == d);
-            if (go[i] && own[i] == d) rank[i] = __popcll(mask & lt) + __popcll(mask & wide & lt);
-            if (lane == leader) wc[i * kWaves + wave][d] = __popcll(mask) + __popcll(mask & wide);
-            todo &= ~mask;
+        const bool go = (inf[i] & 0xFFu) != kNoOwner, reg = (inf[i] >> 16) & 1u;
+        const uint32_t own = inf[i] & 0xFFu;
+        const uint64_t wide = __ballot(go && !reg);
+        uint64_t same = __ballot(go);
+        for (uint32_t bit = 0; bit < nbits; ++bit) {
+            const bool on = (own >> bit) & 1u;
+            const uint64_t bm = __ballot(on);
+            same &= on ? bm : ~bm;
+        }
+        if (go) {
+            rank[i] = __popcll(same & lt) + __popcll(same & wide & lt);
+            if ((same & lt) == 0) wc[i * kWaves + wave][own] = __popcll(same) + __popcll(same & wide);
         }
     }
-    __syncthreads();
+    lds_barrier();
     // the block's per-owner totals (published at once) and its rows' offsets within the block
     for (uint32_t d = threadIdx.x; d < G; d += kBlock) {
         uint32_t run = 0;
@@ -613,7 +647,7 @@ __global__ void __launch_bounds__(kBlock)
         __hip_atomic_store(g.look + (uint64_t)d * NB + b, granule(g.tag, b == 0 ? kFlagP : kFlagA, run),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __syncthreads();
+    lds_barrier();
     if (wave == 0) {
         // lanes [d * W, d * W + W) look back for owner d, lane k of the group at block b - 1 - (r W + k)
         uint32_t Gp = 1;
@@ -646,7 +680,7 @@ __global__ void __launch_bounds__(kBlock)
             if (g.a_self) atomicOr(&g.a_self[1], 7u);
         }
     }
-    __syncthreads();
+    lds_barrier();
     if (b == NB - 1) {  // the last block knows every owner's true count
         for (uint32_t d = threadIdx.x; d < G; d += kBlock) {
             const uint32_t n = base[d] + bcnt[d];
@@ -671,41 +705,44 @@ __global__ void __launch_bounds__(kBlock)
 #pragma unroll
     for (int i = 0; i < kShardIPT; ++i) {
         const uint32_t m = m0 + i * kBlock;
-        if (!go[i]) continue;
-        const uint32_t d = own[i];
+        const uint32_t d = inf[i] & 0xFFu;
+        if (d == kNoOwner) continue;
+        const bool reg = (inf[i] >> 16) & 1u;
         const uint32_t j = base[d] + wc[i * kWaves + wave][d] + rank[i];  // within the owner's segment
         uint32_t slot;
         uint32_t* pm;
         uint32_t* o;
         if (d == in.me) {  // own slots on: this shard's own message, into its own buffer
-            if (j + (reg[i] ? 1u : 2u) > in.own_budget) continue;  // (the owner form's self segment)
+            if (j + (reg ? 1u : 2u) > in.own_budget) continue;  // (the owner form's self segment)
             slot = j;
             pm = in.own_perm;
             o = in.own_slots + (uint64_t)kSlotWords * slot;
         } else {
-            if (j + (reg[i] ? 1u : 2u) > L.budget[d]) continue;  // over budget: the tick is redone exactly
+            if (j + (reg ? 1u : 2u) > L.budget[d]) continue;  // over budget: the tick is redone exactly
             slot = L.base[d] + j;
             pm = perm;
             o = out + (uint64_t)kSlotWords * slot;
         }
-        const uint32_t rp = rpl[i];
-        if (reg[i]) {
-            o[0] = (uint32_t)pk[i];
-            o[1] = (uint32_t)(pk[i] >> 32);
+        const uint32_t rp = (inf[i] >> 8) & 0xFFu;
+        if (reg) {
+            o[0] = pkl[i];
+            o[1] = pkh[i];
             o[2] = ext[i];
             o[3] = snd[i];
             o[4] = rp | (kSlotReg << 8);
             pm[slot] = m;
-        } else {
-            o[0] = (uint32_t)(uint64_t)kx[i];
-            o[1] = (uint32_t)((uint64_t)kx[i] >> 32);
-            o[2] = wrd[i];
+        } else {  // a wide key (rare): head and tail slot with the coordinates, quantised again
+            int64_t kx, ky, kz;
+            msg_key<RAW>(in, m, kx, ky, kz);
+            o[0] = (uint32_t)(uint64_t)kx;
+            o[1] = (uint32_t)((uint64_t)kx >> 32);
+            o[2] = in.world[m];
             o[3] = snd[i];
             o[4] = rp | (kSlotHead << 8);
-            o[5] = (uint32_t)(uint64_t)ky[i];
-            o[6] = (uint32_t)((uint64_t)ky[i] >> 32);
-            o[7] = (uint32_t)(uint64_t)kz[i];
-            o[8] = (uint32_t)((uint64_t)kz[i] >> 32);
+            o[5] = (uint32_t)(uint64_t)ky;
+            o[6] = (uint32_t)((uint64_t)ky >> 32);
+            o[7] = (uint32_t)(uint64_t)kz;
+            o[8] = (uint32_t)((uint64_t)kz >> 32);
             o[9] = kSlotTail << 8;
             pm[slot] = m;
             pm[slot + 1] = kNone;
