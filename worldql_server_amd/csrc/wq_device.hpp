@@ -147,6 +147,46 @@ __host__ __device__ __forceinline__ bool pack_key(uint32_t w, int64_t x, int64_t
     return true;
 }
 
+// coord_clamp_dev on the three coordinates and pack_key on the key, in one pass, with the same
+// results for every input (tests/test_quantize_pack.py checks it against the two functions). For a
+// finite coordinate with n = |c| / s (an exact multiple) or ceil(|c| / s) [+ 1] at most 2^23 + 2
+// and a cube size below 2^29, every product is exact and the key is n s with the sign of c: the key
+// and pack_key's biased axis n + 2^23 come from n in integer arithmetic, and k / s = n exactly is
+// pack_key's integer test. That skips, per axis, the saturating f64 -> i64 conversion, pack_key's
+// second division and its conversion. Anything else (NaN, inf, huge coordinates or cube sizes)
+// takes coord_clamp_dev and pack_key themselves. Used by the slot grouping (wq_shard.hip), whose
+// quantisation is VALU-bound; in the route tick's count it made C2 slower.
+__host__ __device__ __forceinline__ bool quantize_pack(uint32_t w, const double (&c)[3], double sf, int64_t si,
+                                                       int64_t (&k)[3], uint64_t* pk, uint32_t* ext) {
+    bool fast = si >= 1 && si < (1ll << 29), ok = w <= kMaxPackedWorld;
+    uint64_t a[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const double x = c[d], ax = fabs(x), q = ax / sf;
+        const bool is_mult = (q == trunc(q)) && (fma(q, sf, -ax) == 0.0) && (x != 0.0);
+        const double cq = (ax == 0.0) ? 1.0 : ceil(q);
+        const bool add = !is_mult & !(cq * sf > x);
+        const double nd = is_mult ? q : cq + (add ? 1.0 : 0.0);
+        const bool f = nd <= 8388610.0;  // 2^23 + 2; false for NaN
+        fast = fast && f;
+        const int64_t n_abs = (int64_t)(int32_t)(f ? nd : 0.0);
+        const int64_t n = x < 0.0 ? -n_abs : n_abs;
+        k[d] = n * si;
+        ok = ok && n >= -(int64_t)kAxisBias && n < (int64_t)kAxisBias && k[d] > -(1ll << 40) && k[d] < (1ll << 40);
+        a[d] = (uint64_t)(n + (int64_t)kAxisBias);
+    }
+    if (!fast) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) k[d] = coord_clamp_dev(c[d], sf, si);
+        return pack_key(w, k[0], k[1], k[2], sf, pk, ext);
+    }
+    if (ok) {  // (pack_key writes nothing for an irregular key either)
+        *pk = (a[0] << 48) | (a[1] << 24) | a[2];
+        *ext = ((w + 1u) << 8) | (uint32_t)(a[0] >> 16);
+    }
+    return ok;
+}
+
 // The packed key's world and biased axes (a_d = k_d / s + 2^23).
 __host__ __device__ __forceinline__ void unpack_key(uint64_t pk, uint32_t ext, uint32_t* w, uint32_t* a) {
     *w = (ext >> 8) - 1u;

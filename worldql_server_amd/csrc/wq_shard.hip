@@ -590,19 +590,21 @@ __global__ void __launch_bounds__(kBlock)
         rank[i] = 0;
         pkl[i] = pkh[i] = ext[i] = 0;
         if (m < in.M) {
-            int64_t kx, ky, kz;
-            if (RAW) {
-                kx = (int64_t)raw[i][0];
-                ky = (int64_t)raw[i][1];
-                kz = (int64_t)raw[i][2];
-            } else {
-                kx = coord_clamp_dev(__longlong_as_double((long long)raw[i][0]), in.sf, in.si);
-                ky = coord_clamp_dev(__longlong_as_double((long long)raw[i][1]), in.sf, in.si);
-                kz = coord_clamp_dev(__longlong_as_double((long long)raw[i][2]), in.sf, in.si);
-            }
-            const uint32_t own = shard_of(wrd[i], kx, ky, kz, G);
+            int64_t k[3];
             uint64_t pk = 0;
-            const bool reg = pack_key(wrd[i], kx, ky, kz, in.sf, &pk, &ext[i]);
+            bool reg;
+            if (RAW) {
+                k[0] = (int64_t)raw[i][0];
+                k[1] = (int64_t)raw[i][1];
+                k[2] = (int64_t)raw[i][2];
+                reg = pack_key(wrd[i], k[0], k[1], k[2], in.sf, &pk, &ext[i]);
+            } else {
+                const double c[3] = {__longlong_as_double((long long)raw[i][0]),
+                                     __longlong_as_double((long long)raw[i][1]),
+                                     __longlong_as_double((long long)raw[i][2])};
+                reg = quantize_pack(wrd[i], c, in.sf, in.si, k, &pk, &ext[i]);
+            }
+            const uint32_t own = shard_of(wrd[i], k[0], k[1], k[2], G);
             pkl[i] = (uint32_t)pk;
             pkh[i] = (uint32_t)(pk >> 32);
             if (own != in.me || in.own_too) inf[i] = own | (rpl[i] << 8) | (reg ? 1u << 16 : 0u);
