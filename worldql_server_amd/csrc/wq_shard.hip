@@ -420,6 +420,150 @@ __global__ void __launch_bounds__(kScanThreads1)
     }
 }
 
+// A thread's kShardIPT messages (m0 + i * kBlock) once quantised and ranked: what the scatter
+// writes for a regular key (a wide key's coordinates are quantised again there, so few registers
+// stay live across the base computation and every block of a tick can be resident at once).
+// inf: bits 0-7 the owner (kNoOwner: no slot), 8-15 replication, 16 regular.
+constexpr uint32_t kNoOwner = 0xFFu;
+struct SlotRows {
+    uint32_t pkl[kShardIPT], pkh[kShardIPT], ext[kShardIPT], snd[kShardIPT], inf[kShardIPT], rank[kShardIPT];
+};
+
+// (slot_scatter_kernel, slot_group_kernel) load, quantise and rank a block's messages: every load
+// in flight before any is used (no branch between them: a lane past M reads message M - 1 and
+// drops it), the key, owner and slot words by quantize_pack, then the ranks within the wave — the
+// lanes of one owner found by log2(G') ballots of the owner's bits — and each wave-row's per-owner
+// counts in wc (zeroed by the caller; a wide key counts two slots). zero: e[m] = 0 for the slot
+// tick's rows (in.zero_e).
+template <bool RAW>
+__device__ __forceinline__ void slot_rows(const ShardIn& in, uint32_t m0, bool zero,
+                                          uint32_t (&wc)[kShardIPT * kWaves][WQ_MAX_SHARDS], SlotRows& r) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt = (1ull << lane) - 1;
+    const uint32_t G = in.G;
+    uint64_t raw[kShardIPT][3];
+    uint32_t wrd[kShardIPT], rpl[kShardIPT];
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint32_t m = min(m0 + i * kBlock, in.M - 1);
+        const uint64_t* src = RAW ? reinterpret_cast<const uint64_t*>(in.keys) + 3ull * m
+                                  : reinterpret_cast<const uint64_t*>(in.pos) + 3ull * m;
+        raw[i][0] = src[0];
+        raw[i][1] = src[1];
+        raw[i][2] = src[2];
+        wrd[i] = in.world[m];
+        r.snd[i] = in.sender[m];
+        rpl[i] = in.repl[m];
+    }
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint32_t m = m0 + i * kBlock;
+        r.inf[i] = kNoOwner;
+        r.rank[i] = 0;
+        r.pkl[i] = r.pkh[i] = r.ext[i] = 0;
+        if (m < in.M) {
+            int64_t k[3];
+            uint64_t pk = 0;
+            bool reg;
+            if (RAW) {
+                k[0] = (int64_t)raw[i][0];
+                k[1] = (int64_t)raw[i][1];
+                k[2] = (int64_t)raw[i][2];
+                reg = pack_key(wrd[i], k[0], k[1], k[2], in.sf, &pk, &r.ext[i]);
+            } else {
+                const double c[3] = {__longlong_as_double((long long)raw[i][0]),
+                                     __longlong_as_double((long long)raw[i][1]),
+                                     __longlong_as_double((long long)raw[i][2])};
+                reg = quantize_pack(wrd[i], c, in.sf, in.si, k, &pk, &r.ext[i]);
+            }
+            const uint32_t own = shard_of(wrd[i], k[0], k[1], k[2], G);
+            r.pkl[i] = (uint32_t)pk;
+            r.pkh[i] = (uint32_t)(pk >> 32);
+            if (own != in.me || in.own_too) r.inf[i] = own | (rpl[i] << 8) | (reg ? 1u << 16 : 0u);
+        }
+    }
+    if (zero && in.zero_e) {
+#pragma unroll
+        for (int i = 0; i < kShardIPT; ++i)
+            if (m0 + i * kBlock < in.M) in.zero_e[m0 + i * kBlock] = 0u;
+    }
+    uint32_t nbits = 0;
+    while ((1u << nbits) < G) ++nbits;
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const bool go = (r.inf[i] & 0xFFu) != kNoOwner, reg = (r.inf[i] >> 16) & 1u;
+        const uint32_t own = r.inf[i] & 0xFFu;
+        const uint64_t wide = __ballot(go && !reg);
+        uint64_t same = __ballot(go);
+        for (uint32_t bit = 0; bit < nbits; ++bit) {
+            const bool on = (own >> bit) & 1u;
+            const uint64_t bm = __ballot(on);
+            same &= on ? bm : ~bm;
+        }
+        if (go) {
+            r.rank[i] = __popcll(same & lt) + __popcll(same & wide & lt);
+            if ((same & lt) == 0) wc[i * kWaves + wave][own] = __popcll(same) + __popcll(same & wide);
+        }
+    }
+}
+
+// The slots of slot_rows' messages into the budgeted segments: message i of the thread at
+// base[d] (nullable: 0) + wc[row][d] (the row's start within the owner's segment) + its rank. A
+// message that does not fit its owner's budget whole is not written (the tick is redone exactly).
+template <bool RAW>
+__device__ __forceinline__ void scatter_rows(const ShardIn& in, const SlotLayout& L, uint32_t m0,
+                                             const uint32_t (&wc)[kShardIPT * kWaves][WQ_MAX_SHARDS],
+                                             const uint32_t* base, const SlotRows& r, uint32_t* __restrict__ out,
+                                             uint32_t* __restrict__ perm) {
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < kShardIPT; ++i) {
+        const uint32_t m = m0 + i * kBlock;
+        const uint32_t d = r.inf[i] & 0xFFu;
+        if (d == kNoOwner) continue;
+        const bool reg = (r.inf[i] >> 16) & 1u;
+        const uint32_t j = (base ? base[d] : 0u) + wc[i * kWaves + wave][d] + r.rank[i];  // within the owner's segment
+        uint32_t slot;
+        uint32_t* pm;
+        uint32_t* o;
+        if (d == in.me) {  // own slots on: this shard's own message, into its own buffer
+            if (j + (reg ? 1u : 2u) > in.own_budget) continue;  // (the owner form's self segment)
+            slot = j;
+            pm = in.own_perm;
+            o = in.own_slots + (uint64_t)kSlotWords * slot;
+        } else {
+            if (j + (reg ? 1u : 2u) > L.budget[d]) continue;  // over budget: the tick is redone exactly
+            slot = L.base[d] + j;
+            pm = perm;
+            o = out + (uint64_t)kSlotWords * slot;
+        }
+        const uint32_t rp = (r.inf[i] >> 8) & 0xFFu;
+        if (reg) {
+            o[0] = r.pkl[i];
+            o[1] = r.pkh[i];
+            o[2] = r.ext[i];
+            o[3] = r.snd[i];
+            o[4] = rp | (kSlotReg << 8);
+            pm[slot] = m;
+        } else {  // a wide key (rare): head and tail slot with the coordinates, quantised again
+            int64_t kx, ky, kz;
+            msg_key<RAW>(in, m, kx, ky, kz);
+            o[0] = (uint32_t)(uint64_t)kx;
+            o[1] = (uint32_t)((uint64_t)kx >> 32);
+            o[2] = in.world[m];
+            o[3] = r.snd[i];
+            o[4] = rp | (kSlotHead << 8);
+            o[5] = (uint32_t)(uint64_t)ky;
+            o[6] = (uint32_t)((uint64_t)ky >> 32);
+            o[7] = (uint32_t)(uint64_t)kz;
+            o[8] = (uint32_t)((uint64_t)kz >> 32);
+            o[9] = kSlotTail << 8;
+            pm[slot] = m;
+            pm[slot + 1] = kNone;
+        }
+    }
+}
+
 // (b3) the stable ballot-ranked scatter of shard_scatter20_kernel into the budgeted segments; a
 // message that does not fit its owner's budget whole is not written (nor is any after it).
 template <bool RAW>
@@ -427,10 +571,8 @@ __global__ void __launch_bounds__(kBlock)
     slot_scatter_kernel(ShardIn in, const uint32_t* __restrict__ colbase, SlotLayout L, uint32_t* __restrict__ out,
                         uint32_t* __restrict__ perm) {
     __shared__ uint32_t wc[kShardIPT * kWaves][WQ_MAX_SHARDS];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t k = threadIdx.x; k < kShardIPT * kWaves * WQ_MAX_SHARDS; k += kBlock) (&wc[0][0])[k] = 0;
-    __syncthreads();
-    const uint64_t lt = (1ull << lane) - 1;
+    lds_barrier();
     if (in.a_or && blockIdx.x == 0 && threadIdx.x == 0) {  // the scan (previous launch) wrote them
         uint32_t any = 0;
         for (uint32_t d = 0; d < in.G; ++d) any |= in.a_or[2 * d + 1] & kStBudget;
@@ -438,44 +580,9 @@ __global__ void __launch_bounds__(kBlock)
             for (uint32_t d = 0; d < in.G; ++d) in.a_or[2 * d + 1] |= any;
     }
     const uint32_t m0 = blockIdx.x * kShardTile + threadIdx.x;
-    int64_t kx[kShardIPT], ky[kShardIPT], kz[kShardIPT];
-    uint64_t pk[kShardIPT];
-    uint32_t ext[kShardIPT], own[kShardIPT], rank[kShardIPT];
-    bool reg[kShardIPT], go[kShardIPT];
-    uint32_t wrd[kShardIPT], snd[kShardIPT], rpl[kShardIPT];
-    // every message's key, owner and slot words first (all loads in flight together), then the ranks
-#pragma unroll
-    for (int i = 0; i < kShardIPT; ++i) {
-        const uint32_t m = m0 + i * kBlock;
-        go[i] = m < in.M;
-        own[i] = 0xFFFFFFFFu;
-        rank[i] = 0;
-        reg[i] = true;
-        wrd[i] = snd[i] = rpl[i] = 0;
-        if (go[i]) {
-            msg_key<RAW>(in, m, kx[i], ky[i], kz[i]);
-            wrd[i] = in.world[m];
-            snd[i] = in.sender[m];
-            rpl[i] = in.repl[m];
-            own[i] = shard_of(wrd[i], kx[i], ky[i], kz[i], in.G);
-            reg[i] = pack_key(wrd[i], kx[i], ky[i], kz[i], in.sf, &pk[i], &ext[i]);
-            go[i] = own[i] != in.me || in.own_too;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < kShardIPT; ++i) {
-        const uint64_t wide = __ballot(go[i] && !reg[i]);
-        uint64_t todo = __ballot(go[i]);
-        while (todo) {
-            const int leader = __ffsll((unsigned long long)todo) - 1;
-            const uint32_t d = __shfl(own[i], leader, 64);
-            const uint64_t mask = __ballot(go[i] && own[i] == d);
-            if (go[i] && own[i] == d) rank[i] = __popcll(mask & lt) + __popcll(mask & wide & lt);
-            if (lane == leader) wc[i * kWaves + wave][d] = __popcll(mask) + __popcll(mask & wide);
-            todo &= ~mask;
-        }
-    }
-    __syncthreads();
+    SlotRows r;
+    slot_rows<RAW>(in, m0, false, wc, r);
+    lds_barrier();
     for (uint32_t d = threadIdx.x; d < in.G; d += kBlock) {
         uint32_t run = colbase[(uint64_t)d * in.nblk + blockIdx.x];
 #pragma unroll
@@ -485,50 +592,8 @@ __global__ void __launch_bounds__(kBlock)
             run += t;
         }
     }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kShardIPT; ++i) {
-        const uint32_t m = m0 + i * kBlock;
-        if (!go[i]) continue;
-        const uint32_t d = own[i];
-        const uint32_t j = wc[i * kWaves + wave][d] + rank[i];  // within the owner's segment
-        uint32_t slot;
-        uint32_t* pm;
-        uint32_t* o;
-        if (d == in.me) {  // own slots on: this shard's own message, into its own buffer
-            if (j + (reg[i] ? 1u : 2u) > in.own_budget) continue;  // (the owner form's self segment)
-            slot = j;
-            pm = in.own_perm;
-            o = in.own_slots + (uint64_t)kSlotWords * slot;
-        } else {
-            if (j + (reg[i] ? 1u : 2u) > L.budget[d]) continue;  // over budget: the tick is redone exactly
-            slot = L.base[d] + j;
-            pm = perm;
-            o = out + (uint64_t)kSlotWords * slot;
-        }
-        const uint32_t rp = rpl[i];
-        if (reg[i]) {
-            o[0] = (uint32_t)pk[i];
-            o[1] = (uint32_t)(pk[i] >> 32);
-            o[2] = ext[i];
-            o[3] = snd[i];
-            o[4] = rp | (kSlotReg << 8);
-            pm[slot] = m;
-        } else {
-            o[0] = (uint32_t)(uint64_t)kx[i];
-            o[1] = (uint32_t)((uint64_t)kx[i] >> 32);
-            o[2] = wrd[i];
-            o[3] = snd[i];
-            o[4] = rp | (kSlotHead << 8);
-            o[5] = (uint32_t)(uint64_t)ky[i];
-            o[6] = (uint32_t)((uint64_t)ky[i] >> 32);
-            o[7] = (uint32_t)(uint64_t)kz[i];
-            o[8] = (uint32_t)((uint64_t)kz[i] >> 32);
-            o[9] = kSlotTail << 8;
-            pm[slot] = m;
-            pm[slot + 1] = kNone;
-        }
-    }
+    lds_barrier();
+    scatter_rows<RAW>(in, L, m0, wc, nullptr, r, out, perm);
 }
 
 // (b1 + b2 + b3 in one pass: a budgeted tick) block b quantises its kShardTile messages and ranks
@@ -560,81 +625,9 @@ __global__ void __launch_bounds__(kBlock)
     const uint32_t b = blockIdx.x, NB = in.nblk, G = in.G;
     for (uint32_t k = threadIdx.x; k < kShardIPT * kWaves * WQ_MAX_SHARDS; k += kBlock) (&wc[0][0])[k] = 0;
     lds_barrier();
-    const uint64_t lt = (1ull << lane) - 1;
     const uint32_t m0 = b * kShardTile + threadIdx.x;
-    // per message only what the scatter writes for a regular key (a wide key's coordinates are
-    // quantised again there): few registers live across the look-back, so every block of a tick
-    // is resident at once. inf: bits 0-7 the owner (kNoOwner: no slot), 8-15 replication, 16 regular
-    constexpr uint32_t kNoOwner = 0xFFu;
-    uint32_t pkl[kShardIPT], pkh[kShardIPT], ext[kShardIPT], snd[kShardIPT], inf[kShardIPT], rank[kShardIPT];
-    // every load of the block's messages in flight before any is used (no branch between them: a
-    // lane past M reads message M - 1 and drops it), then the keys, owners and slot words
-    uint64_t raw[kShardIPT][3];
-    uint32_t wrd[kShardIPT], rpl[kShardIPT];
-#pragma unroll
-    for (int i = 0; i < kShardIPT; ++i) {
-        const uint32_t m = min(m0 + i * kBlock, in.M - 1);
-        const uint64_t* src = RAW ? reinterpret_cast<const uint64_t*>(in.keys) + 3ull * m
-                                  : reinterpret_cast<const uint64_t*>(in.pos) + 3ull * m;
-        raw[i][0] = src[0];
-        raw[i][1] = src[1];
-        raw[i][2] = src[2];
-        wrd[i] = in.world[m];
-        snd[i] = in.sender[m];
-        rpl[i] = in.repl[m];
-    }
-#pragma unroll
-    for (int i = 0; i < kShardIPT; ++i) {
-        const uint32_t m = m0 + i * kBlock;
-        inf[i] = kNoOwner;
-        rank[i] = 0;
-        pkl[i] = pkh[i] = ext[i] = 0;
-        if (m < in.M) {
-            int64_t k[3];
-            uint64_t pk = 0;
-            bool reg;
-            if (RAW) {
-                k[0] = (int64_t)raw[i][0];
-                k[1] = (int64_t)raw[i][1];
-                k[2] = (int64_t)raw[i][2];
-                reg = pack_key(wrd[i], k[0], k[1], k[2], in.sf, &pk, &ext[i]);
-            } else {
-                const double c[3] = {__longlong_as_double((long long)raw[i][0]),
-                                     __longlong_as_double((long long)raw[i][1]),
-                                     __longlong_as_double((long long)raw[i][2])};
-                reg = quantize_pack(wrd[i], c, in.sf, in.si, k, &pk, &ext[i]);
-            }
-            const uint32_t own = shard_of(wrd[i], k[0], k[1], k[2], G);
-            pkl[i] = (uint32_t)pk;
-            pkh[i] = (uint32_t)(pk >> 32);
-            if (own != in.me || in.own_too) inf[i] = own | (rpl[i] << 8) | (reg ? 1u << 16 : 0u);
-        }
-    }
-    if (in.zero_e) {
-#pragma unroll
-        for (int i = 0; i < kShardIPT; ++i)
-            if (m0 + i * kBlock < in.M) in.zero_e[m0 + i * kBlock] = 0u;
-    }
-    // ranks within the wave: the lanes of one owner found by log2(G') ballots of the owner's bits
-    // (not one ballot round per owner present)
-    uint32_t nbits = 0;
-    while ((1u << nbits) < G) ++nbits;
-#pragma unroll
-    for (int i = 0; i < kShardIPT; ++i) {
-        const bool go = (inf[i] & 0xFFu) != kNoOwner, reg = (inf[i] >> 16) & 1u;
-        const uint32_t own = inf[i] & 0xFFu;
-        const uint64_t wide = __ballot(go && !reg);
-        uint64_t same = __ballot(go);
-        for (uint32_t bit = 0; bit < nbits; ++bit) {
-            const bool on = (own >> bit) & 1u;
-            const uint64_t bm = __ballot(on);
-            same &= on ? bm : ~bm;
-        }
-        if (go) {
-            rank[i] = __popcll(same & lt) + __popcll(same & wide & lt);
-            if ((same & lt) == 0) wc[i * kWaves + wave][own] = __popcll(same) + __popcll(same & wide);
-        }
-    }
+    SlotRows r;
+    slot_rows<RAW>(in, m0, true, wc, r);
     lds_barrier();
     // the block's per-owner totals (published at once) and its rows' offsets within the block
     for (uint32_t d = threadIdx.x; d < G; d += kBlock) {
@@ -704,52 +697,7 @@ __global__ void __launch_bounds__(kBlock)
             }
         }
     }
-#pragma unroll
-    for (int i = 0; i < kShardIPT; ++i) {
-        const uint32_t m = m0 + i * kBlock;
-        const uint32_t d = inf[i] & 0xFFu;
-        if (d == kNoOwner) continue;
-        const bool reg = (inf[i] >> 16) & 1u;
-        const uint32_t j = base[d] + wc[i * kWaves + wave][d] + rank[i];  // within the owner's segment
-        uint32_t slot;
-        uint32_t* pm;
-        uint32_t* o;
-        if (d == in.me) {  // own slots on: this shard's own message, into its own buffer
-            if (j + (reg ? 1u : 2u) > in.own_budget) continue;  // (the owner form's self segment)
-            slot = j;
-            pm = in.own_perm;
-            o = in.own_slots + (uint64_t)kSlotWords * slot;
-        } else {
-            if (j + (reg ? 1u : 2u) > L.budget[d]) continue;  // over budget: the tick is redone exactly
-            slot = L.base[d] + j;
-            pm = perm;
-            o = out + (uint64_t)kSlotWords * slot;
-        }
-        const uint32_t rp = (inf[i] >> 8) & 0xFFu;
-        if (reg) {
-            o[0] = pkl[i];
-            o[1] = pkh[i];
-            o[2] = ext[i];
-            o[3] = snd[i];
-            o[4] = rp | (kSlotReg << 8);
-            pm[slot] = m;
-        } else {  // a wide key (rare): head and tail slot with the coordinates, quantised again
-            int64_t kx, ky, kz;
-            msg_key<RAW>(in, m, kx, ky, kz);
-            o[0] = (uint32_t)(uint64_t)kx;
-            o[1] = (uint32_t)((uint64_t)kx >> 32);
-            o[2] = in.world[m];
-            o[3] = snd[i];
-            o[4] = rp | (kSlotHead << 8);
-            o[5] = (uint32_t)(uint64_t)ky;
-            o[6] = (uint32_t)((uint64_t)ky >> 32);
-            o[7] = (uint32_t)(uint64_t)kz;
-            o[8] = (uint32_t)((uint64_t)kz >> 32);
-            o[9] = kSlotTail << 8;
-            pm[slot] = m;
-            pm[slot + 1] = kNone;
-        }
-    }
+    scatter_rows<RAW>(in, L, m0, wc, base, r, out, perm);
 }
 
 // (b4) the unused rest of every segment becomes tail slots (route to nobody; perm kNone), so the
