@@ -437,7 +437,7 @@ struct SlotRows {
 // tick's rows (in.zero_e).
 template <bool RAW>
 __device__ __forceinline__ void slot_rows(const ShardIn& in, uint32_t m0, bool zero,
-                                          uint32_t (&wc)[kShardIPT * kWaves][WQ_MAX_SHARDS], SlotRows& r) {
+                                          uint32_t (*wc)[WQ_MAX_SHARDS], SlotRows& r) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t lt = (1ull << lane) - 1;
     const uint32_t G = in.G;
@@ -512,7 +512,7 @@ __device__ __forceinline__ void slot_rows(const ShardIn& in, uint32_t m0, bool z
 // message that does not fit its owner's budget whole is not written (the tick is redone exactly).
 template <bool RAW>
 __device__ __forceinline__ void scatter_rows(const ShardIn& in, const SlotLayout& L, uint32_t m0,
-                                             const uint32_t (&wc)[kShardIPT * kWaves][WQ_MAX_SHARDS],
+                                             const uint32_t (*wc)[WQ_MAX_SHARDS],
                                              const uint32_t* base, const SlotRows& r, uint32_t* __restrict__ out,
                                              uint32_t* __restrict__ perm) {
     const int wave = threadIdx.x >> 6;
@@ -606,6 +606,10 @@ __global__ void __launch_bounds__(kBlock)
 // owner's true count, its budget bit; with a_or the bit of any segment in all of them);
 // slot_pad_kernel pads the segments after it. Against the three passes it saves the histogram
 // pass's second quantisation of every message and the scan's launch.
+// message tiles per grouping block: 2 halves the look-back's blocks (owner slots at G = 8: 0.1954 ->
+// 0.1930 ms, alternating); 4 (159 VGPRs, occupancy 3) was slower, 0.209 ms
+constexpr int kGroupTiles = 2;
+
 struct GroupArgs {
     uint64_t* look;  // [G * nblk] granules
     uint32_t tag;    // this launch's tag, 1 .. 2^30 - 1
@@ -619,21 +623,22 @@ struct GroupArgs {
 template <bool RAW>
 __global__ void __launch_bounds__(kBlock)
     slot_group_kernel(ShardIn in, SlotLayout L, uint32_t* __restrict__ out, uint32_t* __restrict__ perm, GroupArgs g) {
-    __shared__ uint32_t wc[kShardIPT * kWaves][WQ_MAX_SHARDS];
+    __shared__ uint32_t wc[kGroupTiles * kShardIPT * kWaves][WQ_MAX_SHARDS];
     __shared__ uint32_t bcnt[WQ_MAX_SHARDS], base[WQ_MAX_SHARDS];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t b = blockIdx.x, NB = in.nblk, G = in.G;
-    for (uint32_t k = threadIdx.x; k < kShardIPT * kWaves * WQ_MAX_SHARDS; k += kBlock) (&wc[0][0])[k] = 0;
+    for (uint32_t k = threadIdx.x; k < kGroupTiles * kShardIPT * kWaves * WQ_MAX_SHARDS; k += kBlock) (&wc[0][0])[k] = 0;
     lds_barrier();
-    const uint32_t m0 = b * kShardTile + threadIdx.x;
-    SlotRows r;
-    slot_rows<RAW>(in, m0, true, wc, r);
+    const uint32_t m0 = b * (kGroupTiles * kShardTile) + threadIdx.x;
+    SlotRows r[kGroupTiles];
+#pragma unroll
+    for (int t = 0; t < kGroupTiles; ++t) slot_rows<RAW>(in, m0 + t * kShardTile, true, wc + t * kShardIPT * kWaves, r[t]);
     lds_barrier();
     // the block's per-owner totals (published at once) and its rows' offsets within the block
     for (uint32_t d = threadIdx.x; d < G; d += kBlock) {
         uint32_t run = 0;
 #pragma unroll
-        for (int k = 0; k < kShardIPT * kWaves; ++k) {
+        for (int k = 0; k < kGroupTiles * kShardIPT * kWaves; ++k) {
             const uint32_t t = wc[k][d];
             wc[k][d] = run;
             run += t;
@@ -697,7 +702,9 @@ __global__ void __launch_bounds__(kBlock)
             }
         }
     }
-    scatter_rows<RAW>(in, L, m0, wc, base, r, out, perm);
+#pragma unroll
+    for (int t = 0; t < kGroupTiles; ++t)
+        scatter_rows<RAW>(in, L, m0 + t * kShardTile, wc + t * kShardIPT * kWaves, base, r[t], out, perm);
 }
 
 // (b4) the unused rest of every segment becomes tail slots (route to nobody; perm kNone), so the
@@ -891,6 +898,7 @@ int launch_budget_slots(wq_router* h, const double* d_pos, const int64_t* d_keys
     // (WQ_DEBUG_SLOT_3PASS: the three passes, diagnostics)
     static const bool three_pass = getenv("WQ_DEBUG_SLOT_3PASS") != nullptr;
     if (M && (phases & 3) == 3 && d_slots && !hist_ready && !three_pass) {
+        in.nblk = (uint32_t)((M + kGroupTiles * kShardTile - 1) / (kGroupTiles * kShardTile));
         const uint64_t ng = (uint64_t)G * in.nblk;
         WQ_ALLOC(h, h->shard_look, ng * 8);
         if (h->shard_look_zeroed < ng) {  // fresh granules: tag 0 never matches a launch's tag
