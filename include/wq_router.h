@@ -267,8 +267,9 @@ int wq_quantize_device(wq_router* h, const double* d_coords, size_t n, int64_t* 
  * holds every subscription a message to that cube can reach. A sharded tick is
  *   wq_shard_messages_device -> all-to-all of the records (RCCL) -> wq_route_records_device on
  *   the owner -> all-to-all of per-message counts and peers back to the ingesting GPU.
- * worldql_server_amd/sharded.py drives these over torch.distributed; the whole tick behind one
- * call is wq_sharded_route_tick_device (below). */
+ * These are the building blocks; the whole tick behind one call is wq_sharded_route_tick_device
+ * (below), over RCCL, the in-process hub, or the caller's transport (wq_shard_attach_exchange;
+ * tests/test_distributed.py and tests/test_gpu_sharded_native.py drive it over gloo). */
 #define WQ_MAX_SHARDS 64
 #define WQ_SHARD_ALL 0xFFFFFFFFu /* owner of a REMOVE_PEER op: every shard */
 
@@ -356,9 +357,12 @@ int wq_sharded_copy_out(wq_router* h, uint32_t* d_offsets, uint32_t* d_peers, ui
  * shard sees the same bits. The budgets of a tick come from the tick two calls back: each call first
  * folds in the read-back of every earlier asynchronous tick but the latest (all shards fold the same
  * ticks, so both ends of every pair agree). A tick that must run exact (the first, or after a bit
- * 64) runs synchronously, as wq_sharded_route_tick_device does. Collective: all G shards make the
- * same sequence of sharded calls. wq_sharded_copy_out does not apply to an asynchronous tick. The
- * slot form only (not wq_debug_set_shard_form's expanded form). */
+ * 64) runs synchronously, as wq_sharded_route_tick_device does. A shard whose local step fails on a
+ * budgeted tick still ends it asynchronously (its snapshot queued like every other shard's, so all
+ * shards keep folding the same ticks) and returns its error code; the others see bit 32. Collective:
+ * all G shards make the same sequence of sharded calls. wq_sharded_copy_out does not apply to an
+ * asynchronous tick. The slot form only (not wq_debug_set_shard_form's expanded form). A result that
+ * never arrives (60 s) returns WQ_E_TIMEOUT naming the tick, its ring slot and the sequence words. */
 int wq_sharded_route_tick_async(wq_router* h, const double* d_pos, const int64_t* d_keys,
                                 const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
                                 size_t n_msgs, uint32_t* d_offsets, uint32_t* d_peers, uint32_t* d_msgs,
@@ -438,7 +442,8 @@ int wq_sharded_route_owner_slots(wq_router* h, const double* d_pos, const int64_
  * are not valid and the next call runs exact; overflow: the handle's pair buffer was short, the
  * outputs are truncated and the buffer grows for the tick after next). A tick that must run exact
  * (the first, one after a short budget, one after the slot tick) runs synchronously and fills
- * n_pairs. The view's arrays are rewritten by the next tick on the handle's stream. */
+ * n_pairs. A local failure on a budgeted tick ends it asynchronously all the same and returns the
+ * error. The view's arrays are rewritten by the next tick on the handle's stream. */
 int wq_sharded_route_owner_slots_async(wq_router* h, const double* d_pos, const int64_t* d_keys,
                                        const uint32_t* d_world, const uint32_t* d_sender, const uint8_t* d_repl,
                                        size_t n_msgs, wq_route_counters* d_counters, wq_owner_slot_view* out);

@@ -5,7 +5,8 @@
 //   (1) shard_messages: quantise each ingested message (kernel 1), compute its owner, and group
 //       the messages by owner into 40-byte records, stable in message order (three launches:
 //       per-block owner histograms -> one flat scan -> ballot-ranked scatter);
-//   (2) an RCCL all-to-all of the records (host side: worldql_server_amd/sharded.py);
+//   (2) an all-to-all of the records (wq_sharded.hip's exchange: RCCL, the hub, or the caller's
+//       transport through wq_shard_attach_exchange);
 //   (3) route_records: the single-GPU route (count / scan / emit) on the received records —
 //       keys are already quantised, so the count pass takes its raw-key branch;
 //   (4) the pairs return to the ingesting GPU with a second all-to-all.

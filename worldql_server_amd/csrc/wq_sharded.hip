@@ -1333,8 +1333,19 @@ static int async_drain(wq_router* h, uint32_t keep) {
             reinterpret_cast<const volatile uint64_t*>(static_cast<const char*>(sc.asnap[k]) + kSmallBytes);
         const auto t0 = std::chrono::steady_clock::now();
         while (*seq != sc.aseq[k]) {
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
-                return set_error(h, WQ_E_TIMEOUT, "asynchronous sharded tick: its result never arrived");
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+                // name everything a post-mortem needs: which tick, which ring slot, what the word holds,
+                // and whether the stream still had work (idle + wrong word = the snapshot was never written)
+                const hipError_t q = hipStreamQuery(h->stream);
+                char msg[320];
+                snprintf(msg, sizeof msg,
+                         "asynchronous sharded tick: its result never arrived (tick %llu of this handle, ring slot %u "
+                         "of %u, %u in flight; sequence word expected %llu, observed %llu; stream %s)",
+                         (unsigned long long)sc.aseq[k], k, ShardCtx::kRing, sc.acount, (unsigned long long)sc.aseq[k],
+                         (unsigned long long)*seq,
+                         q == hipSuccess ? "idle" : q == hipErrorNotReady ? "busy" : hipGetErrorString(q));
+                return set_error(h, WQ_E_TIMEOUT, msg);
+            }
             std::this_thread::yield();
         }
         std::atomic_thread_fence(std::memory_order_acquire);
@@ -1788,11 +1799,13 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
         sc.last_radius = radius;
         sc.last_gen = h->table_gen;
     }
-    // ---- asynchronous end (wq_sharded_route_tick_async, a budgeted tick without a local failure):
-    // no host read; the small vectors go to a pinned snapshot the next calls fold in (budgets), P and
-    // the statuses to the caller's counters and the health words — at the end of the tile scan when
-    // one block runs it, else by k_async_result ----
-    const bool async_end = async && !exact && !late;
+    // ---- asynchronous end (wq_sharded_route_tick_async, a budgeted tick): no host read; the small
+    // vectors go to a pinned snapshot the next calls fold in (budgets), P and the statuses to the
+    // caller's counters and the health words — at the end of the tile scan when one block runs it,
+    // else by k_async_result. A shard whose local step failed takes this end too (and then returns its
+    // error): whether a tick is queued in the snapshot ring must be decided by state every shard
+    // shares, or the shards would fold different ticks and size their next exchanges differently ----
+    const bool async_end = async && !exact;
     AsyncResultParams ar{};
     const uint32_t ak = (sc.ahead + sc.acount) % ShardCtx::kRing;  // async_drain left a free slot
     if (async_end) {
@@ -1824,6 +1837,11 @@ static int slot_tick(wq_router* h, const double* d_pos, const int64_t* d_keys, c
         sc.small_zeroed = true;
         sc.last_ready = false;  // no copy-out of an unread tick (its P is on the device)
         *n_pairs = 0;
+        if (late) {  // st_host (the status copies' source) lives on this frame: let them finish first
+            WQ_HIP(h, hipStreamSynchronize(s));
+            h->err = late_msg;
+            return late;
+        }
         return WQ_OK;
     }
 
@@ -2088,11 +2106,12 @@ static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_k
             out->send_seg[d] = sb.b[d];
         }
     };
-    // ---- asynchronous end (a budgeted tick without a local failure): as the slot tick's — the
-    // small vectors to a pinned snapshot folded in two calls later, P and the statuses to the
-    // caller's counters and the health words; a pair buffer that was short shows as overflow ----
-    if (async_end && !late) {
-        if (!Rb) WQ_HIP(h, hipMemsetAsync(sc.own_off.p, 0, 4, s));
+    // ---- asynchronous end (a budgeted tick): as the slot tick's — the small vectors to a pinned
+    // snapshot folded in two calls later, P and the statuses to the caller's counters and the health
+    // words; a pair buffer that was short shows as overflow. A shard whose local step failed takes
+    // it too, then returns its error (every shard queues the same ticks: ADVICE r5) ----
+    if (async_end) {
+        if (!Rb && !late) WQ_HIP(h, hipMemsetAsync(sc.own_off.p, 0, 4, s));
         if (!ar_done) {
             hipLaunchKernelGGL(k_async_result, dim3(1), dim3(256), 0, s, ar);
             WQ_HIP(h, hipGetLastError());
@@ -2101,6 +2120,11 @@ static int owner_slot_tick(wq_router* h, const double* d_pos, const int64_t* d_k
         sc.n_async++;
         sc.aseq[ak] = sc.n_async;
         sc.small_zeroed = true;
+        if (late) {  // st_host (the status copies' source) lives on this frame: let them finish first
+            WQ_HIP(h, hipStreamSynchronize(s));
+            h->err = late_msg;
+            return late;
+        }
         fill_view(~0ull);  // P: in the caller's counters
         return WQ_OK;
     }
