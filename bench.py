@@ -156,6 +156,26 @@ def cube_workload(rank: int, world_size: int, scale: float = 1.0):
     return w, lo, hi
 
 
+def sysfs_clocks() -> dict:
+    """The current DPM levels the amdgpu driver reports (pp_dpm_sclk / pp_dpm_mclk, the line marked
+    '*') of every card the box exposes; best effort (empty when sysfs is not readable)."""
+    import glob
+    out = {}
+    for kind in ("sclk", "mclk", "fclk"):
+        vals = set()
+        for f in sorted(glob.glob(f"/sys/class/drm/card*/device/pp_dpm_{kind}")):
+            try:
+                with open(f) as fh:
+                    for ln in fh:
+                        if ln.rstrip().endswith("*"):
+                            vals.add(ln.split(":", 1)[-1].strip().rstrip("*").strip())
+            except OSError:
+                pass
+        if vals:
+            out[f"dpm_{kind}"] = sorted(vals)
+    return out
+
+
 def allreduce(vals, op: str, dev, world_size: int) -> list:
     """All-reduce a few float64 values over the ranks ("max" or "sum"). RCCL takes device tensors;
     gloo (the one-GPU rehearsal) takes host tensors — a device tensor handed to gloo is read by its

@@ -214,10 +214,14 @@ def run_c3(a, rank, world_size, local_rank, dev):
     P, F = int(c["n_pairs"]), int(c["n_candidates"])
     assert c["overflow"] == 0 and c["error"] == 0, c
     t_ms = timed_ticks(lambda: r.route_device(*args, 0), a.steps, stream, dev, 1, [r])
+    # the GPU's shader clock right after the timed region (the box-to-box spread of the headline is
+    # partly clock: VERDICT r5 Weak #5), then one event-bracketed launch per tick with events between
+    # its kernels, so the line says which kernel moved
+    sclk_mhz = r.probe_sclk()
     r.profile_enable(True)
     for _ in range(a.steps):
         r.route_device(*args, 0)
-    k_ms, launches = r.profile_read()
+    k_ms, launches, ph_ms, n_ph = r.profile_read_phases()
     r.profile_enable(False)
     k_avg_s = k_ms / launches / 1e3
     B = algorithmic_bytes(M, F, P)
@@ -232,6 +236,15 @@ def run_c3(a, rank, world_size, local_rank, dev):
                  "parallelism": "1 GPU", "table_build_s": round(build_s, 3), "generate_s": round(gen_s, 1)},
                 roofline(B, t_ms / a.steps / 1e3, kernel, _pmc_traffic(PMC_C3, M, P), k_avg_s * 1e6),
                 "synthetic (splitmix64, SURVEY.md §8(d) C3 generator)")
+    if n_ph:
+        us = [x / n_ph * 1e3 for x in ph_ms]
+        # per kernel: its own §8(d) share — count 69M (inputs + bucket record), emit 4F + 8P + 4(M+1)
+        out["roofline"]["kernel_phases_us"] = {"count": round(us[0], 1), "tile_scan": round(us[1], 1),
+                                               "emit": round(us[2], 1)}
+        out["roofline"]["kernel_phase_frac"] = {
+            "count": 69 * M / (us[0] * 1e-6) / 1e9 / HBM_PEAK_GBS,
+            "emit": (4 * F + 8 * P + 4 * (M + 1)) / (us[2] * 1e-6) / 1e9 / HBM_PEAK_GBS}
+    out["clocks"] = {"sclk_mhz_after_timed_region": round(sclk_mhz, 1), **bench.sysfs_clocks()}
     # SURVEY.md §8(b)'s output contract proper: CSR offsets[M+1] + peers[P], msgs = NULL (no per-pair
     # message index: the caller hands message m its slice peers[offsets[m] .. offsets[m+1]) as
     # broadcast_to does). Same tick, same inputs; its peers are checked equal to the full form's.

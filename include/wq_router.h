@@ -473,6 +473,13 @@ int wq_route_health(wq_router* h, uint32_t* error_bits, uint32_t* overflow);
  * wq_profile_read returns the summed kernel-only milliseconds and launch count (and resets). */
 int wq_profile_enable(wq_router* h, int enable);
 int wq_profile_read(wq_router* h, double* kernel_ms, uint64_t* launches);
+/* The same, plus per-kernel time of the launches that ran the three-launch shape (count / tile scan /
+ * emit: events between the kernels): phase_ms[0..2] summed over those `phased` launches. */
+int wq_profile_read_phases(wq_router* h, double* kernel_ms, uint64_t* launches, double* phase_ms,
+                           uint64_t* phased);
+/* The shader clock in MHz right now (a short all-CU spin: s_memtime cycles over s_memrealtime wall
+ * time), so a bench line can say what clock its timed region ran at. Synchronises the stream. */
+int wq_probe_sclk(wq_router* h, double* mhz);
 
 /* ---- test hook: keep only the low `bits` bits of the 64-bit cube hash (64 = normal).
  * Forces bucket collisions so the exact-compare fallback paths are exercised. */

@@ -57,7 +57,7 @@ def main():
         r.lib.wq_quantize_device(r.h, pos.data_ptr(), 3 * M, keys.data_ptr())
     torch.cuda.synchronize()
     ref = None
-    res = {}
+    res, phases = {}, {}
     cfgs = [int(c) for c in a.cfgs.split(",")]
     for rnd in range(a.rounds):
         for cfg in cfgs:
@@ -78,10 +78,13 @@ def main():
             r.profile_enable(True)
             for _ in range(a.steps):
                 r.route_device(*args, **kw)
-            ms, n = r.profile_read()
+            ms, n, ph, nph = r.profile_read_phases()
             r.profile_enable(False)
             res.setdefault(cfg, []).append(ms / n * 1e3)
-    print(json.dumps({"M": M, "P": P, "us_per_launch": {k: [round(x, 2) for x in v] for k, v in res.items()}}))
+            if nph:
+                phases.setdefault(cfg, []).append([round(x / nph * 1e3, 1) for x in ph])
+    print(json.dumps({"M": M, "P": P, "us_per_launch": {k: [round(x, 2) for x in v] for k, v in res.items()},
+                      "count_scan_emit_us": phases, "sclk_mhz": round(r.probe_sclk(), 1)}))
 
 
 if __name__ == "__main__":

@@ -122,6 +122,10 @@ struct RouteWs {
 
 struct ProfileEvents {
     std::vector<hipEvent_t> start, stop;
+    // the three-launch shape (count / tile scan / emit) also records an event after the count and
+    // one after the scan, so wq_profile_read_phases can split a launch's time per kernel
+    std::vector<hipEvent_t> mid1, mid2;
+    std::vector<char> phased;
     size_t used = 0;
     bool enabled = false;
 };

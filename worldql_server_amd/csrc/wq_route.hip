@@ -145,12 +145,18 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     ProfileEvents& pr = h->prof;
     if (pr.enabled) {
         if (pr.used == pr.start.size()) {
-            hipEvent_t a, b;
+            hipEvent_t a, b, c, d;
             WQ_HIP(h, hipEventCreate(&a));
             WQ_HIP(h, hipEventCreate(&b));
+            WQ_HIP(h, hipEventCreate(&c));
+            WQ_HIP(h, hipEventCreate(&d));
             pr.start.push_back(a);
             pr.stop.push_back(b);
+            pr.mid1.push_back(c);
+            pr.mid2.push_back(d);
+            pr.phased.push_back(0);
         }
+        pr.phased[pr.used] = 0;
         WQ_HIP(h, hipEventRecord(pr.start[pr.used], s));
     }
     const RouteIn in{d_pos, d_keys, d_world, d_sender, d_repl, (uint32_t)M, (int64_t)h->cube_size};
@@ -363,6 +369,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         cfg.count(cp, s, (n_count + tpb - 1) / tpb);
     }
     WQ_HIP(h, hipGetLastError());
+    if (pr.enabled) WQ_HIP(h, hipEventRecord(pr.mid1[pr.used], s));
 
     TileScanParams sp;
     sp.tile_total = tile_total;
@@ -376,6 +383,10 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     sp.health = route_health(h);
     sp.stale = tv.stale;
     if (int rc = launch_tile_scan(h, sp)) return rc;
+    if (pr.enabled) {
+        WQ_HIP(h, hipEventRecord(pr.mid2[pr.used], s));
+        pr.phased[pr.used] = 1;
+    }
 
     EmitParams ep;
     ep.sender = d_sender;

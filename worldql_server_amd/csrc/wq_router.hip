@@ -132,8 +132,8 @@ int wq_router_destroy(wq_router* h) {
     (void)hipSetDevice(h->device);
     (void)hipStreamSynchronize(h->stream);
     shard_release(h);
-    for (auto e : h->prof.start) (void)hipEventDestroy(e);
-    for (auto e : h->prof.stop) (void)hipEventDestroy(e);
+    for (auto* v : {&h->prof.start, &h->prof.stop, &h->prof.mid1, &h->prof.mid2})
+        for (auto e : *v) (void)hipEventDestroy(e);
     DevBuf* bufs[] = {&h->st.h, &h->st.w, &h->st.kx, &h->st.ky, &h->st.kz, &h->st.p,
                       &h->st_next.h, &h->st_next.w, &h->st_next.kx, &h->st_next.ky, &h->st_next.kz,
                       &h->st_next.p, &h->tab.slots, &h->tab.claim, &h->tab.list, &h->tab.any,
@@ -752,6 +752,69 @@ int wq_profile_read(wq_router* h, double* kernel_ms, uint64_t* launches) {
     *kernel_ms = total;
     *launches = h->prof.used;
     h->prof.used = 0;
+    return WQ_OK;
+}
+
+int wq_profile_read_phases(wq_router* h, double* kernel_ms, uint64_t* launches, double* phase_ms,
+                           uint64_t* phased) {
+    if (!h || !kernel_ms || !launches || !phase_ms || !phased) return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    ProfileEvents& pr = h->prof;
+    double ph[3] = {0.0, 0.0, 0.0};
+    uint64_t np = 0;
+    for (size_t i = 0; i < pr.used; ++i) {
+        if (!pr.phased[i]) continue;
+        WQ_HIP(h, hipEventSynchronize(pr.stop[i]));
+        const hipEvent_t ev[4] = {pr.start[i], pr.mid1[i], pr.mid2[i], pr.stop[i]};
+        for (int k = 0; k < 3; ++k) {
+            float ms = 0.0f;
+            WQ_HIP(h, hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+            ph[k] += ms;
+        }
+        ++np;
+    }
+    for (int k = 0; k < 3; ++k) phase_ms[k] = ph[k];
+    *phased = np;
+    return wq_profile_read(h, kernel_ms, launches);
+}
+
+// The shader clock the GPU runs at right now: every workgroup spins on dependent VALU work between
+// two reads of the shader-clock counter (s_memtime) and of the constant-rate wall clock
+// (s_memrealtime, hipDeviceAttributeWallClockRate); cycles / wall time per workgroup, median.
+static __global__ __launch_bounds__(256) void k_sclk_probe(uint64_t* out, uint32_t iters) {
+    const uint64_t c0 = clock64(), w0 = wall_clock64();
+    float x = (float)threadIdx.x;
+    for (uint32_t i = 0; i < iters; ++i) x = __builtin_fmaf(x, 0.9999999f, 1e-7f);
+    const uint64_t c1 = clock64(), w1 = wall_clock64();
+    if (threadIdx.x == 0) {
+        out[2 * blockIdx.x] = c1 - c0;
+        out[2 * blockIdx.x + 1] = w1 - w0;
+    }
+    if (x == -1.0f) out[0] = 0;  // keeps the loop
+}
+
+int wq_probe_sclk(wq_router* h, double* mhz) {
+    if (!h || !mhz) return WQ_E_INVALID;
+    WQ_HIP(h, hipSetDevice(h->device));
+    int rate_khz = 0;
+    WQ_HIP(h, hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, h->device));
+    if (rate_khz <= 0) return set_error(h, WQ_E_HIP, "no wall clock rate");
+    constexpr unsigned kBlocks = 1024;
+    uint64_t* d = nullptr;
+    WQ_HIP(h, hipMalloc(&d, kBlocks * 16));
+    hipLaunchKernelGGL(k_sclk_probe, dim3(kBlocks), dim3(256), 0, h->stream, d, 200000u);
+    std::vector<uint64_t> v(2 * kBlocks);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(v.data(), d, kBlocks * 16, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return set_error(h, WQ_E_HIP, "sclk probe", e);
+    std::vector<double> f;
+    for (unsigned b = 0; b < kBlocks; ++b)
+        if (v[2 * b + 1]) f.push_back((double)v[2 * b] / (double)v[2 * b + 1] * rate_khz / 1e3);
+    if (f.empty()) return set_error(h, WQ_E_HIP, "sclk probe: no wall-clock ticks");
+    std::nth_element(f.begin(), f.begin() + f.size() / 2, f.end());
+    *mhz = f[f.size() / 2];
     return WQ_OK;
 }
 

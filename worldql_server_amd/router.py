@@ -79,6 +79,9 @@ def load_library(build_if_missing: bool = True):
         "wq_quantize_device": ([vp, vp, sz, vp], i32),
         "wq_profile_enable": ([vp, i32], i32),
         "wq_profile_read": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)], i32),
+        "wq_profile_read_phases": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64),
+                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)], i32),
+        "wq_probe_sclk": ([vp, ctypes.POINTER(ctypes.c_double)], i32),
         "wq_debug_set_hash_bits": ([vp, i32], i32),
         "wq_debug_set_record_slack": ([vp, u32], i32),
         "wq_debug_set_route_config": ([vp, i32], i32),
@@ -566,6 +569,20 @@ class Router:
         n = ctypes.c_uint64()
         self._check(self.lib.wq_profile_read(self.h, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
+
+    def profile_read_phases(self):
+        """(kernel ms, launches, [count, tile_scan, emit] ms summed over the three-launch launches, their
+        number) — wq_profile_read_phases; resets like profile_read."""
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        ph, npz = (ctypes.c_double * 3)(), ctypes.c_uint64()
+        self._check(self.lib.wq_profile_read_phases(self.h, ctypes.byref(ms), ctypes.byref(n), ph, ctypes.byref(npz)))
+        return ms.value, n.value, list(ph), npz.value
+
+    def probe_sclk(self) -> float:
+        """The shader clock in MHz right now (wq_probe_sclk)."""
+        mhz = ctypes.c_double()
+        self._check(self.lib.wq_probe_sclk(self.h, ctypes.byref(mhz)))
+        return mhz.value
 
 
 class Hub:
