@@ -340,7 +340,7 @@ def _c3_slice(w, rank, world_size, dev):
 
 def _c3_replicated(a, w, rank, world_size, local_rank, dev, stream, sl):
     """The replicated-table form (wq_router_create_multi_mode's WQ_MULTI_REPLICATE, one process per
-    GPU): every rank holds the WHOLE table (C3: ~10 GB of 288 GB; every op applied on every GPU) and
+    GPU): every rank holds the WHOLE table (C3: ~25 GB of 288 GB; every op applied on every GPU) and
     routes its own M/N messages with the single-GPU tick — no exchange at all."""
     import torch
     from worldql_server_amd.router import Router
@@ -510,7 +510,7 @@ def _run_c3_multi(a, w, rank, world_size, local_rank, dev, gen_s):
     """C3 over N GPUs, strong scaling (the 10M messages of a tick split over the ranks), both
     multi-GPU forms measured in the same run on the same slices:
       replicate   every GPU holds the whole table and routes its slice — the headline (DESIGN.md §6:
-                  C3's table is ~10 GB of 288 GB, so the exchange the cube-hash form needs buys
+                  C3's table is ~25 GB of 288 GB, so the exchange the cube-hash form needs buys
                   nothing at this size; value = all ranks' pairs / the max-over-ranks time)
       cube        the cube-hash sharded tick over RCCL (the form for tables beyond one GPU's HBM),
                   under extra.cube_hash (--shard cube: the headline instead)

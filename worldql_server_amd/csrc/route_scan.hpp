@@ -5,6 +5,7 @@
 // counters. The emit pass turns tile_prefix + a block-local scan into every CSR offset, so no
 // 1M-element global scan and no inter-block look-back is needed anywhere in the tick.
 #pragma once
+#include <cstdlib>
 #include <cstring>  // rocPRIM's host code needs memset declared first
 
 #include <rocprim/rocprim.hpp>
@@ -163,6 +164,148 @@ static __global__ __launch_bounds__(kBlock) void tile_finish_kernel(TileScanPara
     }
 }
 
+// Many tiles in ONE launch: block b scans tiles [4096 b, 4096 b + 4096) (16 consecutive per thread,
+// 16-byte loads), publishes its exact {E, F} aggregates as tagged granules, sums every lower block's
+// aggregates itself (blocks wait only on lower, already dispatched blocks; C3's 39,063 tiles are 10
+// blocks) and writes its prefixes; the last block writes P, F and the flags. It replaces rocPRIM's
+// look-back scan + tile_finish_kernel (init, scan and finish: three launches, ~18 us on C3).
+constexpr int kMScanThreads = 256;
+constexpr int kMScanPer = 16;
+constexpr uint32_t kMScanTile = kMScanThreads * kMScanPer;
+constexpr uint32_t kSGranTagBits = 24;
+constexpr uint32_t kSpinLimitScan = 1u << 21;  // x s_sleep(2) ~ 0.1 s (route_tick.hpp's bound)
+constexpr uint32_t kErrSpinScan = 4u;          // error bit 4: a bounded spin gave up (WQ_E_TIMEOUT)
+
+__device__ __forceinline__ uint64_t sgranule(uint32_t tag, uint64_t v) {
+    return ((uint64_t)tag << (64 - kSGranTagBits)) | (v & ((1ull << (64 - kSGranTagBits)) - 1ull));
+}
+
+static __global__ __launch_bounds__(kMScanThreads) void tile_scan_multi_kernel(TileScanParams p, uint64_t* gran,
+                                                                                uint32_t tag) {
+    constexpr int NW = kMScanThreads / 64;
+    __shared__ uint32_t s_wave[NW];
+    __shared__ uint64_t s_e[NW], s_f[NW], s_pe[NW], s_pf[NW];
+    __shared__ uint32_t s_gave;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t b = blockIdx.x, n = p.n_tiles;
+    const uint32_t t0 = b * kMScanTile + (uint32_t)tid * kMScanPer;
+    uint32_t v[kMScanPer];
+    uint64_t f = 0;
+    if (t0 + kMScanPer <= n) {  // 64-byte aligned runs (t0 is a multiple of 16 tiles)
+        const uint4* tv = reinterpret_cast<const uint4*>(p.tile_total + t0);
+        const uint4* fv = reinterpret_cast<const uint4*>(p.tile_F + t0);
+        uint4 a[kMScanPer / 4], c[kMScanPer / 4];
+#pragma unroll
+        for (int k = 0; k < kMScanPer / 4; ++k) {
+            a[k] = tv[k];
+            c[k] = fv[k];
+        }
+#pragma unroll
+        for (int k = 0; k < kMScanPer / 4; ++k) {
+            v[4 * k] = a[k].x;
+            v[4 * k + 1] = a[k].y;
+            v[4 * k + 2] = a[k].z;
+            v[4 * k + 3] = a[k].w;
+            f += (uint64_t)c[k].x + c[k].y + c[k].z + c[k].w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kMScanPer; ++k) {
+            const bool in = t0 + k < n;
+            v[k] = in ? p.tile_total[t0 + k] : 0u;
+            f += in ? p.tile_F[t0 + k] : 0u;
+        }
+    }
+    uint32_t run = 0;
+    uint64_t esum = 0;
+#pragma unroll
+    for (int k = 0; k < kMScanPer; ++k) {
+        const uint32_t x = v[k];
+        v[k] = run;  // exclusive within the thread (u32, wrapping like the CSR offsets)
+        run += x;
+        esum += x;
+    }
+    const uint32_t incl = wave_incl_scan_u32_dpp(run);
+    const uint64_t we = wave_sum_u64(esum), wf = wave_sum_u64(f);
+    if (lane == 63) s_wave[wave] = incl;
+    if (lane == 0) {
+        s_e[wave] = we;
+        s_f[wave] = wf;
+    }
+    if (tid == 0) s_gave = 0;
+    __syncthreads();
+    uint32_t before = incl - run;
+    uint64_t E = 0, F = 0;
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+        if (u < wave) before += s_wave[u];
+        E += s_e[u];
+        F += s_f[u];
+    }
+    if (tid == 0) {  // this block's aggregates, for the blocks above it
+        __hip_atomic_store(gran + 2 * b, sgranule(tag, E), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gran + 2 * b + 1, sgranule(tag, F), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the lower blocks' aggregates: thread j polls block j (and j + 256, ...)
+    uint64_t pe = 0, pf = 0;
+    bool gave = false;
+    for (uint32_t j = tid; j < b; j += kMScanThreads) {
+        for (int h = 0; h < 2; ++h) {
+            const uint64_t* g = gran + 2 * j + h;
+            uint64_t x = 0;
+            for (uint32_t it = 0;; ++it) {
+                x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)(x >> (64 - kSGranTagBits)) == tag) break;
+                if (it >= kSpinLimitScan) {
+                    gave = true;
+                    x = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            const uint64_t val = x & ((1ull << (64 - kSGranTagBits)) - 1ull);
+            if (h == 0) pe += val;
+            else pf += val;
+        }
+    }
+    pe = wave_sum_u64(pe);
+    pf = wave_sum_u64(pf);
+    if (lane == 0) {
+        s_pe[wave] = pe;
+        s_pf[wave] = pf;
+    }
+    if (gave) s_gave = 1;
+    __syncthreads();
+    uint64_t PE = 0, PF = 0;
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+        PE += s_pe[u];
+        PF += s_pf[u];
+    }
+    const uint32_t base = (uint32_t)PE + before;
+    if (t0 + kMScanPer <= n) {
+        uint4* o = reinterpret_cast<uint4*>(p.tile_prefix + t0);
+#pragma unroll
+        for (int k = 0; k < kMScanPer / 4; ++k)
+            o[k] = make_uint4(base + v[4 * k], base + v[4 * k + 1], base + v[4 * k + 2], base + v[4 * k + 3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < kMScanPer; ++k)
+            if (t0 + k < n) p.tile_prefix[t0 + k] = base + v[k];
+    }
+    if (tid == 0) {
+        if (s_gave) flag_route(p.cnt, p.health, kErrSpinScan, 0u);
+        if (b == gridDim.x - 1) {
+            const uint64_t P = PE + E;
+            p.cnt->n_candidates = PF + F;
+            p.offsets[p.M] = (uint32_t)P;
+            p.cnt->n_pairs = P;
+            flag_route(p.cnt, p.health, P > 0xFFFFFFFFull ? 2u : 0u, P > p.capacity ? 1u : 0u);
+            if (p.stale && *p.stale) flag_route(p.cnt, p.health, kErrStale, 0u);
+        }
+    }
+}
+
 constexpr uint32_t kScanOneBlockMax = 8192;  // tiles: up to here the one-block scan is the faster
 
 // The tick's tile scan (n_tiles >= 1): one block for a few thousand tiles (C2: 3,907),
@@ -172,10 +315,29 @@ constexpr uint32_t kScanOneBlockMax = 8192;  // tiles: up to here the one-block 
 inline int launch_tile_scan(wq_router* h, const TileScanParams& sp, bool* async_done = nullptr) {
     hipStream_t s = h->stream;
     if (async_done) *async_done = false;
-    if (sp.n_tiles <= kScanOneBlockMax) {
+    // the one-block scan up to kScanOneBlockMax tiles (always when it takes an asynchronous tick's
+    // end); WQ_SCAN_MULTI_MIN moves the threshold down for the multi-block scan (tuning)
+    static const uint32_t multi_min =
+        getenv("WQ_SCAN_MULTI_MIN") ? (uint32_t)strtoul(getenv("WQ_SCAN_MULTI_MIN"), nullptr, 10) : kScanOneBlockMax + 1;
+    if (sp.n_tiles <= kScanOneBlockMax && (sp.async_end || sp.n_tiles < multi_min)) {
         hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, sp);
         WQ_HIP(h, hipGetLastError());
         if (async_done) *async_done = sp.async_end;
+        return WQ_OK;
+    }
+    // WQ_SCAN_MULTI=0: rocPRIM's look-back scan + tile_finish_kernel (the round-5 path, for A/B)
+    static const bool multi = !getenv("WQ_SCAN_MULTI") || atoi(getenv("WQ_SCAN_MULTI")) != 0;
+    if (multi) {
+        RouteWs& rw = h->rws;
+        const uint32_t nb = (sp.n_tiles + kMScanTile - 1) / kMScanTile;
+        WQ_ALLOC(h, rw.sgran, (uint64_t)nb * 16);
+        if (rw.sgran_zeroed < 2ull * nb) {  // fresh granules: tag 0 never matches
+            WQ_HIP(h, hipMemsetAsync(rw.sgran.p, 0, rw.sgran.bytes, s));
+            rw.sgran_zeroed = rw.sgran.bytes / 8;
+        }
+        const uint32_t tag = (uint32_t)(rw.scan_calls++ % ((1ull << kSGranTagBits) - 1)) + 1u;
+        hipLaunchKernelGGL(tile_scan_multi_kernel, dim3(nb), dim3(kMScanThreads), 0, s, sp, rw.sgran.as<uint64_t>(), tag);
+        WQ_HIP(h, hipGetLastError());
         return WQ_OK;
     }
     size_t bytes = 0;

@@ -107,7 +107,10 @@ struct RouteWs {
     DevBuf tiles;  // u32[2 * n_count_blocks]: block totals, then their exclusive prefix
     DevBuf spill;  // per-block output images of the count+spill tick (route config 7)
     DevBuf agg;    // u64[2 * blocks]: look-back and candidate granules of the single-launch tick
-    DevBuf scan_tmp;  // rocPRIM temporary storage of the many-tile scan (launch_tile_scan)
+    DevBuf scan_tmp;  // rocPRIM temporary storage of the many-tile scan (WQ_SCAN_MULTI=0)
+    DevBuf sgran;     // u64[2 * blocks]: the multi-block tile scan's tagged block aggregates {E, F}
+    uint64_t sgran_zeroed = 0;  // granules zeroed so far (a fresh one never matches a tag)
+    uint64_t scan_calls = 0;    // multi-block scans so far (their tags)
     uint64_t agg_zeroed = 0;
     uint64_t* stamps = nullptr;  // wq_debug_set_timeline
     // the pipelined heavy tick (wq_route.hip, short ticks): count chunks on `side` while the launch
