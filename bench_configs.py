@@ -31,8 +31,9 @@ import numpy as np
 import bench
 from bench import HBM_PEAK_GBS, METRIC, algorithmic_bytes, reduce_over_ranks, roofline, timed_ticks
 
-PMC_C3 = "r04_pmc_route_c3_hdr.json"  # rocprofv3 --pmc summary of the C3 tick, dense headers on (the
-                                       # default; tools/pmc_route.sh; x2 calibrated: r04_fetch_calibration.json)
+PMC_C3 = "r06_pmc_route_c3.json"  # rocprofv3 --pmc summary of the C3 tick on the round-6 build (dense headers,
+                                   # aligned lists; tools/pmc_route.sh 10 --workload c3; x2 calibrated:
+                                   # r04_fetch_calibration.json)
 
 
 def run(a, rank, world_size, local_rank, dev):

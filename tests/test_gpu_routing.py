@@ -450,3 +450,81 @@ def test_pipelined_heavy_tick_is_identical(chunks):
         assert a[3:] == b[3:] and a[3] == P, (a[3:], b[3:])
         assert (a[0] == b[0]).all() and (a[1] == b[1]).all() and (a[2] == b[2]).all()
     assert got[(1, P // 3)][5] == 1  # the short capacity is reported, the kept prefix identical
+
+
+@pytest.mark.parametrize("n_tiles", [2047, 2048, 4096, 4097, 8192 + 17])
+def test_multi_block_tile_scan_boundaries(n_tiles):
+    """Round 6: the count / scan / emit shape scans its per-256-message tile totals with the one-launch
+    multi-block scan from 2,048 tiles on (4,096 tiles per block, 16 per thread): tile counts at and
+    across its thresholds, its block boundary and its 16-tile vector tail, on C2-shaped input with
+    mixed replication — the oracle's CSR and msgs, and P / F in the device counters."""
+    w = synth.config_c2(repl_mode="mixed", scale=2.2)
+    M = n_tiles * 256 - 37
+    assert M <= len(w.world)
+    r = mk_router(16)
+    r.apply_ops(w.ops)
+    o = orc.COracle(16)
+    o.apply_ops(w.ops)
+    r.set_route_config(10)  # count / tile_scan / emit
+    _compare(r, o, w.pos[:M], w.world[:M], w.sender[:M], w.repl[:M])
+    r.set_route_config(0)
+
+
+@pytest.mark.parametrize("hash_bits", [64, 6, 1])
+def test_compact_headers_heavy_shape_vs_oracle(hash_bits):
+    """Round 6: the count pass probes the compact header table (load <= 1/2, its own probe runs, the
+    record slot carried in the header). Heavy-fan-out messages through count / scan / emit: scaled C3
+    hotspots, or (6 / 1 hash bits: every cube in one probe run of both tables) 40 cubes of 60 peers;
+    then a churn batch (the headers go stale and the count probes the records) — against the oracle."""
+    from worldql_server_amd import synth_ext
+    if hash_bits == 64:
+        w = synth_ext.config_c3(scale=0.01)
+        ops, args = w.ops, (w.pos, w.world, w.sender, w.repl)
+    else:
+        n_cubes, per_cube = 40, 60
+        cx = np.repeat(np.arange(n_cubes) * 16.0 + 8.0, per_cube)
+        pos = np.stack([cx, np.full_like(cx, 8.0), np.full_like(cx, -8.0)], 1)
+        ops = abi.ops_array(np.zeros(len(cx), np.uint32), np.arange(len(cx), dtype=np.uint32),
+                            np.zeros(len(cx), np.uint8), pos=pos)
+        rng = synth.SplitMix64(79)
+        M = 20000
+        mpos = np.stack([rng.below(n_cubes + 3, M) * 16.0 + rng.uniform(0.5, 15.5, M), rng.uniform(0.5, 15.5, M),
+                         -rng.uniform(0.5, 15.5, M)], 1)
+        args = (mpos, np.zeros(M, np.uint32), rng.below(n_cubes * per_cube, M), rng.below(3, M).astype(np.uint8))
+    r = mk_router(16, hash_bits=hash_bits)
+    r.apply_ops(ops)
+    r.set_fanout_hint(40.0)
+    o = orc.COracle(16)
+    o.apply_ops(ops)
+    _compare(r, o, *args)
+    un = ops[::7].copy()
+    un["kind"] = abi.OP_UNSUBSCRIBE
+    r.apply_ops(un)
+    o.apply_ops(un)
+    _compare(r, o, *args)
+
+
+def test_profile_phases_and_sclk_probe():
+    """wq_profile_read_phases splits each three-launch tick into count / tile scan / emit (their sum is
+    the bracketed launch time, within event granularity); wq_probe_sclk reports a plausible clock."""
+    w = synth.config_c2(scale=0.3)
+    r = mk_router(16)
+    r.apply_ops(w.ops)
+    r.set_route_config(10)
+    r.route(w.pos, w.world, w.sender, w.repl)
+    r.profile_enable(True)
+    for _ in range(3):
+        r.route(w.pos, w.world, w.sender, w.repl)
+    ms, n, ph, nph = r.profile_read_phases()
+    r.profile_enable(False)
+    assert n == 3 and nph == 3
+    assert all(x > 0 for x in ph)
+    assert abs(sum(ph) - ms) <= 0.05 * ms + 0.02
+    r.set_route_config(0)
+    r.profile_enable(True)
+    r.route(w.pos, w.world, w.sender, w.repl)  # single launch: not phased
+    ms, n, ph, nph = r.profile_read_phases()
+    r.profile_enable(False)
+    assert n == 1 and nph == 0 and ph == [0.0, 0.0, 0.0]
+    mhz = r.probe_sclk()
+    assert 300.0 < mhz < 4000.0, mhz

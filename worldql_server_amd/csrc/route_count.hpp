@@ -69,6 +69,8 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
                                            uint32_t& E_local, uint4 (*peers_out)[6] = nullptr,
                                            uint32_t* owner_out = nullptr) {
     const int tid = threadIdx.x;
+    // the probe reads the compact header table (TableView::hdr_mask; not FULL, which reads whole lines)
+    const bool chdr = !FULL && tv.hdr && tv.hdr_mask;
 
     // ---- A: inputs (all loads first), quantise (kernel 1), packed key, home slot ----
     // SLOTS: compact slots of the sharded tick (route_common.hpp) — the key arrives packed (a
@@ -148,9 +150,10 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
             }
         }
         // lanes with nothing to probe read a dummy line spread by message index (never one shared
-        // line: a chip-wide hot line serialises on its L2 channel)
-        sl[i] = reg ? (uint32_t)slot_of(rec_hash(pk[i], ext[i]) & tv.hash_mask, tv.rec_shift)
-                    : (m & (uint32_t)tv.rec_mask);
+        // line: a chip-wide hot line serialises on its L2 channel). With compact headers the probe
+        // walks the header table; the match then hands over the record slot (below)
+        sl[i] = reg ? (uint32_t)slot_of(rec_hash(pk[i], ext[i]) & tv.hash_mask, chdr ? tv.hdr_shift : tv.rec_shift)
+                    : (m & (uint32_t)(chdr ? tv.hdr_mask : tv.rec_mask));
         via_rec[i] = valid && reg;
         st[i] = via_rec[i] ? kStProbe : kStDone;
         e_out[i] = 0;
@@ -215,6 +218,7 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
                     cnt[i] = empty ? 0u : c0[i].z;
                     loff[i] = c0[i].w;
                     st[i] = kStDone;
+                    if (chdr && !empty) sl[i] = c1[i].z;  // from here on: the cube's record slot
                     if (cnt[i] && in_rp[i] != WQ_REPL_INCLUDING_SELF) {
                         const uint64_t sig = ((uint64_t)c1[i].y << 32) | c1[i].x;
                         const uint64_t bits = peer_sig(me);
@@ -241,7 +245,7 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
                         }
                     }
                 } else {
-                    sl[i] = (sl[i] + 1) & (uint32_t)tv.rec_mask;
+                    sl[i] = (sl[i] + 1) & (uint32_t)(chdr ? tv.hdr_mask : tv.rec_mask);
                 }
             } else if (st[i] == kStVerify) {
                 // chunks vc, vc+1 hold peers 4*vc-8 .. 4*vc-1; the list is ascending, so the first

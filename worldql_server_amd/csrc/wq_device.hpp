@@ -266,6 +266,12 @@ struct TableView {
     // dense copy of every record's first 32 bytes (key, count, list offset, signature) at the same
     // slot index, 4 per 128-B line; nullptr: the count pass probes the records themselves
     const uint4* hdr = nullptr;
+    // hdr_mask != 0: the headers are a COMPACT table of their own (load <= 1/2, 4 per line, so the hot
+    // cubes of a tick share lines and the table is 1/8 of the records' size): a cube's header is found
+    // by linear probing from slot_of(hash, hdr_shift), and its word 6 holds the cube's record slot
+    // (the record's cap, which no tick reads). hdr_mask == 0: header i is record i's.
+    uint64_t hdr_mask = 0;
+    int hdr_shift = 64;
 };
 
 // ---- per-peer boxes: a fast "certainly not subscribed" for long lists ---------------------

@@ -74,6 +74,11 @@ struct Table {
     // off (hdr_ok false) from the first in-place change until the next build
     DevBuf hdr;
     bool hdr_ok = false;
+    // compact headers (round 6, default): their own open-addressed table at load <= 1/2 (hdr_cap
+    // slots), each header's cap word replaced by its record slot; hdr_cap == 0: the round-4 layout
+    // (header i = record i's first 32 bytes, WQ_HDR_COMPACT=0)
+    uint64_t hdr_cap = 0;
+    int hdr_shift = 64;
 };
 
 // The last incremental batch (wq_delta.hip), in flight: its status and stat deltas arrive in
@@ -220,6 +225,8 @@ inline TableView table_view(const wq_router* h) {
     v.pbox_valid = h->tab.n_pbox ? h->tab.pbox.as<uint32_t>() + (uint64_t)kBoxWords * h->tab.n_pbox : nullptr;
     v.stale = h->tab.stale.as<uint32_t>();
     v.hdr = h->tab.hdr_ok ? h->tab.hdr.as<uint4>() : nullptr;
+    v.hdr_mask = h->tab.hdr_cap ? h->tab.hdr_cap - 1 : 0;
+    v.hdr_shift = h->tab.hdr_shift;
     return v;
 }
 // Sticky {error OR, overflow OR} words of every route / global call since the last

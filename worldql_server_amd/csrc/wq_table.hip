@@ -436,6 +436,28 @@ int table_remove_peers(wq_router* h, const uint64_t* keys, size_t n_rm) {
     return table_remove_peers_inplace(h, keys, n_rm);
 }
 
+// Compact headers: every occupied record (ext != 0; emptied cubes keep theirs) claims the first free
+// slot of its probe run in the header table by a CAS on the header's ext word (each cube is inserted
+// once, so a claimed slot is simply passed), then writes {pk, count, list_off | sig, record slot}.
+__global__ void k_hdr_compact(const uint4* __restrict__ recs, uint64_t n, uint4* __restrict__ hdr, uint64_t hmask,
+                              int hshift, uint64_t hash_mask) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint4 a = recs[8 * i], b = recs[8 * i + 1];
+    if (b.w == 0) return;  // an empty record slot
+    const uint64_t pk = ((uint64_t)a.y << 32) | a.x;
+    uint64_t s = slot_of(rec_hash(pk, b.w) & hash_mask, hshift);
+    for (;;) {
+        uint32_t* ext_word = reinterpret_cast<uint32_t*>(hdr + 2 * s + 1) + 3;
+        if (atomicCAS(ext_word, 0u, b.w) == 0u) break;
+        s = (s + 1) & hmask;
+    }
+    hdr[2 * s] = a;
+    uint2* w2 = reinterpret_cast<uint2*>(hdr + 2 * s + 1);
+    w2[0] = make_uint2(b.x, b.y);                           // sig
+    reinterpret_cast<uint32_t*>(hdr + 2 * s + 1)[2] = (uint32_t)i;  // the record slot (ext already set)
+}
+
 __global__ void k_hdr_fill(const uint4* __restrict__ recs, uint64_t n, uint4* __restrict__ hdr) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
@@ -550,8 +572,30 @@ int table_rebuild_derived(wq_router* h) {
     // dense headers (TableView::hdr): the records' first 32 bytes at the same slot index, 4 per line,
     // read by the count pass's probes (C3: count 368 -> 351 us, tick -1.4%, same box; WQ_HDR=0: off)
     t.hdr_ok = false;
+    t.hdr_cap = 0;
+    t.hdr_shift = 64;
     static const bool want_hdr = !getenv("WQ_HDR") || atoi(getenv("WQ_HDR")) != 0;
-    if (want_hdr) {
+    // compact headers (default): their own table of >= WQ_HDR_SLOTS header slots per cube (default 4:
+    // load <= 1/4, 1/8 after the power-of-two rounding of C3's 8.56M cubes; C3 count 344.5-345.2 us
+    // with one header per record slot, 350.6 at 2 slots per cube, 453 at 1 — the probe runs, not the
+    // lines' reuse, decide); WQ_HDR_COMPACT=0: the round-4 layout, one header per record slot
+    static const bool compact = !getenv("WQ_HDR_COMPACT") || atoi(getenv("WQ_HDR_COMPACT")) != 0;
+    static const uint64_t hslots = getenv("WQ_HDR_SLOTS") ? std::max(1ul, strtoul(getenv("WQ_HDR_SLOTS"), nullptr, 10)) : 4ul;
+    if (want_hdr && compact) {
+        uint64_t hcap = 1024;
+        int log2h = 10;
+        while (hcap < hslots * n_cubes || hcap < n_cubes + 1) {
+            hcap <<= 1;
+            log2h++;
+        }
+        WQ_ALLOC(h, t.hdr, hcap * 32);
+        WQ_HIP(h, hipMemsetAsync(t.hdr.p, 0, hcap * 32, s));
+        t.hdr_cap = hcap;
+        t.hdr_shift = 64 - log2h;
+        hipLaunchKernelGGL(k_hdr_compact, dim3(grid_for(rcap)), dim3(kBlock), 0, s, t.recs.as<uint4>(), rcap,
+                           t.hdr.as<uint4>(), hcap - 1, t.hdr_shift, h->hash_mask);
+        t.hdr_ok = true;
+    } else if (want_hdr) {
         WQ_ALLOC(h, t.hdr, rcap * 32);
         hipLaunchKernelGGL(k_hdr_fill, dim3(grid_for(rcap)), dim3(kBlock), 0, s, t.recs.as<uint4>(), rcap,
                            t.hdr.as<uint4>());
