@@ -185,9 +185,12 @@ int wq_debug_route_config_count(void) { return route_config_count(); }
 
 // The radius filter's f32 copy of the positions (round to nearest, as the error bound in
 // within_radius assumes); with copy64, the f64 rows too (device-to-device: one pass over the input).
+// It also resets the bounding box k_pos_box accumulates next (box: 6 order keys, min all ones, max
+// zero), in place of two memset launches per call (round 6: C5 sets positions every tick).
 static __global__ void k_pos_f32(const double* __restrict__ pos, uint64_t n, float4* __restrict__ out,
-                                 double* __restrict__ copy64) {
+                                 double* __restrict__ copy64, unsigned long long* __restrict__ box) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (box && i < 6) box[i] = i < 3 ? ~0ull : 0ull;
     if (i >= n) return;
     const double x = pos[3 * i], y = pos[3 * i + 1], z = pos[3 * i + 2];
     out[i] = make_float4((float)x, (float)y, (float)z, 0.0f);
@@ -294,13 +297,12 @@ static int set_peer_positions(wq_router* h, const double* pos, size_t n, hipMemc
     WQ_ALLOC(h, h->pcode, (n ? n : 1) * 4);
     WQ_ALLOC(h, h->qbox, 128);
     if (n) {
+        // the f32 copy, and the reset of the bounding box of the 4-byte codes (the radius filter's first
+        // test: bounding box, then one code per peer)
         hipLaunchKernelGGL(k_pos_f32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream,
                            d2d ? pos : h->ppos.as<double>(), (uint64_t)n, h->ppos4.as<float4>(),
-                           d2d ? h->ppos.as<double>() : nullptr);
+                           d2d ? h->ppos.as<double>() : nullptr, h->qbox.as<unsigned long long>());
         WQ_HIP(h, hipGetLastError());
-        // the 4-byte codes of the radius filter's first test: bounding box, then one code per peer
-        WQ_HIP(h, hipMemsetAsync(h->qbox.p, 0xFF, 24, h->stream));  // min keys: all ones
-        WQ_HIP(h, hipMemsetAsync(h->qbox.as<uint64_t>() + 3, 0, 24, h->stream));  // max keys: zero
         const unsigned gb = (unsigned)std::min<size_t>(256, (n + 255) / 256);
         hipLaunchKernelGGL(k_pos_box, dim3(gb), dim3(256), 0, h->stream, h->ppos.as<double>(), (uint64_t)n,
                            h->qbox.as<unsigned long long>());
