@@ -37,6 +37,9 @@ struct TileScanParams {
     // an asynchronous sharded tick's end (route_async.hpp), run by the one-block scan after its counters
     AsyncResultParams ar{};
     bool async_end = false;
+    // the caller's counters (wq_route_tick_device), copied from cnt once final (the emit after the
+    // scan sets no counter bit), nullable
+    wq_route_counters* out = nullptr;
 };
 
 // Inclusive wave64 prefix sum of u32 by DPP row shifts and row broadcasts (no LDS round trips).
@@ -129,6 +132,7 @@ static __global__ __launch_bounds__(kScanThreads) void tile_scan_kernel(TileScan
         // u32 CSR offsets cannot hold more than 2^32-1 pairs: error bit 2
         flag_route(p.cnt, p.health, P > 0xFFFFFFFFull ? 2u : 0u, P > p.capacity ? 1u : 0u);
         if (p.stale && *p.stale) flag_route(p.cnt, p.health, kErrStale, 0u);
+        if (p.out) *p.out = *p.cnt;
     }
     if (p.async_end) {  // (never with chunks) the counters above are final: the tick's end, here
         __syncthreads();
@@ -302,6 +306,7 @@ static __global__ __launch_bounds__(kMScanThreads) void tile_scan_multi_kernel(T
             p.cnt->n_pairs = P;
             flag_route(p.cnt, p.health, P > 0xFFFFFFFFull ? 2u : 0u, P > p.capacity ? 1u : 0u);
             if (p.stale && *p.stale) flag_route(p.cnt, p.health, kErrStale, 0u);
+            if (p.out) *p.out = *p.cnt;
         }
     }
 }
@@ -312,9 +317,11 @@ constexpr uint32_t kScanOneBlockMax = 8192;  // tiles: up to here the one-block 
 // rocPRIM + tile_finish_kernel beyond. P must fit the u32 offsets either way (error bit 2 if not);
 // a tick of > 2^32 pairs wraps the prefix, which the error bit already reports. With sp.async_end,
 // *async_done says whether the scan took the asynchronous tick's end (the one-block scan only).
-inline int launch_tile_scan(wq_router* h, const TileScanParams& sp, bool* async_done = nullptr) {
+inline int launch_tile_scan(wq_router* h, const TileScanParams& sp, bool* async_done = nullptr,
+                            bool* out_done = nullptr) {
     hipStream_t s = h->stream;
     if (async_done) *async_done = false;
+    if (out_done) *out_done = false;
     // the one-block scan below 2,048 tiles, and up to kScanOneBlockMax when it takes an asynchronous
     // tick's end; the multi-block scan otherwise (C3 17.8 -> 8.7 us; an 8-GPU rank's 4,883 tiles
     // 206.8-207.5 -> 205.8-206.3 us per tick, alternating). WQ_SCAN_MULTI_MIN moves the threshold
@@ -324,6 +331,7 @@ inline int launch_tile_scan(wq_router* h, const TileScanParams& sp, bool* async_
         hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, sp);
         WQ_HIP(h, hipGetLastError());
         if (async_done) *async_done = sp.async_end;
+        if (out_done) *out_done = sp.out != nullptr;
         return WQ_OK;
     }
     // WQ_SCAN_MULTI=0: rocPRIM's look-back scan + tile_finish_kernel (the round-5 path, for A/B)
@@ -339,6 +347,7 @@ inline int launch_tile_scan(wq_router* h, const TileScanParams& sp, bool* async_
         const uint32_t tag = (uint32_t)(rw.scan_calls++ % ((1ull << kSGranTagBits) - 1)) + 1u;
         hipLaunchKernelGGL(tile_scan_multi_kernel, dim3(nb), dim3(kMScanThreads), 0, s, sp, rw.sgran.as<uint64_t>(), tag);
         WQ_HIP(h, hipGetLastError());
+        if (out_done) *out_done = sp.out != nullptr;
         return WQ_OK;
     }
     size_t bytes = 0;

@@ -126,6 +126,10 @@ struct RouteWs {
     DevBuf carry;
     uint64_t calls = 0;
     wq_route_counters* last = nullptr;  // counters of the most recent call (device)
+    // wq_route_tick_device's caller counters: the three-launch tick's scan writes them itself when it
+    // can (out_done), instead of a copy launch after the tick
+    wq_route_counters* out = nullptr;
+    bool out_done = false;
 };
 
 struct ProfileEvents {
@@ -192,7 +196,8 @@ struct wq_router {
     wq::DevBuf ppos;
     wq::DevBuf ppos4;  // f32 copy (float4 per peer) for the radius filter's second test
     wq::DevBuf pcode;  // 4-byte position codes (the first test) and their box (wq_device.hpp)
-    wq::DevBuf qbox;   // u64 box keys [0, 6), then {lo, step} doubles [6, 12)
+    wq::DevBuf qbox;   // u64 box keys [0, 6), then {lo, step} doubles [6, 12), the second box slot [12, 18)
+    int qbox_phase = -1;  // the box slot the next wq_set_peer_positions accumulates into (-1: not reset yet)
     uint64_t n_ppos = 0;
     double radius = 0.0;
     wq::ProfileEvents prof;

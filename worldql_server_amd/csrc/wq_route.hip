@@ -382,7 +382,8 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
     sp.cnt = cur;
     sp.health = route_health(h);
     sp.stale = tv.stale;
-    if (int rc = launch_tile_scan(h, sp)) return rc;
+    sp.out = rw.out;
+    if (int rc = launch_tile_scan(h, sp, nullptr, &rw.out_done)) return rc;
     if (pr.enabled) {
         WQ_HIP(h, hipEventRecord(pr.mid2[pr.used], s));
         pr.phased[pr.used] = 1;

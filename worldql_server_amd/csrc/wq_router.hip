@@ -183,24 +183,6 @@ int wq_get_stats(wq_router* h, wq_stats* out) {
 
 int wq_debug_route_config_count(void) { return route_config_count(); }
 
-// The radius filter's f32 copy of the positions (round to nearest, as the error bound in
-// within_radius assumes); with copy64, the f64 rows too (device-to-device: one pass over the input).
-// It also resets the bounding box k_pos_box accumulates next (box: 6 order keys, min all ones, max
-// zero), in place of two memset launches per call (round 6: C5 sets positions every tick).
-static __global__ void k_pos_f32(const double* __restrict__ pos, uint64_t n, float4* __restrict__ out,
-                                 double* __restrict__ copy64, unsigned long long* __restrict__ box) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (box && i < 6) box[i] = i < 3 ? ~0ull : 0ull;
-    if (i >= n) return;
-    const double x = pos[3 * i], y = pos[3 * i + 1], z = pos[3 * i + 2];
-    out[i] = make_float4((float)x, (float)y, (float)z, 0.0f);
-    if (copy64) {
-        copy64[3 * i] = x;
-        copy64[3 * i + 1] = y;
-        copy64[3 * i + 2] = z;
-    }
-}
-
 // The positions' bounding box (finite coordinates only) as order-preserving u64 keys: 6 words
 // {min x, y, z, max x, y, z}; a few hundred blocks, one atomic per block and word.
 __device__ __forceinline__ uint64_t ord_key(double x) {
@@ -211,18 +193,44 @@ __device__ __forceinline__ double ord_val(uint64_t k) {
     return __longlong_as_double((long long)((k >> 63) ? (k & ~(1ull << 63)) : ~k));
 }
 
-static __global__ __launch_bounds__(256) void k_pos_box(const double* __restrict__ pos, uint64_t n,
-                                                        unsigned long long* __restrict__ box) {
+// One pass over the positions (round 6: it was two, k_pos_f32 then k_pos_box): the radius filter's
+// f32 copy (round to nearest, as the error bound in within_radius assumes; with copy64 the f64 rows
+// too, device to device) and the bounding box of the finite coordinates as order-preserving u64 keys
+// — 6 words {min x, y, z, max x, y, z} in `box`, reset by the previous call's k_pos_code (two box
+// slots alternate); a few hundred blocks, one atomic per block and word.
+static __global__ __launch_bounds__(256) void k_pos_f32_box(const double* __restrict__ pos, uint64_t n,
+                                                            float4* __restrict__ out, double* __restrict__ copy64,
+                                                            unsigned long long* __restrict__ box) {
     __shared__ uint64_t part[4][6];
     uint64_t lo[3] = {~0ull, ~0ull, ~0ull}, hi[3] = {0, 0, 0};
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-        const double v[3] = {pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]};
-        if (!(isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]))) continue;
+    constexpr int U = 4;  // positions per thread per round, all loads in flight first
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += U * stride) {
+        double v[U][3];
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            const uint64_t k = ord_key(v[d]);
-            lo[d] = k < lo[d] ? k : lo[d];
-            hi[d] = k > hi[d] ? k : hi[d];
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = i0 + u * stride, j = i < n ? i : i0;  // (i0 < n)
+            v[u][0] = pos[3 * j];
+            v[u][1] = pos[3 * j + 1];
+            v[u][2] = pos[3 * j + 2];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = i0 + u * stride;
+            if (i >= n) continue;
+            out[i] = make_float4((float)v[u][0], (float)v[u][1], (float)v[u][2], 0.0f);
+            if (copy64) {
+                copy64[3 * i] = v[u][0];
+                copy64[3 * i + 1] = v[u][1];
+                copy64[3 * i + 2] = v[u][2];
+            }
+            if (!(isfinite(v[u][0]) && isfinite(v[u][1]) && isfinite(v[u][2]))) continue;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const uint64_t k = ord_key(v[u][d]);
+                lo[d] = k < lo[d] ? k : lo[d];
+                hi[d] = k > hi[d] ? k : hi[d];
+            }
         }
     }
 #pragma unroll
@@ -252,7 +260,9 @@ static __global__ __launch_bounds__(256) void k_pos_box(const double* __restrict
 
 // The box -> {lo, step} (kept at box + 6 as doubles for the count pass) and every peer's code.
 static __global__ __launch_bounds__(256) void k_pos_code(const double* __restrict__ pos, uint64_t n,
-                                                         unsigned long long* __restrict__ box, uint32_t* __restrict__ code) {
+                                                         const unsigned long long* __restrict__ box,
+                                                         double* __restrict__ dec, unsigned long long* __restrict__ next,
+                                                         uint32_t* __restrict__ code) {
     double qb[6];
     bool any = true;
 #pragma unroll
@@ -266,10 +276,10 @@ static __global__ __launch_bounds__(256) void k_pos_code(const double* __restric
     }
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i == 0) {
-        double* out = reinterpret_cast<double*>(box + 6);
 #pragma unroll
-        for (int k = 0; k < 6; ++k) out[k] = qb[k];
+        for (int k = 0; k < 6; ++k) dec[k] = qb[k];
     }
+    if (i < 6) next[i] = i < 3 ? ~0ull : 0ull;  // the other box slot, for the next call
     if (i >= n) return;
     const double x = pos[3 * i], y = pos[3 * i + 1], z = pos[3 * i + 2];
     uint32_t c = any ? pos_code(x, y, z, qb) : kQNone;
@@ -295,20 +305,30 @@ static int set_peer_positions(wq_router* h, const double* pos, size_t n, hipMemc
     const bool d2d = kind == hipMemcpyDeviceToDevice;
     if (n && !d2d) WQ_HIP(h, hipMemcpyAsync(h->ppos.p, pos, n * 24, kind, h->stream));
     WQ_ALLOC(h, h->pcode, (n ? n : 1) * 4);
-    WQ_ALLOC(h, h->qbox, 128);
+    // qbox: u64 box slot A [0, 6), the decoded {lo, step} doubles [6, 12) (TableView::qbox), slot B
+    // [12, 18); the slots alternate between calls, each call's k_pos_code resetting the other one
+    if (!h->qbox.p) h->qbox_phase = -1;
+    WQ_ALLOC(h, h->qbox, 192);
     if (n) {
-        // the f32 copy, and the reset of the bounding box of the 4-byte codes (the radius filter's first
-        // test: bounding box, then one code per peer)
-        hipLaunchKernelGGL(k_pos_f32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream,
-                           d2d ? pos : h->ppos.as<double>(), (uint64_t)n, h->ppos4.as<float4>(),
-                           d2d ? h->ppos.as<double>() : nullptr, h->qbox.as<unsigned long long>());
-        WQ_HIP(h, hipGetLastError());
+        unsigned long long* q = h->qbox.as<unsigned long long>();
+        if (h->qbox_phase < 0) {  // first use: both slots reset (one memset pair, once per handle)
+            WQ_HIP(h, hipMemsetAsync(q, 0xFF, 24, h->stream));
+            WQ_HIP(h, hipMemsetAsync(q + 3, 0, 24, h->stream));
+            WQ_HIP(h, hipMemsetAsync(q + 12, 0xFF, 24, h->stream));
+            WQ_HIP(h, hipMemsetAsync(q + 15, 0, 24, h->stream));
+            h->qbox_phase = 0;
+        }
+        unsigned long long* cur = q + (h->qbox_phase ? 12 : 0);
+        unsigned long long* nxt = q + (h->qbox_phase ? 0 : 12);
         const unsigned gb = (unsigned)std::min<size_t>(256, (n + 255) / 256);
-        hipLaunchKernelGGL(k_pos_box, dim3(gb), dim3(256), 0, h->stream, h->ppos.as<double>(), (uint64_t)n,
-                           h->qbox.as<unsigned long long>());
-        hipLaunchKernelGGL(k_pos_code, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream,
-                           h->ppos.as<double>(), (uint64_t)n, h->qbox.as<unsigned long long>(), h->pcode.as<uint32_t>());
+        hipLaunchKernelGGL(k_pos_f32_box, dim3(gb), dim3(256), 0, h->stream, d2d ? pos : h->ppos.as<double>(),
+                           (uint64_t)n, h->ppos4.as<float4>(), d2d ? h->ppos.as<double>() : nullptr, cur);
         WQ_HIP(h, hipGetLastError());
+        hipLaunchKernelGGL(k_pos_code, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream,
+                           h->ppos.as<double>(), (uint64_t)n, cur, reinterpret_cast<double*>(q + 6), nxt,
+                           h->pcode.as<uint32_t>());
+        WQ_HIP(h, hipGetLastError());
+        h->qbox_phase ^= 1;
     }
     if (kind == hipMemcpyHostToDevice) WQ_HIP(h, hipStreamSynchronize(h->stream));
     h->n_ppos = n;
@@ -478,9 +498,13 @@ int wq_route_tick_device(wq_router* h, const double* d_pos, const int64_t* d_key
         }
         return rc == WQ_E_CAPACITY ? WQ_OK : rc;  // as the single-GPU form: the counters report overflow
     }
+    // the three-launch shape's scan writes d_counters itself once they are final (no copy launch)
+    h->rws.out = d_counters;
+    h->rws.out_done = false;
     int rc = launch_route(h, d_pos, d_keys, d_world, d_sender, d_repl, n_msgs, d_offsets, d_peers, d_msgs, capacity);
+    h->rws.out = nullptr;
     if (rc) return rc;
-    if (d_counters)
+    if (d_counters && !h->rws.out_done)
         WQ_HIP(h, hipMemcpyAsync(d_counters, h->rws.last, sizeof(wq_route_counters), hipMemcpyDeviceToDevice,
                                  h->stream));
     return WQ_OK;
