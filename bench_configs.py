@@ -699,6 +699,8 @@ def run_c4(a, rank, world_size, local_rank, dev):
     stream = torch.cuda.Stream(device=dev)
     r = Router(16, local_rank)
     r.set_stream(stream.cuda_stream)
+    if os.environ.get("WQ_BENCH_FANOUT_HINT"):  # tuning: the route shape a server's hint would pick
+        r.set_fanout_hint(float(os.environ["WQ_BENCH_FANOUT_HINT"]))
     t0 = time.perf_counter()
     r.apply_ops(init)
     build_s = time.perf_counter() - t0
