@@ -39,6 +39,9 @@ struct TickParams {
     uint32_t* health;   // sticky {error, overflow} words (flag_route)
     uint64_t* stamps;  // diagnostics (wq_debug_set_timeline) or nullptr
     uint32_t n_tiles;   // 256-message tiles (one block each)
+    // the caller's counters (wq_route_tick_device): the last block copies cnt there once it is final,
+    // instead of a copy launch after the tick; nullable
+    wq_route_counters* out_cnt = nullptr;
 };
 
 constexpr uint32_t kErrSpin = 4u;
@@ -281,6 +284,17 @@ __global__ __launch_bounds__(kBlock) void tick_kernel(TickParams p) {
         }
     }
     lds_barrier();
+    if (b == NB - 1 && p.out_cnt) {  // block-uniform: every wave's counter atomics drained first
+        __syncthreads();
+        if (tid == 0) {
+            wq_route_counters c;
+            c.n_pairs = __hip_atomic_load(&p.cnt->n_pairs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            c.n_candidates = __hip_atomic_load(&p.cnt->n_candidates, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            c.overflow = __hip_atomic_load(&p.cnt->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            c.error = __hip_atomic_load(&p.cnt->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *p.out_cnt = c;
+        }
+    }
     const uint64_t g0 = sm.pre;
     if (stamp) p.stamps[4 * b + 2] = __builtin_amdgcn_s_memrealtime();
 

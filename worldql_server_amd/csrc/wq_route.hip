@@ -183,8 +183,10 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         tp.health = route_health(h);
         tp.stamps = rw.stamps;
         tp.n_tiles = (uint32_t)nb;
+        tp.out_cnt = rw.out;
         cfg.tick(tp, s, (unsigned)nb);
         WQ_HIP(h, hipGetLastError());
+        rw.out_done = rw.out != nullptr;
         if (pr.enabled) {
             WQ_HIP(h, hipEventRecord(pr.stop[pr.used], s));
             pr.used++;
