@@ -340,11 +340,14 @@ inline int launch_tile_scan(wq_router* h, const TileScanParams& sp, bool* async_
         RouteWs& rw = h->rws;
         const uint32_t nb = (sp.n_tiles + kMScanTile - 1) / kMScanTile;
         WQ_ALLOC(h, rw.sgran, (uint64_t)nb * 16);
-        if (rw.sgran_zeroed < 2ull * nb) {  // fresh granules: tag 0 never matches
+        const uint64_t period = (1ull << kSGranTagBits) - 1;
+        // fresh granules (tag 0 never matches), and all of them again when the tags wrap, so a granule
+        // left by a scan 2^24 - 1 calls back can never pass for this call's
+        if (rw.sgran_zeroed < 2ull * nb || (rw.scan_calls && rw.scan_calls % period == 0)) {
             WQ_HIP(h, hipMemsetAsync(rw.sgran.p, 0, rw.sgran.bytes, s));
             rw.sgran_zeroed = rw.sgran.bytes / 8;
         }
-        const uint32_t tag = (uint32_t)(rw.scan_calls++ % ((1ull << kSGranTagBits) - 1)) + 1u;
+        const uint32_t tag = (uint32_t)(rw.scan_calls++ % period) + 1u;
         hipLaunchKernelGGL(tile_scan_multi_kernel, dim3(nb), dim3(kMScanThreads), 0, s, sp, rw.sgran.as<uint64_t>(), tag);
         WQ_HIP(h, hipGetLastError());
         if (out_done) *out_done = sp.out != nullptr;
