@@ -311,6 +311,119 @@ static __global__ __launch_bounds__(kMScanThreads) void tile_scan_multi_kernel(T
     }
 }
 
+// The same decoupled shape for a plain u32 exclusive scan (out[i] = sum of in[0 .. i), wrapping):
+// 4,096 elements per block, each block summing every lower block's tagged total itself. One launch
+// instead of rocPRIM's scan (its state init, the scan and its temporary storage).
+static __global__ __launch_bounds__(kMScanThreads) void scan_u32_multi_kernel(const uint32_t* __restrict__ in,
+                                                                               uint32_t* __restrict__ out, uint32_t n,
+                                                                               uint64_t* gran, uint32_t tag,
+                                                                               wq_route_counters* err) {
+    constexpr int NW = kMScanThreads / 64;
+    __shared__ uint32_t s_wave[NW], s_pre[NW];
+    __shared__ uint32_t s_gave;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t b = blockIdx.x;
+    const uint32_t t0 = b * kMScanTile + (uint32_t)tid * kMScanPer;
+    uint32_t v[kMScanPer];
+    if (t0 + kMScanPer <= n && (reinterpret_cast<uintptr_t>(in) & 15) == 0) {
+        const uint4* iv = reinterpret_cast<const uint4*>(in + t0);
+        uint4 a[kMScanPer / 4];
+#pragma unroll
+        for (int k = 0; k < kMScanPer / 4; ++k) a[k] = iv[k];
+#pragma unroll
+        for (int k = 0; k < kMScanPer / 4; ++k) {
+            v[4 * k] = a[k].x;
+            v[4 * k + 1] = a[k].y;
+            v[4 * k + 2] = a[k].z;
+            v[4 * k + 3] = a[k].w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kMScanPer; ++k) v[k] = t0 + k < n ? in[t0 + k] : 0u;
+    }
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < kMScanPer; ++k) {
+        const uint32_t x = v[k];
+        v[k] = run;
+        run += x;
+    }
+    const uint32_t incl = wave_incl_scan_u32_dpp(run);
+    if (lane == 63) s_wave[wave] = incl;
+    if (tid == 0) s_gave = 0;
+    __syncthreads();
+    uint32_t before = incl - run, tot = 0;
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+        if (u < wave) before += s_wave[u];
+        tot += s_wave[u];
+    }
+    if (tid == 0) __hip_atomic_store(gran + b, sgranule(tag, tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t pe = 0;
+    bool gave = false;
+    for (uint32_t j = tid; j < b; j += kMScanThreads) {
+        uint64_t x = 0;
+        for (uint32_t it = 0;; ++it) {
+            x = __hip_atomic_load(gran + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(x >> (64 - kSGranTagBits)) == tag) break;
+            if (it >= kSpinLimitScan) {
+                gave = true;
+                x = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        pe += (uint32_t)x;
+    }
+    pe = (uint32_t)wave_sum_u64(pe);
+    if (lane == 0) s_pre[wave] = pe;
+    if (gave) s_gave = 1;
+    __syncthreads();
+    uint32_t base = before;
+#pragma unroll
+    for (int u = 0; u < NW; ++u) base += s_pre[u];
+    if (t0 + kMScanPer <= n && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+        uint4* o = reinterpret_cast<uint4*>(out + t0);
+#pragma unroll
+        for (int k = 0; k < kMScanPer / 4; ++k)
+            o[k] = make_uint4(base + v[4 * k], base + v[4 * k + 1], base + v[4 * k + 2], base + v[4 * k + 3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < kMScanPer; ++k)
+            if (t0 + k < n) out[t0 + k] = base + v[k];
+    }
+    if (tid == 0 && s_gave && err) atomicOr(&err->error, kErrSpinScan);
+}
+
+// The multi-block scans' tagged granules (RouteWs::sgran): room for `words`, zeroed when fresh or
+// when the tags wrap; returns this launch's tag.
+inline int scan_granules(wq_router* h, uint64_t words, uint32_t* tag) {
+    RouteWs& rw = h->rws;
+    WQ_ALLOC(h, rw.sgran, words * 8);
+    const uint64_t period = (1ull << kSGranTagBits) - 1;
+    // fresh granules (tag 0 never matches), and all of them again when the tags wrap, so a granule
+    // left by a scan 2^24 - 1 calls back can never pass for this call's
+    if (rw.sgran_zeroed < words || (rw.scan_calls && rw.scan_calls % period == 0)) {
+        WQ_HIP(h, hipMemsetAsync(rw.sgran.p, 0, rw.sgran.bytes, h->stream));
+        rw.sgran_zeroed = rw.sgran.bytes / 8;
+    }
+    *tag = (uint32_t)(rw.scan_calls++ % period) + 1u;
+    return WQ_OK;
+}
+
+// out[i] = sum of in[0 .. i) (u32, wrapping) in one launch on the handle's stream; a spin that gave
+// up (never in practice) sets error bit 4 in *err when given.
+inline int launch_scan_u32(wq_router* h, const uint32_t* in, uint32_t* out, uint32_t n, wq_route_counters* err) {
+    if (!n) return WQ_OK;
+    const uint32_t nb = (n + kMScanTile - 1) / kMScanTile;
+    uint32_t tag = 0;
+    if (int rc = scan_granules(h, nb, &tag)) return rc;
+    hipLaunchKernelGGL(scan_u32_multi_kernel, dim3(nb), dim3(kMScanThreads), 0, h->stream, in, out, n,
+                       h->rws.sgran.as<uint64_t>(), tag, err);
+    WQ_HIP(h, hipGetLastError());
+    return WQ_OK;
+}
+
 constexpr uint32_t kScanOneBlockMax = 8192;  // tiles: up to here the one-block scan is the faster
 
 // The tick's tile scan (n_tiles >= 1): one block for a few thousand tiles (C2: 3,907),
@@ -339,15 +452,8 @@ inline int launch_tile_scan(wq_router* h, const TileScanParams& sp, bool* async_
     if (multi) {
         RouteWs& rw = h->rws;
         const uint32_t nb = (sp.n_tiles + kMScanTile - 1) / kMScanTile;
-        WQ_ALLOC(h, rw.sgran, (uint64_t)nb * 16);
-        const uint64_t period = (1ull << kSGranTagBits) - 1;
-        // fresh granules (tag 0 never matches), and all of them again when the tags wrap, so a granule
-        // left by a scan 2^24 - 1 calls back can never pass for this call's
-        if (rw.sgran_zeroed < 2ull * nb || (rw.scan_calls && rw.scan_calls % period == 0)) {
-            WQ_HIP(h, hipMemsetAsync(rw.sgran.p, 0, rw.sgran.bytes, s));
-            rw.sgran_zeroed = rw.sgran.bytes / 8;
-        }
-        const uint32_t tag = (uint32_t)(rw.scan_calls++ % period) + 1u;
+        uint32_t tag = 0;
+        if (int rc = scan_granules(h, 2ull * nb, &tag)) return rc;
         hipLaunchKernelGGL(tile_scan_multi_kernel, dim3(nb), dim3(kMScanThreads), 0, s, sp, rw.sgran.as<uint64_t>(), tag);
         WQ_HIP(h, hipGetLastError());
         if (out_done) *out_done = sp.out != nullptr;

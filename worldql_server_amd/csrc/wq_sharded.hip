@@ -482,6 +482,9 @@ __global__ __launch_bounds__(kBlock) void k_unshard(const wq_msg_rec* __restrict
 
 int scan_excl(wq_router* h, DevBuf& tmp, const uint32_t* in, uint32_t* out, size_t n) {
     if (!n) return WQ_OK;
+    // one launch (route_scan.hpp launch_scan_u32) up to 2^32 - 1 elements; WQ_SCAN_MULTI=0: rocPRIM
+    static const bool multi = !getenv("WQ_SCAN_MULTI") || atoi(getenv("WQ_SCAN_MULTI")) != 0;
+    if (multi && n < 0xFFFFFFFFull) return launch_scan_u32(h, in, out, (uint32_t)n, nullptr);
     size_t bytes = 0;
     WQ_HIP(h, rocprim::exclusive_scan(nullptr, bytes, in, out, 0u, n, rocprim::plus<uint32_t>(), h->stream));
     WQ_ALLOC(h, tmp, bytes);
