@@ -361,5 +361,40 @@ __global__ __launch_bounds__(kBlock, MINW) void count_kernel(CountParams p) {
     }
 }
 
-}  // namespace wq
+// One wave per block, one 64-message tile per wave (route config 13, an experiment of round 6): no
+// block barrier, so a wave whose lanes finish early leaves its slot to the next tile at once instead
+// of waiting for the block's slowest wave. The tile totals are per 64 messages (count_tile = 64;
+// the emit's tile prefix addressing takes any count_tile dividing its 256-message blocks).
+template <bool RAW_KEYS, int MINB>
+__global__ __launch_bounds__(64, MINB) void count_wave_kernel(CountParams p) {
+    const int lane = threadIdx.x;
+    if (blockIdx.x == 0 && lane == 0) {
+        p.cnt_next->n_pairs = 0;
+        p.cnt_next->n_candidates = 0;
+        p.cnt_next->overflow = 0;
+        p.cnt_next->error = 0;
+    }
+    const uint32_t nt = p.n_tiles ? p.n_tiles : gridDim.x;
+    for (uint32_t blk = blockIdx.x; blk < nt; blk += gridDim.x) {
+        const uint32_t m0 = blk * 64u;
+        uint64_t F_local = 0;
+        uint32_t E_local = 0;
+        uint32_t e_out[1];
+        uint2 inf_out[1];
+        count_rows<RAW_KEYS, 1>(p.in, p.t, m0, e_out, inf_out, F_local, E_local);
+        const uint32_t m = m0 + lane;
+        if (m < p.in.M) {
+            p.e[m] = e_out[0];
+            p.info[m] = inf_out[0];
+        }
+        const uint64_t Fw = wave_sum_u64(F_local);
+        const uint64_t Ew = wave_sum_u64(E_local);
+        if (lane == 0) {
+            p.tile_F[blk] = Fw > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Fw;
+            p.tile_total[blk] = Ew > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)Ew;
+            if (Ew > 0xFFFFFFFFull) flag_route(p.cnt, p.health, 2u, 0u);
+        }
+    }
+}
 
+}  // namespace wq

@@ -53,6 +53,14 @@ void launch_count(const CountParams& p, hipStream_t s, unsigned grid) {
         hipLaunchKernelGGL((count_kernel<false, IPT, MINW, 0, FULL>), dim3(grid), dim3(kBlock), 0, s, p);
 }
 
+// route config 13: one-wave count blocks of 64 messages (route_count.hpp count_wave_kernel)
+void launch_count_wave(const CountParams& p, hipStream_t s, unsigned grid) {
+    if (p.in.keys)
+        hipLaunchKernelGGL((count_wave_kernel<true, 32>), dim3(grid), dim3(64), 0, s, p);
+    else
+        hipLaunchKernelGGL((count_wave_kernel<false, 32>), dim3(grid), dim3(64), 0, s, p);
+}
+
 template <int STAGE, int U, bool NT = false>
 void launch_tick(const TickParams& p, hipStream_t s, unsigned grid) {
     if (p.in.keys)
@@ -87,6 +95,8 @@ const Cfg kCfgs[] = {
     // 12: cfg 0 with plain (not non-temporal) copy-out stores: C2 64.8 us against cfg 0's 63.2
     //     (tools/tune_route.py, 4 rounds; a non-temporal emit_map on C3 was 4% slower, not kept)
     {kBlock, &launch_count<1, 8>, 4096, 2816, &launch_tick<2816, 2, false>, 0, 0},
+    // 13: cfg 10 with one-wave count blocks of 64 messages (count_wave_kernel; round-6 experiment)
+    {64, &launch_count_wave, 4096 + 2, 0, nullptr, 0, 116},
 };
 #undef WQ_CFG1
 #undef WQ_CFGS
@@ -366,7 +376,7 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         // slice: 4,883 tiles) is faster with one (212-213 vs 221-222 us, with one emit block per
         // workgroup too; 2.5M messages 383-384 vs 389-390). WQ_DEBUG_COUNT_TPB overrides (diagnostics)
         static const uint32_t tpb_env = getenv("WQ_DEBUG_COUNT_TPB") ? (uint32_t)std::max(1, atoi(getenv("WQ_DEBUG_COUNT_TPB"))) : 0u;
-        const uint32_t tpb = tpb_env ? tpb_env : (n_count <= kShortTickTiles ? 1u : 2u);
+        const uint32_t tpb = tpb_env ? tpb_env : ((uint64_t)n_count * count_tile <= (uint64_t)kShortTickTiles * kBlock ? 1u : 2u);
         cp.n_tiles = n_count;
         cfg.count(cp, s, (n_count + tpb - 1) / tpb);
     }
