@@ -154,6 +154,7 @@ struct wq_router {
     hipStream_t stream = nullptr;
     uint64_t hash_mask = ~0ull;
     uint32_t rec_slack = 8;  // record slots per cube at build (load <= 1/rec_slack)
+    bool rec_slack_set = false;  // set by wq_debug_set_record_slack (then no footprint cap)
     uint64_t hash_fallbacks = 0;
     std::string err;
 

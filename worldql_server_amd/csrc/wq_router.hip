@@ -419,6 +419,7 @@ int wq_debug_set_timeline(wq_router* h, uint64_t* d_stamps) {
 int wq_debug_set_record_slack(wq_router* h, uint32_t slots_per_cube) {
     if (!h || slots_per_cube < 2 || slots_per_cube > 1024) return WQ_E_INVALID;
     h->rec_slack = slots_per_cube;  // takes effect at the next rebuild
+    h->rec_slack_set = true;        // ... exactly (no footprint cap, wq_table.hip)
     return WQ_OK;
 }
 
