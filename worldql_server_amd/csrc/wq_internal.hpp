@@ -19,6 +19,9 @@ constexpr uint32_t kErrBadBatch = 16u;
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    // hipExtMallocWithFlags flags for the next allocation (0: hipMalloc); a flagged allocation that
+    // fails falls back to hipMalloc
+    unsigned flags = 0;
     hipError_t ensure(size_t need) {
         if (need <= bytes) return hipSuccess;
         if (p) {
@@ -28,7 +31,12 @@ struct DevBuf {
             bytes = 0;
         }
         size_t cap = need < 4096 ? 4096 : need + need / 4;
-        hipError_t e = hipMalloc(&p, cap);
+        hipError_t e = flags ? hipExtMallocWithFlags(&p, cap, flags) : hipMalloc(&p, cap);
+        if (e != hipSuccess && flags) {
+            (void)hipGetLastError();
+            p = nullptr;
+            e = hipMalloc(&p, cap);
+        }
         if (e == hipSuccess) bytes = cap;
         return e;
     }

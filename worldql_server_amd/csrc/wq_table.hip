@@ -538,16 +538,21 @@ int table_rebuild_derived(wq_router* h) {
         log2r++;
     }
     // Round 6: the count probes the compact headers (their own table), so past them a tick only reads
-    // a record at a known slot and the record table's load barely matters — its footprint does. A
-    // default-slack table of more than WQ_REC_CAP_GB (8) GiB is halved while its load stays <= 1/4:
-    // C3's 17.2 GB of records become 8.6 GB. Same-box A/B: the C3 emit 977 -> 900 us on one box,
-    // unchanged on another (count, N = 8 rank too); C2-sized tables keep load 1/8 (at 1/4 their
-    // record-probing single launch is 4% slower). An explicit wq_debug_set_record_slack is kept as is.
-    static const double cap_gb = getenv("WQ_REC_CAP_GB") ? atof(getenv("WQ_REC_CAP_GB")) : 8.0;
-    while (!h->rec_slack_set && (double)rcap * sizeof(Record) > cap_gb * 1073741824.0 && rcap / 2 >= 4ull * n_cubes) {
+    // a record at a known slot and the record table's load barely matters — its footprint does.
+    // WQ_REC_CAP_GB=G halves a default-slack table of more than G GiB while its load stays <= 1/4
+    // (C3: 17.2 -> 8.6 GB of records). Opt-in: four boxes measured the C3 tick with and without it
+    // (profiles/r06_record_cap_ab.json) — faster on one (emit 977 -> 900 us), slower on one
+    // (900 -> 970 us), equal on two; the 900/975 us emit modes follow the box and the allocation, not
+    // the table size. An explicit wq_debug_set_record_slack is kept as is.
+    static const double cap_gb = getenv("WQ_REC_CAP_GB") ? atof(getenv("WQ_REC_CAP_GB")) : 0.0;
+    while (cap_gb > 0.0 && !h->rec_slack_set && (double)rcap * sizeof(Record) > cap_gb * 1073741824.0 && rcap / 2 >= 4ull * n_cubes) {
         rcap >>= 1;
         log2r--;
     }
+    // WQ_CONTIG=1: the record table as one hipDeviceMallocContiguous allocation (hipMalloc if that
+    // fails). Measured equal to hipMalloc on a box in the fast emit mode (r06_record_cap_ab.json).
+    static const bool contig = getenv("WQ_CONTIG") && atoi(getenv("WQ_CONTIG")) != 0;
+    t.recs.flags = contig ? hipDeviceMallocContiguous : 0u;
     WQ_ALLOC(h, t.recs, rcap * sizeof(Record));
     WQ_ALLOC(h, t.rclaim, rcap * 4);
     WQ_HIP(h, hipMemsetAsync(t.recs.p, 0, rcap * sizeof(Record), s));
