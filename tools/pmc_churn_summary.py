@@ -11,7 +11,7 @@ import json
 import os
 
 TICK = ("k_delta_", "k_sort_", "k_bucket_", "k_pos_", "count_radius_kernel", "count_kernel", "tile_scan_kernel",
-        "tile_finish_kernel", "emit_kernel", "emit_map_kernel", "tick_kernel")
+        "tile_finish_kernel", "tile_scan_multi_kernel", "emit_kernel", "emit_map_kernel", "tick_kernel")
 
 
 def main():

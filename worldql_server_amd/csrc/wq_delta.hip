@@ -208,17 +208,20 @@ __global__ __launch_bounds__(kBlock) void k_delta_stats(const uint64_t* __restri
 constexpr int kWin = 256;        // ops per window (a bucket's ops are taken in op-order windows)
 constexpr uint32_t kInlineOnly = 0xFFFFFFFEu;  // a round cube's new list fits the record: no list write
 constexpr int kLaneList = 256;         // old lists longer than this go to the wave path
-constexpr uint32_t kRoundWords = 1024;  // a round stages at most this many old-list words (and 64 cubes)
-constexpr uint32_t kWaveList = kRoundWords;  // the wave path stages lists up to this in LDS
+// RW (the bucket kernel's template argument): a round stages at most RW old-list words (and 64
+// cubes), and the wave path stages lists of up to RW words in LDS. 1024 (16 KB of LDS per wave, 155
+// VGPRs: 10 waves per CU) or 256 (11.2 KB, 119 VGPRs: 14 waves per CU), chosen per batch from the
+// table's mean list length (table_apply_delta below).
 
 __device__ __forceinline__ uint32_t grown(uint32_t n) { return n + n / 2 + 4; }
 
+template <uint32_t RW>
 struct BucketLds {
     uint64_t op[kWin];              // the window's ops, sorted: slot_lo << 48 | peer << 16 | pos << 8 | kind
-    uint32_t lst[kRoundWords];      // a round's staged old lists (flat), or the wave path's one list
+    uint32_t lst[RW];      // a round's staged old lists (flat), or the wave path's one list
     union {
         struct {                    // a round
-            uint16_t wf[kRoundWords];  // staged word: bit 15 removed, bits 9-14 its cube in the round, 0-8 adds placed right before it
+            uint16_t wf[RW];  // staged word: bit 15 removed, bits 9-14 its cube in the round, 0-8 adds placed right before it
             uint8_t fl[kWin];          // per op: 1 add / 2 remove
             uint16_t at[kWin];         // per op: #old peers below it
             uint16_t pa[kWin + 1];     // exclusive prefix of add flags over the round's ops
@@ -236,8 +239,8 @@ struct BucketLds {
     uint32_t cslot[64];             // round: per cube, its record slot
     uint16_t cR[64];                // round: per cube, removed staged words before its first word
     uint16_t cA[64];                // round: per cube, adds placed before its first word
-    uint64_t smask[kRoundWords / 64];  // round: bit x = staged word x starts a cube's list
-    uint16_t mcum[kRoundWords / 64];   // round: list starts in the mask words before this one
+    uint64_t smask[RW / 64];  // round: bit x = staged word x starts a cube's list
+    uint16_t mcum[RW / 64];   // round: list starts in the mask words before this one
     uint8_t su[64];                 // round: the cubes with staged words, in order
     uint64_t bigm[kWin / 64];       // window: cubes (cs index) the wave path takes
     uint16_t cs[kWin + 1];          // cube starts in op[]
@@ -245,7 +248,8 @@ struct BucketLds {
 };
 
 // The round cube owning staged word x (the last list start at or before x).
-__device__ __forceinline__ uint32_t owner_of(const BucketLds& sm, uint32_t x) {
+template <uint32_t RW>
+__device__ __forceinline__ uint32_t owner_of(const BucketLds<RW>& sm, uint32_t x) {
     const uint32_t j = x >> 6;
     const uint64_t upto = (2ull << (x & 63)) - 1ull;  // bits 0..x & 63 (all ones for bit 63)
     return sm.su[sm.mcum[j] + (uint32_t)__popcll(sm.smask[j] & upto) - 1];
@@ -521,8 +525,9 @@ __device__ __forceinline__ uint32_t bump_alloc(const BucketArgs& a, uint32_t wan
     return (uint32_t)(a.list_base + d);
 }
 
+template <uint32_t RW>
 __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
-    __shared__ BucketLds sm;
+    __shared__ BucketLds<RW> sm;
     const uint32_t flags = a.status->flags;
     if (flags & 3u) return;  // an op without a record: nothing applied, the rebuild takes the batch
     const int lane = threadIdx.x;
@@ -627,8 +632,8 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
             bool isbig = act && oc > (uint32_t)kLaneList;
             uint32_t oc_st = isbig ? 0u : oc;
             const uint32_t incl = wave_incl_scan_dpp(oc_st);
-            // the round: the cubes whose staged words fit kRoundWords (at least one: oc <= kLaneList)
-            n_round = (uint32_t)__popcll(__ballot(act && incl <= kRoundWords));
+            // the round: the cubes whose staged words fit RW (at least one: oc <= kLaneList)
+            n_round = (uint32_t)__popcll(__ballot(act && incl <= RW));
             act = act && (uint32_t)lane < n_round;
             isbig = isbig && act;
             oc_st = act ? oc_st : 0u;
@@ -642,7 +647,7 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                 sm.cslot[lane] = slot;
             }
             // owner map: a bit at each staged list's first word, the cubes with words in order
-            if (lane < (int)(kRoundWords / 64)) sm.smask[lane] = 0;
+            if (lane < (int)(RW / 64)) sm.smask[lane] = 0;
             wave_lds_sync();
             {
                 const bool has = oc_st > 0;  // (implies act)
@@ -654,24 +659,24 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
             }
             wave_lds_sync();
             {
-                const uint32_t pc = lane < (int)(kRoundWords / 64) ? (uint32_t)__popcll(sm.smask[lane]) : 0u;
+                const uint32_t pc = lane < (int)(RW / 64) ? (uint32_t)__popcll(sm.smask[lane]) : 0u;
                 const uint32_t ic = wave_incl_scan_dpp(pc);
-                if (lane < (int)(kRoundWords / 64)) sm.mcum[lane] = (uint16_t)(ic - pc);
+                if (lane < (int)(RW / 64)) sm.mcum[lane] = (uint16_t)(ic - pc);
             }
             wave_lds_sync();
             WQ_STAMP(2);
             // stage the round's old lists flat: all of the round's loads in flight at once
-            // (T <= kRoundWords = 16 per lane)
+            // (T <= RW: RW / 64 per lane)
             {
                 // owners and source addresses first (LDS only), then every global load: the
                 // sources are global memory (record inline words or `list`), so they are read as
                 // such — a flat load would also count in lgkmcnt, and each LDS wait would then wait
                 // for the loads issued before it
                 typedef const __attribute__((address_space(1))) uint32_t* gptr;
-                uint32_t val[kRoundWords / 64];
-                uint64_t src[kRoundWords / 64];
+                uint32_t val[RW / 64];
+                uint64_t src[RW / 64];
 #pragma unroll
-                for (int r = 0; r < (int)(kRoundWords / 64); ++r) {
+                for (int r = 0; r < (int)(RW / 64); ++r) {
                     const uint32_t x = r * 64 + lane;
                     src[r] = 0;
                     if (x < T) {
@@ -681,12 +686,12 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                     }
                 }
 #pragma unroll
-                for (int r = 0; r < (int)(kRoundWords / 64); ++r) {
+                for (int r = 0; r < (int)(RW / 64); ++r) {
                     const uint32_t x = r * 64 + lane;
                     val[r] = x < T ? *reinterpret_cast<gptr>(src[r]) : 0u;
                 }
 #pragma unroll
-                for (int r = 0; r < (int)(kRoundWords / 64); ++r) {
+                for (int r = 0; r < (int)(RW / 64); ++r) {
                     const uint32_t x = r * 64 + lane;
                     if (x < T) sm.lst[x] = val[r];
                 }
@@ -783,7 +788,7 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                     for (int r = 0; r < NG; ++r) {  // the chunks' mark words and list-start masks at once
                         const uint32_t x = g0 + r * 64 + lane;
                         wv[r] = x < T ? (uint32_t)sm.u.r.wf[x] : 0u;
-                        sm_m[r] = sm.smask[(x >> 6) < kRoundWords / 64 ? (x >> 6) : 0u];
+                        sm_m[r] = sm.smask[(x >> 6) < RW / 64 ? (x >> 6) : 0u];
                     }
 #pragma unroll
                     for (int r = 0; r < NG; ++r) {
@@ -814,7 +819,7 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                         const uint32_t x = g0 + r * 64 + lane;
                         const uint32_t u = (aex[r] >> 25) & 0x3Fu;  // (0 past T)
                         cd[r] = sm.cdst[u];
-                        cy[r] = sm.lst[x < (uint32_t)kRoundWords ? x : 0u];
+                        cy[r] = sm.lst[x < (uint32_t)RW ? x : 0u];
                         cp[r] = sm.cpre[u];
                         cq[r] = sm.cR[u];
                         cz[r] = sm.cA[u];
@@ -874,7 +879,7 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
             Record* rec = a.tb.recs + slot;
             const uint4 h0 = reinterpret_cast<const uint4*>(rec)[0];
             const uint32_t oc = h0.z, off = h0.w, cap = reinterpret_cast<const uint32_t*>(rec)[6];
-            const bool staged = oc <= kWaveList;
+            const bool staged = oc <= RW;
             const uint32_t* G = L + off + 1;
             if (staged)
                 for (uint32_t i = lane; i < oc; i += 64) sm.lst[i] = G[i];
@@ -1310,7 +1315,17 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     // waves (0.254). WQ_DELTA_BPW overrides (diagnostics, tools/delta_bpw.sh).
     static const int bpw_env = getenv("WQ_DELTA_BPW") ? std::max(1, atoi(getenv("WQ_DELTA_BPW"))) : 0;
     const uint32_t bpw = bpw_env ? (uint32_t)bpw_env : (NBr >= 4096 ? 2u : 1u);
-    hipLaunchKernelGGL(k_delta_bucket, dim3((NBr + bpw - 1) / bpw), dim3(64), 0, s, ba);
+    // Round words: 256 while the table's lists average <= 20 peers (C5, ~13: update 0.718 -> 0.680 ms
+    // on one box — the higher occupancy outweighs the extra rounds), 1024 above (C4, ~34: 0.189 ms
+    // against 0.237 at 256 and 0.202 at 512; profiles/r06_churn_round_words_ab.json). The counts
+    // lag one batch (folded in by the next call), which a mean does not notice. WQ_ROUND_WORDS
+    // (256 / 1024) overrides.
+    static const int rw_env = getenv("WQ_ROUND_WORDS") ? atoi(getenv("WQ_ROUND_WORDS")) : 0;
+    const bool short_lists = rw_env ? rw_env <= 256 : h->st.n <= 20ull * std::max<uint64_t>(t.n_cubes, 1);
+    if (short_lists)
+        hipLaunchKernelGGL(k_delta_bucket<256>, dim3((NBr + bpw - 1) / bpw), dim3(64), 0, s, ba);
+    else
+        hipLaunchKernelGGL(k_delta_bucket<1024>, dim3((NBr + bpw - 1) / bpw), dim3(64), 0, s, ba);
     WQ_HIP(h, hipGetLastError());
     if (ba.stamps) {  // diagnostics: mean cycles per bucket and phase
         std::vector<uint64_t> st((size_t)NBr * 16);
