@@ -528,6 +528,7 @@ __device__ __forceinline__ uint32_t bump_alloc(const BucketArgs& a, uint32_t wan
 template <uint32_t RW>
 __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
     __shared__ BucketLds<RW> sm;
+    constexpr uint32_t kLL = RW < (uint32_t)kLaneList ? RW : (uint32_t)kLaneList;  // lane-path lists: <= kLL peers
     const uint32_t flags = a.status->flags;
     if (flags & 3u) return;  // an op without a record: nothing applied, the rebuild takes the batch
     const int lane = threadIdx.x;
@@ -629,7 +630,7 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
             }
             const uint64_t src_base = reinterpret_cast<uint64_t>(
                 oc <= (uint32_t)kInline ? reinterpret_cast<const uint32_t*>(a.tb.recs + slot) + kInlineWord0 : L + off + 1);
-            bool isbig = act && oc > (uint32_t)kLaneList;
+            bool isbig = act && oc > kLL;
             uint32_t oc_st = isbig ? 0u : oc;
             const uint32_t incl = wave_incl_scan_dpp(oc_st);
             // the round: the cubes whose staged words fit RW (at least one: oc <= kLaneList)
@@ -710,7 +711,7 @@ __global__ __launch_bounds__(64) void k_delta_bucket(BucketArgs a) {
                     uint8_t f = 0;
                     uint32_t l2 = 0;
                     if (last) {  // (a wave-path cube stages nothing: n0 = 0, and its cdst is kNone)
-                        l2 = lds_lower_bound_fixed<kLaneList>(sm.lst + b0, n0, pp);
+                        l2 = lds_lower_bound_fixed<kLL>(sm.lst + b0, n0, pp);
                         const bool present = l2 < n0 && sm.lst[b0 + l2] == pp;
                         const uint32_t wpos = b0 + l2;
                         uint32_t* wf32 = reinterpret_cast<uint32_t*>(sm.u.r.wf) + (wpos >> 1);
@@ -1317,7 +1318,8 @@ int table_apply_delta(wq_router* h, size_t n_ops, bool* applied) {
     const uint32_t bpw = bpw_env ? (uint32_t)bpw_env : (NBr >= 4096 ? 2u : 1u);
     // Round words: 256 while the table's lists average <= 20 peers (C5, ~13: update 0.718 -> 0.680 ms
     // on one box — the higher occupancy outweighs the extra rounds), 1024 above (C4, ~34: 0.189 ms
-    // against 0.237 at 256 and 0.202 at 512; profiles/r06_churn_round_words_ab.json). The counts
+    // against 0.237 at 256 and 0.202 at 512; profiles/r06_churn_round_words_ab.json). 128 (15 waves
+    // per CU) was slower at C5: 0.758-0.770 ms. The counts
     // lag one batch (folded in by the next call), which a mean does not notice. WQ_ROUND_WORDS
     // (256 / 1024) overrides.
     static const int rw_env = getenv("WQ_ROUND_WORDS") ? atoi(getenv("WQ_ROUND_WORDS")) : 0;
