@@ -22,6 +22,7 @@ struct DevBuf {
     // hipExtMallocWithFlags flags for the next allocation (0: hipMalloc); a flagged allocation that
     // fails falls back to hipMalloc
     unsigned flags = 0;
+    bool flagged = false;  // the current allocation came from hipExtMallocWithFlags
     hipError_t ensure(size_t need) {
         if (need <= bytes) return hipSuccess;
         if (p) {
@@ -32,6 +33,7 @@ struct DevBuf {
         }
         size_t cap = need < 4096 ? 4096 : need + need / 4;
         hipError_t e = flags ? hipExtMallocWithFlags(&p, cap, flags) : hipMalloc(&p, cap);
+        flagged = flags && e == hipSuccess;
         if (e != hipSuccess && flags) {
             (void)hipGetLastError();
             p = nullptr;

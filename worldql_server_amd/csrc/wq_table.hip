@@ -552,8 +552,9 @@ int table_rebuild_derived(wq_router* h) {
     // WQ_CONTIG=1: the record table as one hipDeviceMallocContiguous allocation (hipMalloc if that
     // fails). Measured equal to hipMalloc on a box in the fast emit mode (r06_record_cap_ab.json).
     static const bool contig = getenv("WQ_CONTIG") && atoi(getenv("WQ_CONTIG")) != 0;
-    t.recs.flags = contig ? hipDeviceMallocContiguous : 0u;
+    t.recs.flags = t.hdr.flags = contig ? hipDeviceMallocContiguous : 0u;
     WQ_ALLOC(h, t.recs, rcap * sizeof(Record));
+    if (contig) fprintf(stderr, "wq: WQ_CONTIG record table %.2f GB contiguous: %d\n", t.recs.bytes / 1e9, (int)t.recs.flagged);
     WQ_ALLOC(h, t.rclaim, rcap * 4);
     WQ_HIP(h, hipMemsetAsync(t.recs.p, 0, rcap * sizeof(Record), s));
     WQ_HIP(h, hipMemsetAsync(t.rclaim.p, 0, rcap * 4, s));
