@@ -152,7 +152,8 @@ __device__ __forceinline__ void count_rows(const RouteIn& in, const TableView& t
         // lanes with nothing to probe read a dummy line spread by message index (never one shared
         // line: a chip-wide hot line serialises on its L2 channel). With compact headers the probe
         // walks the header table; the match then hands over the record slot (below)
-        sl[i] = reg ? (uint32_t)slot_of(rec_hash(pk[i], ext[i]) & tv.hash_mask, chdr ? tv.hdr_shift : tv.rec_shift)
+        sl[i] = reg ? (uint32_t)(chdr ? hdr_home(pk[i], ext[i], tv.hash_mask, tv.hdr_shift, tv.hdr_blk)
+                                      : slot_of(rec_hash(pk[i], ext[i]) & tv.hash_mask, tv.rec_shift))
                     : (m & (uint32_t)(chdr ? tv.hdr_mask : tv.rec_mask));
         via_rec[i] = valid && reg;
         st[i] = via_rec[i] ? kStProbe : kStDone;

@@ -208,6 +208,16 @@ __host__ __device__ __forceinline__ uint64_t rec_hash(uint64_t pk, uint32_t ext)
 // Slot index from the hash's high bits. shift = 64 - log2(capacity), capacity >= 1024.
 __device__ __forceinline__ uint64_t slot_of(uint64_t h, int shift) { return h >> shift; }
 
+// Home slot of a cube in the compact header table. blk = 0: the cube's own hash. blk = 4 / 8: the
+// cube's 2 x 2 (y, z) / 2 x 2 x 2 block hashes to a group of blk consecutive slots and the cube takes
+// slot (x, y, z low bits) of it, so neighbouring cubes share header lines (4 32-B headers per line).
+__device__ __forceinline__ uint64_t hdr_home(uint64_t pk, uint32_t ext, uint64_t hash_mask, int shift, uint32_t blk) {
+    if (!blk) return slot_of(rec_hash(pk, ext) & hash_mask, shift);
+    const uint64_t sub = ((pk >> 48) & 1ull) << 2 | ((pk >> 24) & 1ull) << 1 | (pk & 1ull);
+    const uint64_t low = blk == 8 ? (1ull << 48) | (1ull << 24) | 1ull : (1ull << 24) | 1ull;
+    return (slot_of(rec_hash(pk & ~low, ext) & hash_mask, shift) & ~(uint64_t)(blk - 1)) | (sub & (blk - 1));
+}
+
 struct SlotView {
     int64_t k0, k1, k2;
     uint32_t world, off;
@@ -272,6 +282,7 @@ struct TableView {
     // (the record's cap, which no tick reads). hdr_mask == 0: header i is record i's.
     uint64_t hdr_mask = 0;
     int hdr_shift = 64;
+    uint32_t hdr_blk = 0;  // hdr_home's block grouping (0: per-cube hashing)
 };
 
 // ---- per-peer boxes: a fast "certainly not subscribed" for long lists ---------------------

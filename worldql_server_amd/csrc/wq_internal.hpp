@@ -89,6 +89,7 @@ struct Table {
     // (header i = record i's first 32 bytes, WQ_HDR_COMPACT=0)
     uint64_t hdr_cap = 0;
     int hdr_shift = 64;
+    uint32_t hdr_blk = 0;  // wq_device.hpp hdr_home (WQ_HDR_BLOCK)
 };
 
 // The last incremental batch (wq_delta.hip), in flight: its status and stat deltas arrive in
@@ -243,6 +244,7 @@ inline TableView table_view(const wq_router* h) {
     v.hdr = h->tab.hdr_ok ? h->tab.hdr.as<uint4>() : nullptr;
     v.hdr_mask = h->tab.hdr_cap ? h->tab.hdr_cap - 1 : 0;
     v.hdr_shift = h->tab.hdr_shift;
+    v.hdr_blk = h->tab.hdr_blk;
     return v;
 }
 // Sticky {error OR, overflow OR} words of every route / global call since the last

@@ -440,13 +440,13 @@ int table_remove_peers(wq_router* h, const uint64_t* keys, size_t n_rm) {
 // slot of its probe run in the header table by a CAS on the header's ext word (each cube is inserted
 // once, so a claimed slot is simply passed), then writes {pk, count, list_off | sig, record slot}.
 __global__ void k_hdr_compact(const uint4* __restrict__ recs, uint64_t n, uint4* __restrict__ hdr, uint64_t hmask,
-                              int hshift, uint64_t hash_mask) {
+                              int hshift, uint64_t hash_mask, uint32_t blk) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const uint4 a = recs[8 * i], b = recs[8 * i + 1];
     if (b.w == 0) return;  // an empty record slot
     const uint64_t pk = ((uint64_t)a.y << 32) | a.x;
-    uint64_t s = slot_of(rec_hash(pk, b.w) & hash_mask, hshift);
+    uint64_t s = hdr_home(pk, b.w, hash_mask, hshift, blk);
     for (;;) {
         uint32_t* ext_word = reinterpret_cast<uint32_t*>(hdr + 2 * s + 1) + 3;
         if (atomicCAS(ext_word, 0u, b.w) == 0u) break;
@@ -591,6 +591,7 @@ int table_rebuild_derived(wq_router* h) {
     t.hdr_ok = false;
     t.hdr_cap = 0;
     t.hdr_shift = 64;
+    t.hdr_blk = 0;
     static const bool want_hdr = !getenv("WQ_HDR") || atoi(getenv("WQ_HDR")) != 0;
     // compact headers (default): their own table of >= WQ_HDR_SLOTS header slots per cube (default 4:
     // load <= 1/4, 1/8 after the power-of-two rounding of C3's 8.56M cubes; C3 count 344.5-345.2 us
@@ -609,8 +610,12 @@ int table_rebuild_derived(wq_router* h) {
         WQ_HIP(h, hipMemsetAsync(t.hdr.p, 0, hcap * 32, s));
         t.hdr_cap = hcap;
         t.hdr_shift = 64 - log2h;
+        // WQ_HDR_BLOCK = 4 / 8: neighbouring cubes' headers grouped per 2 x 2 / 2 x 2 x 2 block
+        // (wq_device.hpp hdr_home; round-5 verdict item 6)
+        static const uint32_t blk_env = getenv("WQ_HDR_BLOCK") ? (uint32_t)atoi(getenv("WQ_HDR_BLOCK")) : 0u;
+        t.hdr_blk = blk_env == 4 || blk_env == 8 ? blk_env : 0u;
         hipLaunchKernelGGL(k_hdr_compact, dim3(grid_for(rcap)), dim3(kBlock), 0, s, t.recs.as<uint4>(), rcap,
-                           t.hdr.as<uint4>(), hcap - 1, t.hdr_shift, h->hash_mask);
+                           t.hdr.as<uint4>(), hcap - 1, t.hdr_shift, h->hash_mask, t.hdr_blk);
         t.hdr_ok = true;
     } else if (want_hdr) {
         WQ_ALLOC(h, t.hdr, rcap * 32);
