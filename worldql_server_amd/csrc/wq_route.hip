@@ -193,10 +193,14 @@ int launch_route(wq_router* h, const double* d_pos, const int64_t* d_keys, const
         tp.health = route_health(h);
         tp.stamps = rw.stamps;
         tp.n_tiles = (uint32_t)nb;
-        tp.out_cnt = rw.out;
+        // the caller's counters: a copy launch after the tick by default. The tick's last block can
+        // write them itself (WQ_TICK_OUTCNT=1), one launch fewer, but its extra tail made C2 slower:
+        // 62.8-63.4 against 62.5-62.8 us, alternating on one box (profiles/r06_tick_outcnt_ab.json)
+        static const bool outcnt_in_tick = getenv("WQ_TICK_OUTCNT") && atoi(getenv("WQ_TICK_OUTCNT")) != 0;
+        tp.out_cnt = outcnt_in_tick ? rw.out : nullptr;
         cfg.tick(tp, s, (unsigned)nb);
         WQ_HIP(h, hipGetLastError());
-        rw.out_done = rw.out != nullptr;
+        rw.out_done = tp.out_cnt != nullptr;
         if (pr.enabled) {
             WQ_HIP(h, hipEventRecord(pr.stop[pr.used], s));
             pr.used++;
